@@ -1,0 +1,29 @@
+# Native build: libthrs.so (HIP kernels for gfx950 + the C-ABI), the C++ test
+# binary, and the CPU oracle.  Used by __graft_entry__.build().
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+HIPFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Iinclude -Wall -Wno-unused-result
+PKG := tinyhipradixsort_amd
+KSRC := $(PKG)/csrc/thrs_capi.hip $(PKG)/csrc/thrs_kernels.hpp include/thrs/thrs_capi.h
+
+all: $(PKG)/libthrs.so $(PKG)/libthrs_testutil.so tests/cpp/unittest_thrs examples/helloworld oracle
+
+$(PKG)/libthrs.so: $(KSRC)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(PKG)/csrc/thrs_capi.hip
+
+$(PKG)/libthrs_testutil.so: $(PKG)/csrc/thrs_testutil.hip $(PKG)/csrc/thrs_kernels.hpp
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(PKG)/csrc/thrs_testutil.hip
+
+CXX ?= g++
+tests/cpp/unittest_thrs: tests/cpp/unittest_thrs.cpp include/thrs/tinyhipradixsort.hpp include/thrs/fpKey.hpp $(PKG)/libthrs.so
+	$(CXX) -O2 -std=c++17 -fopenmp -Iinclude -o $@ $< -L$(PKG) -lthrs -Wl,-rpath,'$$ORIGIN/../../$(PKG)'
+
+examples/helloworld: examples/helloworld.cpp include/thrs/tinyhipradixsort.hpp $(PKG)/libthrs.so
+	$(CXX) -O2 -std=c++17 -Iinclude -o $@ $< -L$(PKG) -lthrs -Wl,-rpath,'$$ORIGIN/../$(PKG)'
+
+oracle:
+	$(MAKE) -s -C oracle
+
+clean:
+	rm -f $(PKG)/*.so oracle/liboracle.so tests/cpp/unittest_thrs examples/helloworld
+.PHONY: all clean oracle

@@ -1,0 +1,124 @@
+/* thrs_capi.h -- the C-ABI drop-in boundary of libthrs.so (MI355X / gfx950).
+ *
+ * Plain pointers, sizes and ints only; no C++ or torch types.  Every entry
+ * point replaces one piece of the reference's host API
+ * (/root/reference/tinyhipradixsort.hpp), cited per function.  The header-only
+ * C++ API in <thrs/tinyhipradixsort.hpp> is a thin wrapper over these, and the
+ * Python mirror (tinyhipradixsort_amd) binds them with ctypes.
+ *
+ * Conventions
+ *   - Return value: THRS_SUCCESS (0) or a negative thrs_status; never aborts.
+ *   - Streams are HIP streams (hipStream_t, ABI-identical to the reference's
+ *     oroStream on the HIP backend); 0 means the null stream.
+ *   - Sorting is asynchronous on the stream; the caller synchronises.
+ *   - All per-call scratch lives in the caller's temporary buffer, so two
+ *     sorts on distinct temporary buffers may run concurrently.
+ */
+#ifndef THRS_CAPI_H
+#define THRS_CAPI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#ifndef THRS_HIP_STREAM_DECLARED
+#define THRS_HIP_STREAM_DECLARED
+typedef struct ihipStream_t* hipStream_t; /* identical to HIP's own typedef */
+#endif
+
+#define THRS_ABI_VERSION 1
+
+typedef enum thrs_status {
+  THRS_SUCCESS = 0,
+  THRS_ERROR_INVALID_VALUE = -1,   /* bad enum, null pointer, negative bits   */
+  THRS_ERROR_BIT_RANGE = -2,       /* (endBits-startBits)%8 != 0 (hpp:856)    */
+  THRS_ERROR_HIP = -3,             /* a HIP runtime call failed               */
+  THRS_ERROR_OUT_OF_MEMORY = -4,   /* thrs_malloc failed                      */
+  THRS_ERROR_LOOKBACK_TIMEOUT = -5 /* device look-back spin bound hit         */
+} thrs_status;
+
+/* == thrs::KeyType / ValueType / SortOrder (tinyhipradixsort.hpp:638-683) */
+enum { THRS_KEY_U32 = 0, THRS_KEY_U64 = 1, THRS_KEY_F32 = 2, THRS_KEY_F64 = 3 };
+enum { THRS_VALUE_U32 = 0, THRS_VALUE_U64 = 1, THRS_VALUE_U128 = 2 };
+enum { THRS_ORDER_ASCENDING = 0, THRS_ORDER_DESCENDING = 1 };
+
+/* == RadixSort::Config (tinyhipradixsort.hpp:697-749) */
+typedef struct thrs_config {
+  int32_t keyIs16byteAligned; /* hint only: alignment is re-checked per call */
+  int32_t keyType;            /* THRS_KEY_*   */
+  int32_t valueType;          /* THRS_VALUE_* */
+  int32_t sortOrder;          /* THRS_ORDER_* */
+} thrs_config;
+
+/* == RadixSort::TemporaryBufferDef (tinyhipradixsort.hpp:806-832).
+ * Layout of the caller's temporary buffer: [pSumBuffer][keyOut][valueOut].
+ * pSumBuffer is this implementation's scratch (histograms, digit bases, tile
+ * counters, look-back status words); keyOut/valueOut are the ping-pong
+ * partners of the caller's key/value buffers. */
+typedef struct thrs_temp_def {
+  uint64_t pSumBuffer;
+  uint64_t keyOutBuffer;
+  uint64_t valueOutBuffer;
+} thrs_temp_def;
+
+/* ABI version of the loaded library (== THRS_ABI_VERSION). */
+int thrs_abi_version(void);
+
+/* Human-readable name of a thrs_status. */
+const char* thrs_status_string(int status);
+
+/* == bytesOf(KeyType) / bytesOf(ValueType) (tinyhipradixsort.hpp:651-678);
+ * 0 for an invalid enum. */
+uint64_t thrs_key_bytes(int keyType);
+uint64_t thrs_value_bytes(int valueType);
+
+/* == RadixSort::getTemporaryBufferBytes (tinyhipradixsort.hpp:833-843). */
+int thrs_get_temporary_buffer_bytes(const thrs_config* config, uint32_t numberOfMaxInputs, thrs_temp_def* out);
+
+/* == RadixSort::sortKeys (tinyhipradixsort.hpp:845-848).  Sorts the 8-bit
+ * digits of getKeyBits(key) (XOR all-ones when descending) covering
+ * [startBits, endBits), least significant first; result in inputKeyBuffer.
+ * startBits >= endBits is a no-op; numberOfInputs == 0 is a no-op. */
+int thrs_sort_keys(const thrs_config* config, void* inputKeyBuffer, uint32_t numberOfInputs, void* temporaryBuffer,
+                   int startBits, int endBits, hipStream_t stream);
+
+/* == RadixSort::sortPairs (tinyhipradixsort.hpp:849-852).  Stable: equal keys
+ * keep their input order, so values follow their keys bit-exactly. */
+int thrs_sort_pairs(const thrs_config* config, void* inputKeyBuffer, void* inputValueBuffer, uint32_t numberOfInputs,
+                    void* temporaryBuffer, int startBits, int endBits, hipStream_t stream);
+
+/* Synchronising debug check: THRS_ERROR_LOOKBACK_TIMEOUT if any look-back of
+ * the last sort that used `temporaryBuffer` gave up its bounded spin (no
+ * reference counterpart; the reference would hang instead). */
+int thrs_check_device_error(void* temporaryBuffer, hipStream_t stream);
+
+/* Kernel timing for benchmarks (no reference counterpart; the reference's
+ * per-kernel stopwatches are commented out at tinyhipradixsort.hpp:881-928).
+ * While enabled, every sort records hipEvents on ITS stream around the
+ * histogram+scan launches and around each per-digit pass launch.
+ * thrs_profile_read synchronises those events and returns the summed
+ * milliseconds and launch counts since the last enable.  Off by default; not
+ * for use under stream capture. */
+int thrs_profile_enable(int enable);
+int thrs_profile_read(double* histMs, int* histLaunches, double* passMs, int* passLaunches);
+
+/* == thrs::Buffer (tinyhipradixsort.hpp:501-528): hipMalloc(max(bytes,1)). */
+int thrs_malloc(void** ptr, int64_t bytes);
+int thrs_free(void* ptr);
+
+/* Helpers the header-only API and ported tests use in place of the
+ * reference's Orochi calls (oroMemcpyHtoDAsync / oroMemcpyDtoH /
+ * oroStreamSynchronize / oroStreamCreate, unittest.cpp:55, 143-152). */
+int thrs_memcpy_htod_async(void* dst, const void* src, uint64_t bytes, hipStream_t stream);
+int thrs_memcpy_dtoh(void* dst, const void* src, uint64_t bytes);
+int thrs_memcpy_dtod_async(void* dst, const void* src, uint64_t bytes, hipStream_t stream);
+int thrs_stream_create(hipStream_t* stream);
+int thrs_stream_destroy(hipStream_t stream);
+int thrs_stream_synchronize(hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* THRS_CAPI_H */

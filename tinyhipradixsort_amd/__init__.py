@@ -1,0 +1,298 @@
+"""tinyhipradixsort_amd -- MI355X-native LSD radix sort, Python host mirror.
+
+Mirrors the reference's host API (/root/reference/tinyhipradixsort.hpp) name
+for name, over the C-ABI of the in-tree ``libthrs.so`` (declared in
+``include/thrs/thrs_capi.h``):
+
+    KeyType / ValueType / SortOrder / bytesOf          (hpp:638-692)
+    Buffer                                             (hpp:501-528)
+    RadixSort.Config + configureWithKey(KeyT)
+                     + configureWithKeyPair(KeyT, V)  (hpp:697-749)
+    RadixSort(extraArgs, config)                       (hpp:751-804)
+    TemporaryBufferDef / getTemporaryBufferBytes       (hpp:806-843)
+    sortKeys / sortPairs                               (hpp:845-852)
+
+Device buffers may be passed as torch tensors (``.data_ptr()`` is used) or as
+integer device addresses; streams as ``torch.cuda.Stream``, an integer HIP
+stream handle, or ``None`` for torch's current stream.  Errors raise
+``ThrsError`` (the reference's THRS_ASSERT -> __debugbreak).
+
+There is no CPU fallback: if ``libthrs.so`` is missing the import of the sort
+entry points raises.  The CPU oracle under ``oracle/`` is test
+infrastructure and is never imported from here.
+"""
+from __future__ import annotations
+
+import ctypes
+import enum
+import os
+from dataclasses import dataclass
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libthrs.so")
+TESTUTIL_PATH = os.path.join(_HERE, "libthrs_testutil.so")
+ABI_VERSION = 1
+
+__all__ = ["KeyType", "ValueType", "SortOrder", "bytesOf", "div_round_up64", "next_multiple64", "Buffer",
+           "RadixSort", "ThrsError", "lib", "LIB_PATH"]
+
+
+class ThrsError(RuntimeError):
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"{msg} (status {status})")
+        self.status = status
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """The in-tree libthrs.so.  Raises if it has not been built -- never
+    substitutes anything else."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} is missing: run `make` (or __graft_entry__.build()) first")
+        L = ctypes.CDLL(LIB_PATH)
+        vp, u32, u64, i32, i64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int, ctypes.c_int64
+        L.thrs_abi_version.restype = i32
+        L.thrs_status_string.argtypes = [i32]
+        L.thrs_status_string.restype = ctypes.c_char_p
+        L.thrs_key_bytes.argtypes = [i32]
+        L.thrs_key_bytes.restype = u64
+        L.thrs_value_bytes.argtypes = [i32]
+        L.thrs_value_bytes.restype = u64
+        L.thrs_get_temporary_buffer_bytes.argtypes = [ctypes.POINTER(_CConfig), u32, ctypes.POINTER(_CTempDef)]
+        L.thrs_sort_keys.argtypes = [ctypes.POINTER(_CConfig), vp, u32, vp, i32, i32, vp]
+        L.thrs_sort_pairs.argtypes = [ctypes.POINTER(_CConfig), vp, vp, u32, vp, i32, i32, vp]
+        L.thrs_check_device_error.argtypes = [vp, vp]
+        L.thrs_malloc.argtypes = [ctypes.POINTER(vp), i64]
+        L.thrs_free.argtypes = [vp]
+        L.thrs_memcpy_htod_async.argtypes = [vp, vp, u64, vp]
+        L.thrs_memcpy_dtoh.argtypes = [vp, vp, u64]
+        L.thrs_memcpy_dtod_async.argtypes = [vp, vp, u64, vp]
+        L.thrs_stream_create.argtypes = [ctypes.POINTER(vp)]
+        L.thrs_stream_destroy.argtypes = [vp]
+        L.thrs_stream_synchronize.argtypes = [vp]
+        L.thrs_profile_enable.argtypes = [i32]
+        L.thrs_profile_read.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32),
+                                        ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32)]
+        for f in ("thrs_profile_enable", "thrs_profile_read", "thrs_get_temporary_buffer_bytes", "thrs_sort_keys", "thrs_sort_pairs", "thrs_check_device_error",
+                  "thrs_malloc", "thrs_free", "thrs_memcpy_htod_async", "thrs_memcpy_dtoh", "thrs_memcpy_dtod_async",
+                  "thrs_stream_create", "thrs_stream_destroy", "thrs_stream_synchronize"):
+            getattr(L, f).restype = i32
+        if L.thrs_abi_version() != ABI_VERSION:
+            raise ImportError(f"libthrs ABI {L.thrs_abi_version()} != {ABI_VERSION}")
+        _lib = L
+    return _lib
+
+
+def _check(rc: int):
+    if rc != 0:
+        raise ThrsError(rc, lib().thrs_status_string(rc).decode())
+
+
+class _CConfig(ctypes.Structure):
+    _fields_ = [("keyIs16byteAligned", ctypes.c_int32), ("keyType", ctypes.c_int32),
+                ("valueType", ctypes.c_int32), ("sortOrder", ctypes.c_int32)]
+
+
+class _CTempDef(ctypes.Structure):
+    _fields_ = [("pSumBuffer", ctypes.c_uint64), ("keyOutBuffer", ctypes.c_uint64),
+                ("valueOutBuffer", ctypes.c_uint64)]
+
+
+class KeyType(enum.IntEnum):      # hpp:638-644
+    U32 = 0
+    U64 = 1
+    F32 = 2
+    F64 = 3
+
+
+class ValueType(enum.IntEnum):    # hpp:645-650
+    U32 = 0
+    U64 = 1
+    U128 = 2
+
+
+class SortOrder(enum.IntEnum):    # hpp:679-683
+    Ascending = 0
+    Descending = 1
+
+
+def bytesOf(t) -> int:            # hpp:651-678
+    if isinstance(t, KeyType):
+        return int(lib().thrs_key_bytes(int(t)))
+    if isinstance(t, ValueType):
+        return int(lib().thrs_value_bytes(int(t)))
+    raise ThrsError(-1, "bytesOf: not a KeyType/ValueType")
+
+
+def div_round_up64(val: int, divisor: int) -> int:
+    return (val + divisor - 1) // divisor
+
+
+def next_multiple64(val: int, divisor: int) -> int:
+    return div_round_up64(val, divisor) * divisor
+
+
+def _ptr(x) -> int | None:
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    if hasattr(x, "data_ptr"):
+        return x.data_ptr()
+    if isinstance(x, Buffer):
+        return x.data()
+    raise TypeError(f"cannot take a device address of {type(x)}")
+
+
+def _stream(s) -> int | None:
+    if s is None:
+        import torch
+        return torch.cuda.current_stream().cuda_stream
+    if isinstance(s, int):
+        return s
+    if hasattr(s, "cuda_stream"):
+        return s.cuda_stream
+    raise TypeError(f"not a stream: {type(s)}")
+
+
+class Buffer:
+    """hpp:501-528 -- device allocation of max(bytes, 1) via thrs_malloc."""
+
+    def __init__(self, bytes_: int):
+        self._bytes = max(int(bytes_), 1)
+        p = ctypes.c_void_p()
+        _check(lib().thrs_malloc(ctypes.byref(p), self._bytes))
+        self._ptr = p.value
+
+    def bytes(self) -> int:
+        return self._bytes
+
+    def data(self) -> int:
+        return self._ptr
+
+    def __del__(self):
+        if getattr(self, "_ptr", None) and _lib is not None:
+            _lib.thrs_free(self._ptr)
+            self._ptr = None
+
+
+def _key_type_of(k) -> KeyType:
+    import numpy as np
+    try:
+        import torch
+        tmap = {torch.float32: KeyType.F32, torch.float64: KeyType.F64, torch.int32: KeyType.U32,
+                torch.int64: KeyType.U64, torch.uint32: KeyType.U32, torch.uint64: KeyType.U64}
+        if k in tmap:
+            return tmap[k]
+    except (ImportError, AttributeError):
+        pass
+    dt = np.dtype(k)
+    if dt == np.float32:
+        return KeyType.F32
+    if dt == np.float64:
+        return KeyType.F64
+    if dt.itemsize == 4:
+        return KeyType.U32
+    if dt.itemsize == 8:
+        return KeyType.U64
+    raise ThrsError(-1, f"configureWithKey: unsupported key type {k}")   # hpp:710 static_assert
+
+
+def _itemsize(v) -> int:
+    import numpy as np
+    if isinstance(v, int):
+        return v
+    try:
+        import torch
+        if isinstance(v, torch.dtype):
+            return torch.empty((), dtype=v).element_size()
+    except ImportError:
+        pass
+    return np.dtype(v).itemsize
+
+
+class RadixSort:
+    """hpp:694-948 over the C-ABI."""
+
+    @dataclass
+    class Config:                 # hpp:697-749
+        keyIs16byteAligned: bool = True
+        keyType: KeyType = KeyType.U32
+        valueType: ValueType = ValueType.U32
+        sortOrder: SortOrder = SortOrder.Ascending
+
+        def configureWithKey(self, key):
+            self.keyType = _key_type_of(key)
+
+        def configureWithKeyPair(self, key, value):
+            self.configureWithKey(key)
+            vb = _itemsize(value)
+            if vb not in (4, 8, 16):
+                raise ThrsError(-1, "configureWithKeyPair: value must be 4, 8 or 16 bytes")  # hpp:734
+            self.valueType = {4: ValueType.U32, 8: ValueType.U64, 16: ValueType.U128}[vb]
+
+    @dataclass
+    class TemporaryBufferDef:     # hpp:806-832
+        pSumBuffer: int
+        keyOutBuffer: int
+        valueOutBuffer: int
+
+        def getTemporaryBufferBytesForSortKeys(self) -> int:
+            return self.pSumBuffer + self.keyOutBuffer
+
+        def getTemporaryBufferBytesForSortPairs(self) -> int:
+            return self.pSumBuffer + self.keyOutBuffer + self.valueOutBuffer
+
+        def getPSumBuffer(self, p: int) -> int:
+            return p
+
+        def getOutputKeyBuffer(self, p: int) -> int:
+            return p + self.pSumBuffer
+
+        def getOutputValueBuffer(self, p: int) -> int:
+            return p + self.pSumBuffer + self.keyOutBuffer
+
+    def __init__(self, extraArgs=(), config: "RadixSort.Config | None" = None):
+        self.m_config = config if config is not None else RadixSort.Config()
+        lib()   # fail loudly here, like the reference's compile-time THRS_ASSERT (hpp:591)
+
+    def _c(self) -> _CConfig:
+        c = self.m_config
+        return _CConfig(int(bool(c.keyIs16byteAligned)), int(c.keyType), int(c.valueType), int(c.sortOrder))
+
+    def getTemporaryBufferBytes(self, numberOfMaxInputs: int) -> "RadixSort.TemporaryBufferDef":
+        d = _CTempDef()
+        _check(lib().thrs_get_temporary_buffer_bytes(ctypes.byref(self._c()), int(numberOfMaxInputs), ctypes.byref(d)))
+        return RadixSort.TemporaryBufferDef(d.pSumBuffer, d.keyOutBuffer, d.valueOutBuffer)
+
+    def sortKeys(self, inputKeyBuffer, numberOfInputs: int, temporaryBuffer, startBits: int, endBits: int,
+                 stream=None):
+        _check(lib().thrs_sort_keys(ctypes.byref(self._c()), _ptr(inputKeyBuffer), int(numberOfInputs),
+                                    _ptr(temporaryBuffer), int(startBits), int(endBits), _stream(stream)))
+
+    def sortPairs(self, inputKeyBuffer, inputValueBuffer, numberOfInputs: int, temporaryBuffer, startBits: int,
+                  endBits: int, stream=None):
+        _check(lib().thrs_sort_pairs(ctypes.byref(self._c()), _ptr(inputKeyBuffer), _ptr(inputValueBuffer),
+                                     int(numberOfInputs), _ptr(temporaryBuffer), int(startBits), int(endBits),
+                                     _stream(stream)))
+
+    def checkDeviceError(self, temporaryBuffer, stream=None):
+        """Synchronising: raises if a look-back spin bound was hit in the last sort."""
+        _check(lib().thrs_check_device_error(_ptr(temporaryBuffer), _stream(stream)))
+
+
+def profile_enable(on: bool = True):
+    """Start (and reset) / stop HIP-event timing of the sort kernels (bench only)."""
+    _check(lib().thrs_profile_enable(int(on)))
+
+
+def profile_read() -> dict:
+    """Synchronise recorded events; summed ms and launch counts since enable."""
+    h, p = ctypes.c_double(), ctypes.c_double()
+    nh, np_ = ctypes.c_int(), ctypes.c_int()
+    _check(lib().thrs_profile_read(ctypes.byref(h), ctypes.byref(nh), ctypes.byref(p), ctypes.byref(np_)))
+    return {"hist_ms": h.value, "hist_launches": nh.value, "pass_ms": p.value, "pass_launches": np_.value}

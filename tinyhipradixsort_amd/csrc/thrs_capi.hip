@@ -1,0 +1,361 @@
+// thrs_capi.hip -- host side of libthrs.so: the C-ABI declared in
+// include/thrs/thrs_capi.h, launching the gfx950 kernels of thrs_kernels.hpp.
+//
+// The pass loop follows RadixSort::sort (tinyhipradixsort.hpp:854-944): one
+// pass per bitLocation = startBits + 8i < endBits, ping-pong between the
+// caller's buffers and the keyOut/valueOut regions of the temporary buffer,
+// and a copy-back when the pass count is odd so the result always lands in the
+// caller's buffers.  Differences, all deliberate:
+//   * one histogram launch for all passes + one tiny scan, then ONE launch per
+//     pass (the reference launches blockCount + prefixSumExclusiveInplace +
+//     reorder per pass, :872-922);
+//   * the odd-pass copy is stream-ordered (hipMemcpyAsync on `stream`); the
+//     reference's oroMemcpyDtoD (:938-941) is not;
+//   * a pass whose bit location is at or past the key width reads only zero
+//     bits, is the identity permutation, and is skipped;
+//   * errors are returned, never __debugbreak (:14-15).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "thrs/thrs_capi.h"
+#include "thrs_kernels.hpp"
+
+using namespace thrs_dev;
+
+namespace {
+
+constexpr uint64_t kAlign = 256;
+constexpr uint64_t kHistOff = 0;                       // u32 [8][256]
+constexpr uint64_t kBaseOff = 8 * 256 * 4;             // u32 [8][256]
+constexpr uint64_t kCounterOff = 2 * 8 * 256 * 4;      // u32 [8]
+constexpr uint64_t kErrOff = kCounterOff + 8 * 4;      // u32
+constexpr uint64_t kHeaderBytes = 16640;               // 65 * 256
+
+inline uint64_t round_up(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
+
+inline bool valid_key(int k) { return k >= THRS_KEY_U32 && k <= THRS_KEY_F64; }
+inline bool valid_value(int v) { return v >= THRS_VALUE_U32 && v <= THRS_VALUE_U128; }
+inline int key_bytes_of(int k) { return (k == THRS_KEY_U32 || k == THRS_KEY_F32) ? 4 : 8; }
+inline int value_bytes_of(int v) { return v == THRS_VALUE_U32 ? 4 : v == THRS_VALUE_U64 ? 8 : 16; }
+
+// keys per thread of the per-pass kernel, per (key bytes, value bytes)
+constexpr int kpt_for(int kb, int vb) {
+  return kb == 4 ? (vb == 0 ? 32 : vb == 16 ? 8 : 16) : (vb == 16 ? 8 : 16);
+}
+inline uint64_t tile_keys(int kb, int vb) { return (uint64_t)kThreads * kpt_for(kb, vb); }
+
+struct Plan {
+  int kb, vb;         // key / value bytes (vb = 0 for sortKeys)
+  uint64_t tileKeys;  // keys per tile of the pass kernel
+  uint64_t nTiles;
+  bool wideStatus;    // 64-bit look-back words (n >= 2^31)
+  uint64_t statusBytes;
+  uint64_t scratchBytes;
+};
+
+Plan make_plan(int keyType, int valueBytesOrZero, uint32_t n) {
+  Plan p{};
+  p.kb = key_bytes_of(keyType);
+  p.vb = valueBytesOrZero;
+  p.tileKeys = tile_keys(p.kb, p.vb);
+  p.nTiles = std::max<uint64_t>(1, ((uint64_t)n + p.tileKeys - 1) / p.tileKeys);
+  p.wideStatus = (uint64_t)n >= (1ull << 31);
+  p.statusBytes = round_up(p.nTiles * kBins * (p.wideStatus ? 8 : 4), kAlign);
+  p.scratchBytes = kHeaderBytes + 2 * p.statusBytes;
+  return p;
+}
+
+int cu_count() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cached[dev]) {
+    int c = 0;
+    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
+    cached[dev] = c;
+  }
+  return cached[dev];
+}
+
+// ---- optional event timing (thrs_profile_*) ----------------------------------
+struct ProfRec {
+  hipEvent_t a, b;
+  int kind;  // 0 = histogram + scan, 1 = pass
+};
+std::mutex g_prof_mu;
+bool g_prof_on = false;
+std::vector<ProfRec> g_prof;
+std::vector<hipEvent_t> g_prof_pool;
+
+hipEvent_t prof_event() {
+  hipEvent_t e = nullptr;
+  if (!g_prof_pool.empty()) {
+    e = g_prof_pool.back();
+    g_prof_pool.pop_back();
+  } else if (hipEventCreate(&e) != hipSuccess) {
+    e = nullptr;
+  }
+  return e;
+}
+struct ProfScope {  // records [a, b) around the launches issued in its lifetime
+  hipStream_t s;
+  int kind;
+  hipEvent_t a = nullptr;
+  ProfScope(hipStream_t s_, int k) : s(s_), kind(k) {
+    if (!g_prof_on) return;
+    std::lock_guard<std::mutex> g(g_prof_mu);
+    a = prof_event();
+    if (a) (void)hipEventRecord(a, s);
+  }
+  ~ProfScope() {
+    if (!a) return;
+    std::lock_guard<std::mutex> g(g_prof_mu);
+    hipEvent_t b = prof_event();
+    if (!b) return;
+    (void)hipEventRecord(b, s);
+    g_prof.push_back({a, b, kind});
+  }
+};
+
+template <typename F>
+hipError_t allow_lds(F kernel, size_t bytes) {
+  if (bytes <= 65536) return hipSuccess;
+  return hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)bytes);
+}
+
+template <int KT, int VB, typename ST>
+int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, void* valOutBuf, int startBits, int nPass,
+             bool desc, const Plan& plan, hipStream_t stream) {
+  using U = typename KeyTraits<KT>::U;
+  using VW = typename ValueWord<VB>::T;
+  constexpr int KPT = kpt_for((int)sizeof(U), VB);
+  static_assert(kThreads * KPT <= 65536, "tile positions must fit the 24-bit rank field");
+
+  char* scratch = static_cast<char*>(tmp);
+  uint32_t* hist = reinterpret_cast<uint32_t*>(scratch + kHistOff);
+  uint32_t* base = reinterpret_cast<uint32_t*>(scratch + kBaseOff);
+  uint32_t* counters = reinterpret_cast<uint32_t*>(scratch + kCounterOff);
+  uint32_t* err = reinterpret_cast<uint32_t*>(scratch + kErrOff);
+  ST* status[2] = {reinterpret_cast<ST*>(scratch + kHeaderBytes),
+                   reinterpret_cast<ST*>(scratch + kHeaderBytes + plan.statusBytes)};
+  U* keyOut = static_cast<U*>(keyOutBuf);
+  VW* valOut = static_cast<VW*>(valOutBuf);
+
+  const U orderMask = desc ? (U)~(U)0 : (U)0;
+
+  // header (histograms, tile counters, error word) + first status table
+  if (hipMemsetAsync(scratch, 0, kHeaderBytes + plan.statusBytes, stream) != hipSuccess) return THRS_ERROR_HIP;
+
+  {  // histograms of every pass in one read of the keys
+    ProfScope prof(stream, 0);
+    const int vec = (reinterpret_cast<uintptr_t>(keys) % 16) == 0;
+    const uint64_t want = ((uint64_t)n + kThreads * 64 - 1) / (kThreads * 64);
+    const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cu_count() * 8));
+    const size_t lds = (size_t)kWaves * sizeof(U) * kBins * 4;
+    hipLaunchKernelGGL(thrs_hist<KT>, dim3(grid), dim3(kThreads), lds, stream, static_cast<const U*>(keys), n,
+                       orderMask, startBits, nPass, vec, hist);
+    hipLaunchKernelGGL(thrs_scan, dim3(1), dim3(kThreads), 0, stream, hist, base, nPass);
+  }
+
+  const size_t lds = (size_t)plan.tileKeys * (sizeof(U) + VB) + (kWaves + 1) * kBins * 4 + 64;
+  auto kernel = thrs_pass<KT, VB, KPT, ST>;
+  if (allow_lds(kernel, lds) != hipSuccess) return THRS_ERROR_HIP;
+
+  U* kin = static_cast<U*>(keys);
+  U* kout = keyOut;
+  VW* vin = static_cast<VW*>(vals);
+  VW* vout = valOut;
+  for (int p = 0; p < nPass; ++p) {
+    ST* next = (p + 1 < nPass) ? status[(p + 1) & 1] : nullptr;
+    ProfScope prof(stream, 1);
+    hipLaunchKernelGGL(kernel, dim3((uint32_t)plan.nTiles), dim3(kThreads), lds, stream, kin, kout, vin, vout, n,
+                       orderMask, startBits + 8 * p, base + p * kBins, status[p & 1], next, counters + p, err);
+    std::swap(kin, kout);
+    std::swap(vin, vout);
+  }
+  if (hipGetLastError() != hipSuccess) return THRS_ERROR_HIP;
+  if (nPass & 1) {  // result must end in the caller's buffers (hpp:936-943), stream-ordered here
+    if (hipMemcpyAsync(keys, keyOut, (size_t)n * sizeof(U), hipMemcpyDeviceToDevice, stream) != hipSuccess)
+      return THRS_ERROR_HIP;
+    if (VB && hipMemcpyAsync(vals, valOut, (size_t)n * VB, hipMemcpyDeviceToDevice, stream) != hipSuccess)
+      return THRS_ERROR_HIP;
+  }
+  return THRS_SUCCESS;
+}
+
+template <int KT, int VB>
+int run_st(void* keys, void* vals, uint32_t n, void* tmp, void* ko, void* vo, int startBits, int nPass, bool desc,
+           const Plan& plan, hipStream_t stream) {
+  if (plan.wideStatus)
+    return run_sort<KT, VB, uint64_t>(keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, stream);
+  return run_sort<KT, VB, uint32_t>(keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, stream);
+}
+
+template <int KT>
+int run_vb(int vb, void* keys, void* vals, uint32_t n, void* tmp, void* ko, void* vo, int startBits, int nPass,
+           bool desc, const Plan& plan, hipStream_t stream) {
+  switch (vb) {
+    case 0: return run_st<KT, 0>(keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, stream);
+    case 4: return run_st<KT, 4>(keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, stream);
+    case 8: return run_st<KT, 8>(keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, stream);
+    case 16: return run_st<KT, 16>(keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, stream);
+  }
+  return THRS_ERROR_INVALID_VALUE;
+}
+
+// Scratch is sized for the larger of the keys-only and pairs tile plans so
+// one buffer serves both sortKeys and sortPairs, like the reference's.
+int temp_def(int keyType, int valueType, uint32_t n, thrs_temp_def* out) {
+  if (!out || !valid_key(keyType)) return THRS_ERROR_INVALID_VALUE;
+  const int vbytes = valid_value(valueType) ? value_bytes_of(valueType) : 16;
+  const Plan pk = make_plan(keyType, 0, n);
+  const Plan pp = make_plan(keyType, vbytes, n);
+  out->pSumBuffer = round_up(std::max(pk.scratchBytes, pp.scratchBytes), 16);
+  out->keyOutBuffer = round_up((uint64_t)key_bytes_of(keyType) * n, 16);
+  out->valueOutBuffer = round_up((uint64_t)vbytes * n, 16);
+  return THRS_SUCCESS;
+}
+
+int sort_impl(const thrs_config* cfg, void* keys, void* vals, bool pairs, uint32_t n, void* tmp, int startBits,
+              int endBits, hipStream_t stream) {
+  if (!cfg || !valid_key(cfg->keyType) || (pairs && !valid_value(cfg->valueType))) return THRS_ERROR_INVALID_VALUE;
+  if (cfg->sortOrder != THRS_ORDER_ASCENDING && cfg->sortOrder != THRS_ORDER_DESCENDING) return THRS_ERROR_INVALID_VALUE;
+  if (((endBits - startBits) % 8) != 0) return THRS_ERROR_BIT_RANGE;  // tinyhipradixsort.hpp:856
+  if (startBits < 0) return THRS_ERROR_INVALID_VALUE;
+  if (n == 0 || startBits >= endBits) return THRS_SUCCESS;
+  const int kb = key_bytes_of(cfg->keyType);
+  const int width = kb * 8;
+  int nPass = 0;  // passes that read at least one key bit; the rest are identities
+  for (int i = 0; startBits + 8 * i < endBits; ++i)
+    if (startBits + 8 * i < width) ++nPass;
+  if (nPass == 0) return THRS_SUCCESS;
+  if (!keys || !tmp || (pairs && !vals)) return THRS_ERROR_INVALID_VALUE;
+  const int vb = pairs ? value_bytes_of(cfg->valueType) : 0;
+  const Plan plan = make_plan(cfg->keyType, vb, n);
+  const bool desc = cfg->sortOrder == THRS_ORDER_DESCENDING;
+  // [pSumBuffer = scratch][keyOut][valueOut], exactly as getTemporaryBufferBytes
+  // reports it (TemporaryBufferDef accessors, tinyhipradixsort.hpp:820-831).
+  thrs_temp_def def;
+  const int rc = temp_def(cfg->keyType, cfg->valueType, n, &def);
+  if (rc) return rc;
+  void* ko = static_cast<char*>(tmp) + def.pSumBuffer;
+  void* vo = static_cast<char*>(tmp) + def.pSumBuffer + def.keyOutBuffer;
+  switch (cfg->keyType) {
+    case THRS_KEY_U32: return run_vb<0>(vb, keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, stream);
+    case THRS_KEY_U64: return run_vb<1>(vb, keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, stream);
+    case THRS_KEY_F32: return run_vb<2>(vb, keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, stream);
+    case THRS_KEY_F64: return run_vb<3>(vb, keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, stream);
+  }
+  return THRS_ERROR_INVALID_VALUE;
+}
+
+}  // namespace
+
+extern "C" {
+
+int thrs_abi_version(void) { return THRS_ABI_VERSION; }
+
+const char* thrs_status_string(int s) {
+  switch (s) {
+    case THRS_SUCCESS: return "THRS_SUCCESS";
+    case THRS_ERROR_INVALID_VALUE: return "THRS_ERROR_INVALID_VALUE";
+    case THRS_ERROR_BIT_RANGE: return "THRS_ERROR_BIT_RANGE: (endBits - startBits) % 8 != 0";
+    case THRS_ERROR_HIP: return "THRS_ERROR_HIP";
+    case THRS_ERROR_OUT_OF_MEMORY: return "THRS_ERROR_OUT_OF_MEMORY";
+    case THRS_ERROR_LOOKBACK_TIMEOUT: return "THRS_ERROR_LOOKBACK_TIMEOUT";
+  }
+  return "THRS_UNKNOWN_STATUS";
+}
+
+uint64_t thrs_key_bytes(int keyType) { return valid_key(keyType) ? (uint64_t)key_bytes_of(keyType) : 0; }
+uint64_t thrs_value_bytes(int valueType) { return valid_value(valueType) ? (uint64_t)value_bytes_of(valueType) : 0; }
+
+int thrs_get_temporary_buffer_bytes(const thrs_config* cfg, uint32_t n, thrs_temp_def* out) {
+  if (!cfg || !valid_value(cfg->valueType)) return THRS_ERROR_INVALID_VALUE;
+  return temp_def(cfg->keyType, cfg->valueType, n, out);
+}
+
+int thrs_sort_keys(const thrs_config* config, void* keys, uint32_t n, void* tmp, int startBits, int endBits,
+                   hipStream_t stream) {
+  return sort_impl(config, keys, nullptr, false, n, tmp, startBits, endBits, stream);
+}
+
+int thrs_sort_pairs(const thrs_config* config, void* keys, void* values, uint32_t n, void* tmp, int startBits,
+                    int endBits, hipStream_t stream) {
+  return sort_impl(config, keys, values, true, n, tmp, startBits, endBits, stream);
+}
+
+int thrs_check_device_error(void* tmp, hipStream_t stream) {
+  if (!tmp) return THRS_ERROR_INVALID_VALUE;
+  uint32_t err = 0;
+  if (hipMemcpyAsync(&err, static_cast<char*>(tmp) + kErrOff, sizeof(err), hipMemcpyDeviceToHost, stream) !=
+          hipSuccess ||
+      hipStreamSynchronize(stream) != hipSuccess)
+    return THRS_ERROR_HIP;
+  return err ? THRS_ERROR_LOOKBACK_TIMEOUT : THRS_SUCCESS;
+}
+
+int thrs_profile_enable(int enable) {
+  std::lock_guard<std::mutex> g(g_prof_mu);
+  for (auto& r : g_prof) {
+    g_prof_pool.push_back(r.a);
+    g_prof_pool.push_back(r.b);
+  }
+  g_prof.clear();
+  g_prof_on = enable != 0;
+  return THRS_SUCCESS;
+}
+
+int thrs_profile_read(double* histMs, int* histLaunches, double* passMs, int* passLaunches) {
+  std::lock_guard<std::mutex> g(g_prof_mu);
+  double h = 0, p = 0;
+  int nh = 0, np = 0;
+  for (auto& r : g_prof) {
+    if (hipEventSynchronize(r.b) != hipSuccess) return THRS_ERROR_HIP;
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, r.a, r.b) != hipSuccess) return THRS_ERROR_HIP;
+    if (r.kind == 0) { h += ms; ++nh; } else { p += ms; ++np; }
+  }
+  if (histMs) *histMs = h;
+  if (histLaunches) *histLaunches = nh;
+  if (passMs) *passMs = p;
+  if (passLaunches) *passLaunches = np;
+  return THRS_SUCCESS;
+}
+
+int thrs_malloc(void** ptr, int64_t bytes) {
+  if (!ptr) return THRS_ERROR_INVALID_VALUE;
+  *ptr = nullptr;
+  if (hipMalloc(ptr, (size_t)std::max<int64_t>(bytes, 1)) != hipSuccess) {
+    *ptr = nullptr;
+    return THRS_ERROR_OUT_OF_MEMORY;
+  }
+  return THRS_SUCCESS;
+}
+int thrs_free(void* ptr) { return hipFree(ptr) == hipSuccess ? THRS_SUCCESS : THRS_ERROR_HIP; }
+
+int thrs_memcpy_htod_async(void* dst, const void* src, uint64_t bytes, hipStream_t stream) {
+  return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, stream) == hipSuccess ? THRS_SUCCESS : THRS_ERROR_HIP;
+}
+int thrs_memcpy_dtoh(void* dst, const void* src, uint64_t bytes) {
+  return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) == hipSuccess ? THRS_SUCCESS : THRS_ERROR_HIP;
+}
+int thrs_memcpy_dtod_async(void* dst, const void* src, uint64_t bytes, hipStream_t stream) {
+  return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, stream) == hipSuccess ? THRS_SUCCESS
+                                                                                          : THRS_ERROR_HIP;
+}
+int thrs_stream_create(hipStream_t* s) {
+  return hipStreamCreateWithFlags(s, hipStreamNonBlocking) == hipSuccess ? THRS_SUCCESS : THRS_ERROR_HIP;
+}
+int thrs_stream_destroy(hipStream_t s) { return hipStreamDestroy(s) == hipSuccess ? THRS_SUCCESS : THRS_ERROR_HIP; }
+int thrs_stream_synchronize(hipStream_t s) {
+  return hipStreamSynchronize(s) == hipSuccess ? THRS_SUCCESS : THRS_ERROR_HIP;
+}
+
+}  // extern "C"
