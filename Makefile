@@ -2,17 +2,21 @@
 # binary, and the CPU oracle.  Used by __graft_entry__.build().
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
-HIPFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Iinclude -Wall -Wno-unused-result
+HIPFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -fvisibility=hidden -Iinclude -Wall -Wno-unused-result
 PKG := tinyhipradixsort_amd
 KSRC := $(PKG)/csrc/thrs_capi.hip $(PKG)/csrc/thrs_kernels.hpp include/thrs/thrs_capi.h
 
-all: $(PKG)/libthrs.so $(PKG)/libthrs_testutil.so tests/cpp/unittest_thrs examples/helloworld oracle
+all: $(PKG)/libthrs.so $(PKG)/libthrs_testutil.so $(PKG)/libthrs_vendor.so tests/cpp/unittest_thrs examples/helloworld oracle
 
 $(PKG)/libthrs.so: $(KSRC)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(PKG)/csrc/thrs_capi.hip
 
 $(PKG)/libthrs_testutil.so: $(PKG)/csrc/thrs_testutil.hip $(PKG)/csrc/thrs_kernels.hpp
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(PKG)/csrc/thrs_testutil.hip
+
+# vendor comparator (hipCUB/rocPRIM), benchmark-only
+$(PKG)/libthrs_vendor.so: $(PKG)/csrc/thrs_vendor.hip
+	$(HIPCC) $(HIPFLAGS) -Wno-unused-parameter -shared -o $@ $<
 
 CXX ?= g++
 tests/cpp/unittest_thrs: tests/cpp/unittest_thrs.cpp include/thrs/tinyhipradixsort.hpp include/thrs/fpKey.hpp $(PKG)/libthrs.so
@@ -27,3 +31,12 @@ oracle:
 clean:
 	rm -f $(PKG)/*.so oracle/liboracle.so tests/cpp/unittest_thrs examples/helloworld
 .PHONY: all clean oracle
+
+# Tuning variants of libthrs.so for scripts/sweep.py: VARIANTS="name:-DFLAG=V,-DFLAG2=W ..."
+VARIANTS ?= kpt16:-DTHRS_KPT_K4V0=16 kpt24:-DTHRS_KPT_K4V0=24 kpt32:-DTHRS_KPT_K4V0=32
+variants:
+	@mkdir -p build/variants
+	@for v in $(VARIANTS); do name=$${v%%:*}; flags=$$(echo $${v#*:} | tr ',' ' '); \
+	  echo "variant $$name: $$flags"; \
+	  $(HIPCC) $(HIPFLAGS) $$flags -shared -o build/variants/libthrs_$$name.so $(PKG)/csrc/thrs_capi.hip & done; wait
+.PHONY: variants

@@ -43,9 +43,26 @@ inline bool valid_value(int v) { return v >= THRS_VALUE_U32 && v <= THRS_VALUE_U
 inline int key_bytes_of(int k) { return (k == THRS_KEY_U32 || k == THRS_KEY_F32) ? 4 : 8; }
 inline int value_bytes_of(int v) { return v == THRS_VALUE_U32 ? 4 : v == THRS_VALUE_U64 ? 8 : 16; }
 
-// keys per thread of the per-pass kernel, per (key bytes, value bytes)
+// keys per thread of the per-pass kernel, per (key bytes, value bytes);
+// overridable at build time for tuning sweeps (scripts/sweep.py)
+#ifndef THRS_KPT_K4V0
+#define THRS_KPT_K4V0 32
+#endif
+#ifndef THRS_KPT_K4V4
+#define THRS_KPT_K4V4 16
+#endif
+#ifndef THRS_KPT_K4V8
+#define THRS_KPT_K4V8 16
+#endif
+#ifndef THRS_KPT_K8V0
+#define THRS_KPT_K8V0 16
+#endif
+#ifndef THRS_KPT_K8V8
+#define THRS_KPT_K8V8 16
+#endif
 constexpr int kpt_for(int kb, int vb) {
-  return kb == 4 ? (vb == 0 ? 32 : vb == 16 ? 8 : 16) : (vb == 16 ? 8 : 16);
+  return kb == 4 ? (vb == 0 ? THRS_KPT_K4V0 : vb == 4 ? THRS_KPT_K4V4 : vb == 8 ? THRS_KPT_K4V8 : 8)
+                 : (vb == 0 ? THRS_KPT_K8V0 : vb == 4 ? 16 : vb == 8 ? THRS_KPT_K8V8 : 8);
 }
 inline uint64_t tile_keys(int kb, int vb) { return (uint64_t)kThreads * kpt_for(kb, vb); }
 
@@ -122,6 +139,8 @@ struct ProfScope {  // records [a, b) around the launches issued in its lifetime
   }
 };
 
+uint64_t* g_stamps = nullptr;  // THRS_STAMPS diagnostic builds only (thrs_debug_set_stamps)
+
 template <typename F>
 hipError_t allow_lds(F kernel, size_t bytes) {
   if (bytes <= 65536) return hipSuccess;
@@ -155,10 +174,11 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   {  // histograms of every pass in one read of the keys
     ProfScope prof(stream, 0);
     const int vec = (reinterpret_cast<uintptr_t>(keys) % 16) == 0;
-    const uint64_t want = ((uint64_t)n + kThreads * 64 - 1) / (kThreads * 64);
-    const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cu_count() * 8));
-    const size_t lds = (size_t)kWaves * sizeof(U) * kBins * 4;
-    hipLaunchKernelGGL(thrs_hist<KT>, dim3(grid), dim3(kThreads), lds, stream, static_cast<const U*>(keys), n,
+    const uint64_t want = ((uint64_t)n + kHistThreads * 64 - 1) / (kHistThreads * 64);
+    const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cu_count()));
+    const size_t lds = (size_t)nPass * kBins * (sizeof(U) == 4 ? 32 : 16) * 4;
+    if (allow_lds(thrs_hist<KT>, lds) != hipSuccess) return THRS_ERROR_HIP;
+    hipLaunchKernelGGL(thrs_hist<KT>, dim3(grid), dim3(kHistThreads), lds, stream, static_cast<const U*>(keys), n,
                        orderMask, startBits, nPass, vec, hist);
     hipLaunchKernelGGL(thrs_scan, dim3(1), dim3(kThreads), 0, stream, hist, base, nPass);
   }
@@ -175,7 +195,8 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     ST* next = (p + 1 < nPass) ? status[(p + 1) & 1] : nullptr;
     ProfScope prof(stream, 1);
     hipLaunchKernelGGL(kernel, dim3((uint32_t)plan.nTiles), dim3(kThreads), lds, stream, kin, kout, vin, vout, n,
-                       orderMask, startBits + 8 * p, base + p * kBins, status[p & 1], next, counters + p, err);
+                       orderMask, startBits + 8 * p, base + p * kBins, status[p & 1], next, counters + p, err,
+                       g_stamps ? g_stamps + (uint64_t)p * plan.nTiles * 8 : nullptr);
     std::swap(kin, kout);
     std::swap(vin, vout);
   }
@@ -257,11 +278,13 @@ int sort_impl(const thrs_config* cfg, void* keys, void* vals, bool pairs, uint32
 
 }  // namespace
 
+#define THRS_API __attribute__((visibility("default")))
+
 extern "C" {
 
-int thrs_abi_version(void) { return THRS_ABI_VERSION; }
+THRS_API int thrs_abi_version(void) { return THRS_ABI_VERSION; }
 
-const char* thrs_status_string(int s) {
+THRS_API const char* thrs_status_string(int s) {
   switch (s) {
     case THRS_SUCCESS: return "THRS_SUCCESS";
     case THRS_ERROR_INVALID_VALUE: return "THRS_ERROR_INVALID_VALUE";
@@ -273,25 +296,25 @@ const char* thrs_status_string(int s) {
   return "THRS_UNKNOWN_STATUS";
 }
 
-uint64_t thrs_key_bytes(int keyType) { return valid_key(keyType) ? (uint64_t)key_bytes_of(keyType) : 0; }
-uint64_t thrs_value_bytes(int valueType) { return valid_value(valueType) ? (uint64_t)value_bytes_of(valueType) : 0; }
+THRS_API uint64_t thrs_key_bytes(int keyType) { return valid_key(keyType) ? (uint64_t)key_bytes_of(keyType) : 0; }
+THRS_API uint64_t thrs_value_bytes(int valueType) { return valid_value(valueType) ? (uint64_t)value_bytes_of(valueType) : 0; }
 
-int thrs_get_temporary_buffer_bytes(const thrs_config* cfg, uint32_t n, thrs_temp_def* out) {
+THRS_API int thrs_get_temporary_buffer_bytes(const thrs_config* cfg, uint32_t n, thrs_temp_def* out) {
   if (!cfg || !valid_value(cfg->valueType)) return THRS_ERROR_INVALID_VALUE;
   return temp_def(cfg->keyType, cfg->valueType, n, out);
 }
 
-int thrs_sort_keys(const thrs_config* config, void* keys, uint32_t n, void* tmp, int startBits, int endBits,
+THRS_API int thrs_sort_keys(const thrs_config* config, void* keys, uint32_t n, void* tmp, int startBits, int endBits,
                    hipStream_t stream) {
   return sort_impl(config, keys, nullptr, false, n, tmp, startBits, endBits, stream);
 }
 
-int thrs_sort_pairs(const thrs_config* config, void* keys, void* values, uint32_t n, void* tmp, int startBits,
+THRS_API int thrs_sort_pairs(const thrs_config* config, void* keys, void* values, uint32_t n, void* tmp, int startBits,
                     int endBits, hipStream_t stream) {
   return sort_impl(config, keys, values, true, n, tmp, startBits, endBits, stream);
 }
 
-int thrs_check_device_error(void* tmp, hipStream_t stream) {
+THRS_API int thrs_check_device_error(void* tmp, hipStream_t stream) {
   if (!tmp) return THRS_ERROR_INVALID_VALUE;
   uint32_t err = 0;
   if (hipMemcpyAsync(&err, static_cast<char*>(tmp) + kErrOff, sizeof(err), hipMemcpyDeviceToHost, stream) !=
@@ -301,7 +324,7 @@ int thrs_check_device_error(void* tmp, hipStream_t stream) {
   return err ? THRS_ERROR_LOOKBACK_TIMEOUT : THRS_SUCCESS;
 }
 
-int thrs_profile_enable(int enable) {
+THRS_API int thrs_profile_enable(int enable) {
   std::lock_guard<std::mutex> g(g_prof_mu);
   for (auto& r : g_prof) {
     g_prof_pool.push_back(r.a);
@@ -312,7 +335,7 @@ int thrs_profile_enable(int enable) {
   return THRS_SUCCESS;
 }
 
-int thrs_profile_read(double* histMs, int* histLaunches, double* passMs, int* passLaunches) {
+THRS_API int thrs_profile_read(double* histMs, int* histLaunches, double* passMs, int* passLaunches) {
   std::lock_guard<std::mutex> g(g_prof_mu);
   double h = 0, p = 0;
   int nh = 0, np = 0;
@@ -329,7 +352,14 @@ int thrs_profile_read(double* histMs, int* histLaunches, double* passMs, int* pa
   return THRS_SUCCESS;
 }
 
-int thrs_malloc(void** ptr, int64_t bytes) {
+// Diagnostic hook, not part of the drop-in boundary: in -DTHRS_STAMPS builds
+// the pass kernel writes per-tile phase timestamps to buf[(pass*nTiles+tile)*8+i].
+THRS_API int thrs_debug_set_stamps(void* buf) {
+  g_stamps = static_cast<uint64_t*>(buf);
+  return THRS_SUCCESS;
+}
+
+THRS_API int thrs_malloc(void** ptr, int64_t bytes) {
   if (!ptr) return THRS_ERROR_INVALID_VALUE;
   *ptr = nullptr;
   if (hipMalloc(ptr, (size_t)std::max<int64_t>(bytes, 1)) != hipSuccess) {
@@ -338,23 +368,23 @@ int thrs_malloc(void** ptr, int64_t bytes) {
   }
   return THRS_SUCCESS;
 }
-int thrs_free(void* ptr) { return hipFree(ptr) == hipSuccess ? THRS_SUCCESS : THRS_ERROR_HIP; }
+THRS_API int thrs_free(void* ptr) { return hipFree(ptr) == hipSuccess ? THRS_SUCCESS : THRS_ERROR_HIP; }
 
-int thrs_memcpy_htod_async(void* dst, const void* src, uint64_t bytes, hipStream_t stream) {
+THRS_API int thrs_memcpy_htod_async(void* dst, const void* src, uint64_t bytes, hipStream_t stream) {
   return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, stream) == hipSuccess ? THRS_SUCCESS : THRS_ERROR_HIP;
 }
-int thrs_memcpy_dtoh(void* dst, const void* src, uint64_t bytes) {
+THRS_API int thrs_memcpy_dtoh(void* dst, const void* src, uint64_t bytes) {
   return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) == hipSuccess ? THRS_SUCCESS : THRS_ERROR_HIP;
 }
-int thrs_memcpy_dtod_async(void* dst, const void* src, uint64_t bytes, hipStream_t stream) {
+THRS_API int thrs_memcpy_dtod_async(void* dst, const void* src, uint64_t bytes, hipStream_t stream) {
   return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, stream) == hipSuccess ? THRS_SUCCESS
                                                                                           : THRS_ERROR_HIP;
 }
-int thrs_stream_create(hipStream_t* s) {
+THRS_API int thrs_stream_create(hipStream_t* s) {
   return hipStreamCreateWithFlags(s, hipStreamNonBlocking) == hipSuccess ? THRS_SUCCESS : THRS_ERROR_HIP;
 }
-int thrs_stream_destroy(hipStream_t s) { return hipStreamDestroy(s) == hipSuccess ? THRS_SUCCESS : THRS_ERROR_HIP; }
-int thrs_stream_synchronize(hipStream_t s) {
+THRS_API int thrs_stream_destroy(hipStream_t s) { return hipStreamDestroy(s) == hipSuccess ? THRS_SUCCESS : THRS_ERROR_HIP; }
+THRS_API int thrs_stream_synchronize(hipStream_t s) {
   return hipStreamSynchronize(s) == hipSuccess ? THRS_SUCCESS : THRS_ERROR_HIP;
 }
 

@@ -93,6 +93,12 @@ __device__ __forceinline__ T load_agent(const T* p) {
   return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Opaque redefinition of a register value: computations that depend on x
+// cannot be hoisted above this point (the compiler otherwise precomputes every
+// item's digit and LDS address up front and spills).
+__device__ __forceinline__ void pin(uint32_t& x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void pin(uint64_t& x) { asm volatile("" : "+v"(x)); }
+
 // ------------------------------------------------------------ wave helpers
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 
@@ -137,19 +143,27 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* s_w
 // ================================================================ histogram
 // Histograms of up to NP_MAX digits of every key in one read.
 //   hist[p*256 + d] += #keys with digit d at bit startBits + 8p.
-// LDS: per-wave private copies [wave][p][256] to spread LDS atomics; merged
-// with one device-scope atomic per (p, bin) per workgroup.
+// LDS layout [p][d][COPIES]: lane l always adds into copy (l % COPIES), so for
+// COPIES = 32 the bank of every ds_add_u32 is l % 32 -- conflict-free whatever
+// the digits are (random digits into one shared 256-bin table collide ~3-4 way
+// per 32-lane half).  128 KiB of LDS -> one 512-thread workgroup per CU;
+// 64-bit keys (8 digits) use 16 copies.  Copies are summed once per workgroup
+// and merged with one device-scope atomic per (p, bin).
+constexpr int kHistThreads = 512;
 template <int KT>
-__global__ __launch_bounds__(kThreads) void thrs_hist(const typename KeyTraits<KT>::U* __restrict__ keys,
-                                                      uint32_t n, typename KeyTraits<KT>::U orderMask,
-                                                      int startBits, int nPass, int vec, uint32_t* __restrict__ hist) {
+__global__ __launch_bounds__(kHistThreads) void thrs_hist(const typename KeyTraits<KT>::U* __restrict__ keys,
+                                                          uint32_t n, typename KeyTraits<KT>::U orderMask,
+                                                          int startBits, int nPass, int vec,
+                                                          uint32_t* __restrict__ hist) {
   using U = typename KeyTraits<KT>::U;
   constexpr int NP_MAX = sizeof(U);
-  extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];  // [kWaves][NP_MAX][256]
-  const uint32_t tid = threadIdx.x, w = tid >> 6;
-  for (uint32_t i = tid; i < (uint32_t)(kWaves * NP_MAX * kBins); i += kThreads) s_hist[i] = 0;
+  constexpr int COPIES = NP_MAX == 4 ? 32 : 16;
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];  // [nPass][256][COPIES]
+  const uint32_t tid = threadIdx.x;
+  const uint32_t words = (uint32_t)nPass * kBins * COPIES;
+  for (uint32_t i = tid; i < words; i += kHistThreads) s_hist[i] = 0;
   __syncthreads();
-  uint32_t* my = s_hist + w * NP_MAX * kBins;
+  uint32_t* my = s_hist + (tid % COPIES);
 
   auto count = [&](U k) {
     const U b = KeyTraits<KT>::bits(k) ^ orderMask;
@@ -157,20 +171,35 @@ __global__ __launch_bounds__(kThreads) void thrs_hist(const typename KeyTraits<K
     for (int p = 0; p < NP_MAX; ++p) {
       if (p < nPass) {
         const uint32_t d = (uint32_t)(b >> (startBits + 8 * p)) & 0xFFu;
-        atomicAdd(&my[p * kBins + d], 1u);
+        __hip_atomic_fetch_add(&my[(p * kBins + d) * COPIES], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     }
   };
 
-  const uint64_t gstride = (uint64_t)gridDim.x * kThreads;
-  const uint64_t gtid = (uint64_t)blockIdx.x * kThreads + tid;
+  const uint64_t gstride = (uint64_t)gridDim.x * kHistThreads;
+  const uint64_t gtid = (uint64_t)blockIdx.x * kHistThreads + tid;
   uint64_t tailStart = 0;
-  if (vec) {  // 16-byte loads; keys base is 16-B aligned (checked on host)
+  if (vec) {  // 16-byte loads, 4 in flight per lane; keys base is 16-B aligned (checked on host)
     constexpr int PER = 16 / sizeof(U);
     const uint64_t nv = n / PER;
     const uint4* kv = reinterpret_cast<const uint4*>(keys);
-    for (uint64_t i = gtid; i < nv; i += gstride) {
-      uint4 q = kv[i];
+    uint64_t i = gtid;
+    for (; i + 3 * gstride < nv; i += 4 * gstride) {
+      uint4 q[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) q[u] = kv[i + u * gstride];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if constexpr (sizeof(U) == 4) {
+          count(q[u].x); count(q[u].y); count(q[u].z); count(q[u].w);
+        } else {
+          count(((uint64_t)q[u].y << 32) | q[u].x);
+          count(((uint64_t)q[u].w << 32) | q[u].z);
+        }
+      }
+    }
+    for (; i < nv; i += gstride) {
+      const uint4 q = kv[i];
       if constexpr (sizeof(U) == 4) {
         count(q.x); count(q.y); count(q.z); count(q.w);
       } else {
@@ -182,10 +211,10 @@ __global__ __launch_bounds__(kThreads) void thrs_hist(const typename KeyTraits<K
   }
   for (uint64_t i = tailStart + gtid; i < n; i += gstride) count(keys[i]);
   __syncthreads();
-  for (uint32_t i = tid; i < (uint32_t)(nPass * kBins); i += kThreads) {
+  for (uint32_t i = tid; i < (uint32_t)(nPass * kBins); i += kHistThreads) {
     uint32_t s = 0;
 #pragma unroll
-    for (int ww = 0; ww < kWaves; ++ww) s += s_hist[ww * NP_MAX * kBins + i];
+    for (int c = 0; c < COPIES; ++c) s += s_hist[i * COPIES + ((c + i) % COPIES)];  // rotate: conflict-free reads
     if (s) atomicAdd(&hist[i], s);
   }
 }
@@ -202,24 +231,45 @@ __global__ __launch_bounds__(kThreads) void thrs_scan(const uint32_t* __restrict
 }
 
 // ================================================================ one pass
+// Workgroup-local barrier that does NOT drain vector memory: every hand-off
+// between the waves of a workgroup in thrs_pass goes through LDS, so only
+// lgkmcnt must be zero.  (__syncthreads() also waits for vmcnt(0), which would
+// park the workgroup on the in-flight look-back load and status store.)
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// Look-back window: predecessors read per round trip once a walk has started.
+constexpr int kLookWindow = 4;
+
 // Tile = 256 threads x KPT keys.  Wave w owns the contiguous chunk
 // [w*64*KPT, (w+1)*64*KPT) of the tile; item j of that chunk is 64
 // consecutive keys, one per lane, so (wave, item, lane) order is input order
 // and ranking item by item is stable.
 //
+// Phases (thread tid doubles as "digit d = tid" in the per-digit phases):
+//   A  tile id, load keys (+values) into registers
+//   B  per-wave digit histogram (LDS atomics) -> tile counts; publish the
+//      tile aggregate and ISSUE the look-back load; local exclusive scan
+//   C  rank item by item (wave64 ballot match + per-wave running counters that
+//      start at the wave's local offsets) and scatter straight into the LDS
+//      tile; the look-back load is in flight meanwhile
+//   D  finish the look-back -> global offset of digit d
+//   E  coalesced write-out of the sorted LDS tile
+//
 // LDS (dynamic, 16-B aligned):
-//   stage_k [T]   keys in tile-sorted order
-//   stage_v [T]   values in tile-sorted order (pairs only)
-//   s_cnt   [4][256]  per-wave running digit counts -> per-wave offsets
-//   s_gofs  [256]     global dst of sorted slot 0 for digit d = base + excl - localStart
+//   stage_k [T]       keys in tile-sorted order
+//   stage_v [T]       values in tile-sorted order (pairs only)
+//   s_cnt   [4][256]  per-wave digit counts -> per-wave running offsets
+//   s_gofs  [256]     global dst of local slot 0 of digit d (base + excl - localStart)
 //   s_misc  [8]       tile id, scan scratch
 template <int KT, int VB, int KPT, typename ST>
-__global__ __launch_bounds__(kThreads) void thrs_pass(
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void thrs_pass(
     const typename KeyTraits<KT>::U* __restrict__ keysIn, typename KeyTraits<KT>::U* __restrict__ keysOut,
     const typename ValueWord<VB>::T* __restrict__ valsIn, typename ValueWord<VB>::T* __restrict__ valsOut,
     uint32_t n, typename KeyTraits<KT>::U orderMask, int shift, const uint32_t* __restrict__ digitBase,
     ST* __restrict__ status, ST* __restrict__ statusNext, uint32_t* __restrict__ tileCounter,
-    uint32_t* __restrict__ errFlag) {
+    uint32_t* __restrict__ errFlag, uint64_t* __restrict__ stamps) {
   using U = typename KeyTraits<KT>::U;
   using VW = typename ValueWord<VB>::T;
   constexpr uint32_t T = kThreads * KPT;
@@ -231,44 +281,79 @@ __global__ __launch_bounds__(kThreads) void thrs_pass(
   uint32_t* s_gofs = s_cnt + kWaves * kBins;
   uint32_t* s_misc = s_gofs + kBins;
 
+  // Diagnostic builds (-DTHRS_STAMPS) record s_memrealtime (100 MHz) per
+  // phase for every tile into stamps[tile*8 + i]; normal builds compile none.
+#ifdef THRS_STAMPS
+#define THRS_STAMP(i)                                                                                  \
+  do {                                                                                                 \
+    if (stamps && threadIdx.x == 0) stamps[(uint64_t)tile * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+  const uint64_t t_entry = __builtin_amdgcn_s_memrealtime();
+#else
+#define THRS_STAMP(i) \
+  do {                \
+  } while (0)
+  (void)stamps;
+#endif
+
   const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
 
+  // ---- A: dynamic tile id (start order, so every tile we wait on is resident)
   if (tid == 0) s_misc[0] = atomicAdd(tileCounter, 1u);
 #pragma unroll
   for (int i = 0; i < kWaves; ++i) s_cnt[i * kBins + tid] = 0;
-  __syncthreads();
+  lds_barrier();
   const uint32_t tile = s_misc[0];
+#ifdef THRS_STAMPS
+  if (stamps && tid == 0) {
+    stamps[(uint64_t)tile * 8 + 0] = t_entry;
+    uint32_t xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    stamps[(uint64_t)tile * 8 + 7] = xcc;
+  }
+#endif
+  THRS_STAMP(1);
   const uint64_t tileBase = (uint64_t)tile * T;
   const uint32_t valid = (uint32_t)min((uint64_t)T, (uint64_t)n - tileBase);
+  const bool full = valid == T;
   const uint64_t chunkBase = tileBase + w * CHUNK;
 
-  // ---- load keys (striped per wave: item j = 64 consecutive keys)
   U k[KPT];
+  if (full) {
 #pragma unroll
-  for (int j = 0; j < KPT; ++j) {
-    const uint32_t local = w * CHUNK + j * 64 + lane;
-    k[j] = (local < valid) ? keysIn[chunkBase + j * 64 + lane] : (U)0;
+    for (int j = 0; j < KPT; ++j) k[j] = keysIn[chunkBase + j * 64 + lane];
+  } else {
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) {
+      const uint32_t local = w * CHUNK + j * 64 + lane;
+      k[j] = (local < valid) ? keysIn[chunkBase + j * 64 + lane] : (U)0;
+    }
   }
-  const uint32_t myBase = digitBase[tid];  // global base of digit `tid` (used after look-back)
+  VW v[VB ? KPT : 1];
+  if constexpr (VB != 0) {
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) {
+      const uint32_t local = w * CHUNK + j * 64 + lane;
+      if (full || local < valid) v[j] = valsIn[chunkBase + j * 64 + lane];
+      else v[j] = VW{};
+    }
+  }
+  const uint32_t myBase = digitBase[tid];  // global base of digit `tid`, used in D
 
-  // ---- stable rank inside the wave chunk
-  uint32_t pk[KPT];  // (rank << 8) | digit
+  auto digit_of = [&](U key, int j) -> uint32_t {
+    uint32_t d = (uint32_t)((KeyTraits<KT>::bits(key) ^ orderMask) >> shift) & 0xFFu;
+    if (!full) d = (w * CHUNK + j * 64 + lane < valid) ? d : 0xFFu;  // padding sorts after every real key
+    return d;
+  };
+
+  // ---- B: per-wave histogram (order-free LDS atomics)
   uint32_t* cnt = s_cnt + w * kBins;
 #pragma unroll
-  for (int j = 0; j < KPT; ++j) {
-    const uint32_t local = w * CHUNK + j * 64 + lane;
-    uint32_t d = (uint32_t)((KeyTraits<KT>::bits(k[j]) ^ orderMask) >> shift) & 0xFFu;
-    d = (local < valid) ? d : 0xFFu;  // padding ranks after every real key
-    uint32_t mlo, mhi;
-    match_digit(d, mlo, mhi);
-    const uint32_t c = cnt[d];
-    const uint32_t r = c + __builtin_amdgcn_mbcnt_hi(mhi, __builtin_amdgcn_mbcnt_lo(mlo, 0u));
-    cnt[d] = c + __builtin_popcount(mlo) + __builtin_popcount(mhi);
-    pk[j] = (r << 8) | d;
-  }
-  __syncthreads();
+  for (int j = 0; j < KPT; ++j)
+    __hip_atomic_fetch_add(&cnt[digit_of(k[j], j)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  lds_barrier();
+  THRS_STAMP(2);
 
-  // ---- per digit (thread tid == digit d): tile count, per-wave offsets
   const uint32_t d = tid;
   const uint32_t c0 = s_cnt[0 * kBins + d], c1 = s_cnt[1 * kBins + d];
   const uint32_t c2 = s_cnt[2 * kBins + d], c3 = s_cnt[3 * kBins + d];
@@ -277,72 +362,118 @@ __global__ __launch_bounds__(kThreads) void thrs_pass(
   ST* myStatus = status + (uint64_t)tile * kBins + d;
   if (tile != 0) store_agent(myStatus, Status<ST>::agg(realTot));
   else store_agent(myStatus, Status<ST>::pre(realTot));
+  ST look = 0;
+  if (tile != 0) look = load_agent(status + (uint64_t)(tile - 1) * kBins + d);
 
-  uint32_t blockTotal;
-  const uint32_t localStart = block_excl_scan256(tot, s_misc + 4, &blockTotal);
+  // local exclusive scan over digits (wave scan + 4 wave totals through LDS)
+  const uint32_t incl = wave_incl_scan(tot, lane);
+  if (lane == 63) s_misc[4 + w] = incl;
+  lds_barrier();
+  const uint32_t w0 = s_misc[4], w1 = s_misc[5], w2 = s_misc[6];
+  const uint32_t localStart = incl - tot + (w > 0 ? w0 : 0u) + (w > 1 ? w1 : 0u) + (w > 2 ? w2 : 0u);
   s_cnt[0 * kBins + d] = localStart;
   s_cnt[1 * kBins + d] = localStart + c0;
   s_cnt[2 * kBins + d] = localStart + c0 + c1;
   s_cnt[3 * kBins + d] = localStart + c0 + c1 + c2;
+  lds_barrier();
+  THRS_STAMP(3);
 
-  // ---- decoupled look-back for digit d
+  // ---- C: stable rank = running per-wave offset + peers in lower lanes; the
+  // slot is final, so the key goes straight into the sorted LDS tile
+#pragma unroll
+  for (int j = 0; j < KPT; ++j) {
+    pin(k[j]);  // keep item j's digit/address math inside iteration j (register pressure)
+    const uint32_t dj = digit_of(k[j], j);
+    uint32_t mlo, mhi;
+    match_digit(dj, mlo, mhi);
+    const uint32_t c = cnt[dj];
+    const uint32_t slot = __builtin_amdgcn_mbcnt_hi(mhi, __builtin_amdgcn_mbcnt_lo(mlo, c));
+    cnt[dj] = __builtin_popcount(mhi) + __builtin_popcount(mlo) + c;
+    stage_k[slot] = k[j];
+    if constexpr (VB != 0) stage_v[slot] = v[j];
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  THRS_STAMP(4);
+
+  // ---- D: finish the decoupled look-back for digit d.  Walks read a window
+  // of kLookWindow predecessors per round trip; a not-yet-published word stops
+  // the window and is re-polled.
   uint32_t excl = 0;
+#ifdef THRS_STAMPS
+  uint32_t dbgRounds = 0;
+  if (tid == 0) { s_misc[1] = 0; s_misc[2] = 0; s_misc[3] = 0; }
+#endif
   if (tile != 0) {
-    int64_t j = (int64_t)tile - 1;
+    int64_t j = (int64_t)tile - 1;  // next predecessor to consume
     uint32_t spins = 0;
+    ST win[kLookWindow];
+    win[0] = look;
+    int have = 1;
     while (true) {
-      const ST s = load_agent(status + (uint64_t)j * kBins + d);
-      if (s == 0) {
-        if (++spins > (1u << 24)) {  // bounded spin: never hang the GPU
+      bool done = false, stall = false;
+#pragma unroll
+      for (int q = 0; q < kLookWindow; ++q) {
+        if (q < have && !done && !stall) {
+          const ST sw = win[q];
+          if (sw == 0) {
+            stall = true;
+          } else {
+            excl += Status<ST>::val(sw);
+            if (Status<ST>::is_pre(sw)) done = true;
+            else --j;
+          }
+        }
+      }
+      if (done) break;
+      if (stall) {
+        if (++spins > (1u << 22)) {  // bounded spin: never hang the GPU
           atomicOr(errFlag, 1u);
           break;
         }
         __builtin_amdgcn_s_sleep(1);
-        continue;
       }
-      excl += Status<ST>::val(s);
-      if (Status<ST>::is_pre(s)) break;
-      --j;
+#ifdef THRS_STAMPS
+      ++dbgRounds;
+#endif
+      // (re)load the next window [j, j-1, ...] (j >= 0: tile 0 is always a prefix)
+#pragma unroll
+      for (int q = 0; q < kLookWindow; ++q)
+        if (j - q >= 0) win[q] = load_agent(status + (uint64_t)(j - q) * kBins + d);
+      have = (int)min<int64_t>(kLookWindow, j + 1);
     }
     store_agent(myStatus, Status<ST>::pre(excl + realTot));
+#ifdef THRS_STAMPS
+    atomicMax(&s_misc[1], dbgRounds);
+    atomicMax(&s_misc[2], spins);
+    atomicMax(&s_misc[3], (uint32_t)(tile - 1 - j));
+#endif
   }
   s_gofs[d] = myBase + excl - localStart;
   if (statusNext) statusNext[(uint64_t)tile * kBins + d] = 0;  // ready for the next pass
-  __syncthreads();
+  lds_barrier();
+  THRS_STAMP(5);
 
-  // ---- scatter into the LDS tile in sorted order
-  const uint32_t* offs = s_cnt + w * kBins;
-#pragma unroll
-  for (int j = 0; j < KPT; ++j) {
-    const uint32_t dd = pk[j] & 0xFFu;
-    const uint32_t p = offs[dd] + (pk[j] >> 8);
-    stage_k[p] = k[j];
-    pk[j] = p;
-  }
-  if constexpr (VB != 0) {
-#pragma unroll
-    for (int j = 0; j < KPT; ++j) {
-      const uint32_t local = w * CHUNK + j * 64 + lane;
-      VW v;
-      if (local < valid) v = valsIn[chunkBase + j * 64 + lane];
-      else v = VW{};
-      stage_v[pk[j]] = v;
-    }
-  }
-  __syncthreads();
-
-  // ---- coalesced write-out: sorted slot i -> s_gofs[digit] + i
+  // ---- E: coalesced write-out: sorted slot i -> s_gofs[digit] + i
 #pragma unroll
   for (int j = 0; j < KPT; ++j) {
     const uint32_t i = j * kThreads + tid;
-    if (i < valid) {
+    if (full || i < valid) {
       const U key = stage_k[i];
       const uint32_t dd = (uint32_t)((KeyTraits<KT>::bits(key) ^ orderMask) >> shift) & 0xFFu;
       const uint32_t dst = s_gofs[dd] + i;
       keysOut[dst] = key;
       if constexpr (VB != 0) valsOut[dst] = stage_v[i];
     }
+    if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);  // bound live 64-bit store addresses
   }
+#ifdef THRS_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  THRS_STAMP(6);
+  if (stamps && tid == 0)  // slot 7: xcc | max rounds << 8 | max depth << 24 | max stalls << 40
+    stamps[(uint64_t)tile * 8 + 7] |= ((uint64_t)min(s_misc[1], 65535u) << 8) |
+                                      ((uint64_t)min(s_misc[3], 65535u) << 24) | ((uint64_t)s_misc[2] << 40);
+#endif
+#undef THRS_STAMP
 }
 
 }  // namespace thrs_dev

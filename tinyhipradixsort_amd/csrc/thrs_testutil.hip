@@ -133,22 +133,23 @@ inline int ok(hipError_t e) { return e == hipSuccess ? THRS_SUCCESS : THRS_ERROR
 
 }  // namespace
 
+#define THRS_API __attribute__((visibility("default")))
 extern "C" {
 
-int thrsu_fill_keys(int keyType, void* out, uint64_t n, uint64_t start, uint64_t state, hipStream_t stream) {
+THRS_API int thrsu_fill_keys(int keyType, void* out, uint64_t n, uint64_t start, uint64_t state, hipStream_t stream) {
   if (!n) return THRS_SUCCESS;
   hipLaunchKernelGGL(k_fill, dim3(grid_for(n)), dim3(256), 0, stream, keyType, out, n, start, state);
   return ok(hipGetLastError());
 }
 
-int thrsu_iota(int valueBytes, void* out, uint64_t n, uint64_t start, hipStream_t stream) {
+THRS_API int thrsu_iota(int valueBytes, void* out, uint64_t n, uint64_t start, hipStream_t stream) {
   if (!n) return THRS_SUCCESS;
   hipLaunchKernelGGL(k_iota, dim3(grid_for(n)), dim3(256), 0, stream, valueBytes, out, n, start);
   return ok(hipGetLastError());
 }
 
 // result[0] = number of out-of-order neighbours (synchronising)
-int thrsu_check_sorted(int keyType, int desc, const void* keys, uint64_t n, int startBits, int endBits,
+THRS_API int thrsu_check_sorted(int keyType, int desc, const void* keys, uint64_t n, int startBits, int endBits,
                        unsigned long long* result, hipStream_t stream) {
   unsigned long long* d = nullptr;
   if (hipMalloc(&d, 8) != hipSuccess) return THRS_ERROR_HIP;
@@ -160,7 +161,7 @@ int thrsu_check_sorted(int keyType, int desc, const void* keys, uint64_t n, int 
   return rc;
 }
 
-int thrsu_fingerprint(int keyType, const void* keys, uint64_t n, unsigned long long* result2, hipStream_t stream) {
+THRS_API int thrsu_fingerprint(int keyType, const void* keys, uint64_t n, unsigned long long* result2, hipStream_t stream) {
   unsigned long long* d = nullptr;
   if (hipMalloc(&d, 16) != hipSuccess) return THRS_ERROR_HIP;
   (void)hipMemsetAsync(d, 0, 16, stream);
@@ -171,7 +172,7 @@ int thrsu_fingerprint(int keyType, const void* keys, uint64_t n, unsigned long l
   return rc;
 }
 
-int thrsu_check_pairs(int keyType, int desc, int valueBytes, const void* keysIn, const void* keysOut, const void* vals,
+THRS_API int thrsu_check_pairs(int keyType, int desc, int valueBytes, const void* keysIn, const void* keysOut, const void* vals,
                       uint64_t n, int startBits, int endBits, unsigned long long* result5, hipStream_t stream) {
   unsigned long long* d = nullptr;
   if (hipMalloc(&d, 40) != hipSuccess) return THRS_ERROR_HIP;
