@@ -32,11 +32,11 @@ clean:
 	rm -f $(PKG)/*.so oracle/liboracle.so tests/cpp/unittest_thrs examples/helloworld
 .PHONY: all clean oracle
 
-# Tuning variants of libthrs.so for scripts/sweep.py: VARIANTS="name:-DFLAG=V,-DFLAG2=W ..."
-VARIANTS ?= kpt16:-DTHRS_KPT_K4V0=16 kpt24:-DTHRS_KPT_K4V0=24 kpt32:-DTHRS_KPT_K4V0=32
+# Tuning variants of libthrs.so for scripts/sweep.py: VARIANTS="name:-DFLAG=V+-DFLAG2=W ..."
+VARIANTS ?= stamps:-DTHRS_STAMPS
 variants:
 	@mkdir -p build/variants
-	@for v in $(VARIANTS); do name=$${v%%:*}; flags=$$(echo $${v#*:} | tr ',' ' '); \
+	@for v in $(VARIANTS); do name=$${v%%:*}; flags=$$(echo $${v#*:} | tr '+' ' '); \
 	  echo "variant $$name: $$flags"; \
 	  $(HIPCC) $(HIPFLAGS) $$flags -shared -o build/variants/libthrs_$$name.so $(PKG)/csrc/thrs_capi.hip & done; wait
 .PHONY: variants

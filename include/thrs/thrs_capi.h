@@ -104,6 +104,13 @@ int thrs_check_device_error(void* temporaryBuffer, hipStream_t stream);
 int thrs_profile_enable(int enable);
 int thrs_profile_read(double* histMs, int* histLaunches, double* passMs, int* passLaunches);
 
+/* Rank path of the current device: 1 = one LDS atomic per key (gfx950
+ * services conflicting lanes of a fully active wave in lane order; checked by
+ * a one-time probe kernel per device), 0 = ballot match (always stable).
+ * THRS_RANK=ballot|atomic in the environment overrides.  No reference
+ * counterpart. */
+int thrs_rank_mode(void);
+
 /* == thrs::Buffer (tinyhipradixsort.hpp:501-528): hipMalloc(max(bytes,1)). */
 int thrs_malloc(void** ptr, int64_t bytes);
 int thrs_free(void* ptr);

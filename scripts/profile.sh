@@ -1,0 +1,16 @@
+#!/bin/bash
+# rocprofv3 collection for profiles/: kernel trace + stats, then one --pmc pass
+# per counter group (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950),
+# never combined with sys/runtime traces.  usage: bash scripts/profile.sh <tag> [workload]
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+TAG=${1:-r01}; WL=${2:-c2}
+OUT=gpurun_out/prof_${TAG}_${WL}
+mkdir -p $OUT
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 scripts/profile_run.py --workload $WL > $OUT/trace.log 2>&1 || { echo "trace failed"; tail -5 $OUT/trace.log; exit 1; }
+for C in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum"; do
+  name=$(echo $C | tr ' ' '_')
+  timeout -k 10 300 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $OUT/pmc_$name -o run -- python3 scripts/profile_run.py --workload $WL > $OUT/pmc_$name.log 2>&1 || { echo "pmc $C failed"; tail -5 $OUT/pmc_$name.log; exit 1; }
+done
+python3 scripts/prof_summary.py $OUT > $OUT/summary.json && cat $OUT/summary.json

@@ -43,8 +43,9 @@ def main():
     tmp = torch.empty(d.pSumBuffer + d.keyOutBuffer + d.valueOutBuffer, dtype=torch.uint8, device="cuda")
     keys = torch.empty(n * kb, dtype=torch.uint8, device="cuda")
     vals = torch.empty(max(1, n * vb), dtype=torch.uint8, device="cuda")
-    tile = {(4, 0): 8192, (4, 4): 4096, (4, 8): 4096, (8, 0): 4096, (8, 8): 4096}.get((kb, vb), 4096)
-    tile = int(os.environ.get("THRS_TILE", tile))
+    L.thrs_debug_tile_keys.argtypes = [ctypes.c_int, ctypes.c_int]
+    L.thrs_debug_tile_keys.restype = ctypes.c_uint64
+    tile = int(L.thrs_debug_tile_keys(kt, vb))
     ntiles = (n + tile - 1) // tile
     passes = kb
     stamps = torch.zeros(passes * ntiles * 8, dtype=torch.int64, device="cuda")

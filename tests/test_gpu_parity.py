@@ -122,6 +122,19 @@ def test_matrix_vs_oracle(gpu, kt, vb, desc):
             assert np.array_equal(v, ev), (n, s, e)
 
 
+def test_rank_probe_and_ballot_fallback(gpu):
+    """The LDS-atomic rank path is used only where the lane-order probe passes;
+    the ballot-match fallback must be bit-exact too (forced via THRS_RANK)."""
+    import tinyhipradixsort_amd as T
+    mode = T.lib().thrs_rank_mode()
+    assert mode in (0, 1)
+    print("rank mode:", "lds-atomic" if mode else "ballot")
+    exe = os.path.join(ROOT, "tests", "cpp", "unittest_thrs")
+    env = dict(os.environ, THRS_RANK="ballot")
+    r = subprocess.run([exe, "--filter=SortPairs.K"], capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stdout[-3000:]
+
+
 def test_cpp_port_of_reference_unittest(gpu):
     """The reference's UTEST matrix, ported to C++ against the drop-in header."""
     exe = os.path.join(ROOT, "tests", "cpp", "unittest_thrs")

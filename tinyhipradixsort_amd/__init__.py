@@ -77,6 +77,7 @@ def lib() -> ctypes.CDLL:
         L.thrs_profile_enable.argtypes = [i32]
         L.thrs_profile_read.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32),
                                         ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32)]
+        L.thrs_rank_mode.restype = i32
         for f in ("thrs_profile_enable", "thrs_profile_read", "thrs_get_temporary_buffer_bytes", "thrs_sort_keys", "thrs_sort_pairs", "thrs_check_device_error",
                   "thrs_malloc", "thrs_free", "thrs_memcpy_htod_async", "thrs_memcpy_dtoh", "thrs_memcpy_dtod_async",
                   "thrs_stream_create", "thrs_stream_destroy", "thrs_stream_synchronize"):

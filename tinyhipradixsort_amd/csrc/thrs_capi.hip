@@ -18,6 +18,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -43,28 +44,20 @@ inline bool valid_value(int v) { return v >= THRS_VALUE_U32 && v <= THRS_VALUE_U
 inline int key_bytes_of(int k) { return (k == THRS_KEY_U32 || k == THRS_KEY_F32) ? 4 : 8; }
 inline int value_bytes_of(int v) { return v == THRS_VALUE_U32 ? 4 : v == THRS_VALUE_U64 ? 8 : 16; }
 
-// keys per thread of the per-pass kernel, per (key bytes, value bytes);
-// overridable at build time for tuning sweeps (scripts/sweep.py)
-#ifndef THRS_KPT_K4V0
-#define THRS_KPT_K4V0 32
-#endif
-#ifndef THRS_KPT_K4V4
-#define THRS_KPT_K4V4 16
-#endif
-#ifndef THRS_KPT_K4V8
-#define THRS_KPT_K4V8 16
-#endif
-#ifndef THRS_KPT_K8V0
-#define THRS_KPT_K8V0 16
-#endif
-#ifndef THRS_KPT_K8V8
-#define THRS_KPT_K8V8 16
-#endif
-constexpr int kpt_for(int kb, int vb) {
-  return kb == 4 ? (vb == 0 ? THRS_KPT_K4V0 : vb == 4 ? THRS_KPT_K4V4 : vb == 8 ? THRS_KPT_K4V8 : 8)
-                 : (vb == 0 ? THRS_KPT_K8V0 : vb == 4 ? 16 : vb == 8 ? THRS_KPT_K8V8 : 8);
+// keys per tile of the pass kernel, per (key bytes, value bytes) -- PassCfg in
+// thrs_kernels.hpp
+inline uint64_t tile_keys(int kb, int vb) {
+  switch (kb * 100 + vb) {
+    case 400: return PassGeom<4, 0>::TILE;
+    case 404: return PassGeom<4, 4>::TILE;
+    case 408: return PassGeom<4, 8>::TILE;
+    case 416: return PassGeom<4, 16>::TILE;
+    case 800: return PassGeom<8, 0>::TILE;
+    case 804: return PassGeom<8, 4>::TILE;
+    case 808: return PassGeom<8, 8>::TILE;
+    default: return PassGeom<8, 16>::TILE;
+  }
 }
-inline uint64_t tile_keys(int kb, int vb) { return (uint64_t)kThreads * kpt_for(kb, vb); }
 
 struct Plan {
   int kb, vb;         // key / value bytes (vb = 0 for sortKeys)
@@ -141,6 +134,44 @@ struct ProfScope {  // records [a, b) around the launches issued in its lifetime
 
 uint64_t* g_stamps = nullptr;  // THRS_STAMPS diagnostic builds only (thrs_debug_set_stamps)
 
+// Per-device result of thrs_probe_lds_order: 1 = lane-ordered LDS atomics
+// (fast rank), 0 = ballot-match rank.  -1 = not probed yet.  THRS_RANK=ballot
+// or THRS_RANK=atomic in the environment forces a path.
+int g_rank_mode[64];
+std::once_flag g_rank_once[64];
+
+int probe_rank_mode(hipStream_t stream) {
+#ifdef THRS_FORCE_BALLOT
+  return 0;
+#endif
+  const char* env = getenv("THRS_RANK");
+  if (env && !strcmp(env, "ballot")) return 0;
+  if (env && !strcmp(env, "atomic")) return 1;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  std::call_once(g_rank_once[dev], [&] {
+    g_rank_mode[dev] = 0;
+    // never probe (synchronising) inside a stream capture: stay on the ballot path
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return;
+    uint32_t* d = nullptr;
+    if (hipMalloc(&d, 4) != hipSuccess) return;
+    uint32_t h = 1;
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess) {
+      if (hipMemsetAsync(d, 0, 4, s) == hipSuccess) {
+        hipLaunchKernelGGL(thrs_probe_lds_order, dim3(256), dim3(256), 0, s, d, 64);
+        if (hipGetLastError() == hipSuccess && hipMemcpyAsync(&h, d, 4, hipMemcpyDeviceToHost, s) == hipSuccess &&
+            hipStreamSynchronize(s) == hipSuccess && h == 0)
+          g_rank_mode[dev] = 1;
+      }
+      (void)hipStreamDestroy(s);
+    }
+    (void)hipFree(d);
+  });
+  return g_rank_mode[dev];
+}
+
 template <typename F>
 hipError_t allow_lds(F kernel, size_t bytes) {
   if (bytes <= 65536) return hipSuccess;
@@ -153,8 +184,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
              bool desc, const Plan& plan, hipStream_t stream) {
   using U = typename KeyTraits<KT>::U;
   using VW = typename ValueWord<VB>::T;
-  constexpr int KPT = kpt_for((int)sizeof(U), VB);
-  static_assert(kThreads * KPT <= 65536, "tile positions must fit the 24-bit rank field");
+  using G = PassGeom<sizeof(U), VB>;
 
   char* scratch = static_cast<char*>(tmp);
   uint32_t* hist = reinterpret_cast<uint32_t*>(scratch + kHistOff);
@@ -183,8 +213,8 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     hipLaunchKernelGGL(thrs_scan, dim3(1), dim3(kThreads), 0, stream, hist, base, nPass);
   }
 
-  const size_t lds = (size_t)plan.tileKeys * (sizeof(U) + VB) + (kWaves + 1) * kBins * 4 + 64;
-  auto kernel = thrs_pass<KT, VB, KPT, ST>;
+  const size_t lds = G::LDS_BYTES;
+  auto kernel = probe_rank_mode(stream) ? thrs_pass<KT, VB, ST, true> : thrs_pass<KT, VB, ST, false>;
   if (allow_lds(kernel, lds) != hipSuccess) return THRS_ERROR_HIP;
 
   U* kin = static_cast<U*>(keys);
@@ -194,7 +224,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   for (int p = 0; p < nPass; ++p) {
     ST* next = (p + 1 < nPass) ? status[(p + 1) & 1] : nullptr;
     ProfScope prof(stream, 1);
-    hipLaunchKernelGGL(kernel, dim3((uint32_t)plan.nTiles), dim3(kThreads), lds, stream, kin, kout, vin, vout, n,
+    hipLaunchKernelGGL(kernel, dim3((uint32_t)plan.nTiles), dim3(G::THREADS), lds, stream, kin, kout, vin, vout, n,
                        orderMask, startBits + 8 * p, base + p * kBins, status[p & 1], next, counters + p, err,
                        g_stamps ? g_stamps + (uint64_t)p * plan.nTiles * 8 : nullptr);
     std::swap(kin, kout);
@@ -358,6 +388,15 @@ THRS_API int thrs_debug_set_stamps(void* buf) {
   g_stamps = static_cast<uint64_t*>(buf);
   return THRS_SUCCESS;
 }
+
+// Diagnostic: keys per tile of the pass kernel for (key type, value bytes).
+THRS_API uint64_t thrs_debug_tile_keys(int keyType, int valueBytes) {
+  return valid_key(keyType) ? tile_keys(key_bytes_of(keyType), valueBytes) : 0;
+}
+
+// Which rank path the current device uses (1 = LDS-atomic, 0 = ballot match);
+// runs the one-time probe if needed.
+THRS_API int thrs_rank_mode(void) { return probe_rank_mode(nullptr); }
 
 THRS_API int thrs_malloc(void** ptr, int64_t bytes) {
   if (!ptr) return THRS_ERROR_INVALID_VALUE;

@@ -146,10 +146,10 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* s_w
 // LDS layout [p][d][COPIES]: lane l always adds into copy (l % COPIES), so for
 // COPIES = 32 the bank of every ds_add_u32 is l % 32 -- conflict-free whatever
 // the digits are (random digits into one shared 256-bin table collide ~3-4 way
-// per 32-lane half).  128 KiB of LDS -> one 512-thread workgroup per CU;
+// per 32-lane half).  128 KiB of LDS -> one 1024-thread workgroup per CU (64 KiB of loads in flight);
 // 64-bit keys (8 digits) use 16 copies.  Copies are summed once per workgroup
 // and merged with one device-scope atomic per (p, bin).
-constexpr int kHistThreads = 512;
+constexpr int kHistThreads = 1024;
 template <int KT>
 __global__ __launch_bounds__(kHistThreads) void thrs_hist(const typename KeyTraits<KT>::U* __restrict__ keys,
                                                           uint32_t n, typename KeyTraits<KT>::U orderMask,
@@ -239,32 +239,58 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-// Look-back window: predecessors read per round trip once a walk has started.
-constexpr int kLookWindow = 4;
+// Look-back window: predecessors read per round trip.
+#ifndef THRS_LOOK_WINDOW
+#define THRS_LOOK_WINDOW 8
+#endif
+constexpr int kLookWindow = THRS_LOOK_WINDOW;
 
-// Tile = 256 threads x KPT keys.  Wave w owns the contiguous chunk
-// [w*64*KPT, (w+1)*64*KPT) of the tile; item j of that chunk is 64
-// consecutive keys, one per lane, so (wave, item, lane) order is input order
-// and ranking item by item is stable.
-//
-// Phases (thread tid doubles as "digit d = tid" in the per-digit phases):
+// Tile configuration per (key bytes, value bytes).  A tile is what one
+// workgroup holds in REGISTERS (THREADS x KPT keys) and publishes one status
+// row for; it is written out through an LDS stage of STAGE keys in ROUNDS
+// rounds.  Large tiles keep the look-back short: its depth is about
+// (tiles completed per us) x (cross-XCD visibility latency, ~1-2 us under load)
+// and every step reads one 1 KiB status row.
+#ifndef THRS_K4V0_CFG
+#define THRS_K4V0_CFG 8, 32, 1, 4
+#endif
+template <int KB, int VB> struct PassCfg;
+template <> struct PassCfg<4, 0> {
+  static constexpr int CFG[4] = {THRS_K4V0_CFG};  // waves, keys/thread, rounds, min waves per SIMD
+  static constexpr int WAVES = CFG[0], KPT = CFG[1], ROUNDS = CFG[2], WPE = CFG[3];
+};
+template <> struct PassCfg<4, 4> { static constexpr int WAVES = 16, KPT = 16, ROUNDS = 4, WPE = 4; };
+template <> struct PassCfg<4, 8> { static constexpr int WAVES = 16, KPT = 16, ROUNDS = 8, WPE = 4; };
+template <> struct PassCfg<4, 16> { static constexpr int WAVES = 16, KPT = 8, ROUNDS = 8, WPE = 4; };
+template <> struct PassCfg<8, 0> { static constexpr int WAVES = 16, KPT = 16, ROUNDS = 4, WPE = 4; };
+template <> struct PassCfg<8, 4> { static constexpr int WAVES = 16, KPT = 16, ROUNDS = 8, WPE = 4; };
+template <> struct PassCfg<8, 8> { static constexpr int WAVES = 16, KPT = 16, ROUNDS = 8, WPE = 4; };
+template <> struct PassCfg<8, 16> { static constexpr int WAVES = 16, KPT = 8, ROUNDS = 8, WPE = 4; };
+
+template <int KB, int VB> struct PassGeom {
+  static constexpr int WAVES = PassCfg<KB, VB>::WAVES, KPT = PassCfg<KB, VB>::KPT, ROUNDS = PassCfg<KB, VB>::ROUNDS;
+  static constexpr int WPE = PassCfg<KB, VB>::WPE;
+  static constexpr int THREADS = 64 * WAVES;
+  static constexpr uint32_t TILE = (uint32_t)THREADS * KPT;
+  static constexpr uint32_t STAGE = TILE / ROUNDS;
+  static constexpr uint32_t LDS_BYTES = STAGE * (KB + VB) + (WAVES + 1) * kBins * 4 + 16 * 4;
+  static_assert(TILE <= 65536, "slots are kept as 16-bit halves");
+  static_assert((STAGE & (STAGE - 1)) == 0 && STAGE % THREADS == 0, "stage must be a power of two");
+};
+
+// Phases (threads tid < 256 double as "digit d = tid" in the per-digit steps):
 //   A  tile id, load keys (+values) into registers
 //   B  per-wave digit histogram (LDS atomics) -> tile counts; publish the
-//      tile aggregate and ISSUE the look-back load; local exclusive scan
-//   C  rank item by item (wave64 ballot match + per-wave running counters that
-//      start at the wave's local offsets) and scatter straight into the LDS
-//      tile; the look-back load is in flight meanwhile
-//   D  finish the look-back -> global offset of digit d
-//   E  coalesced write-out of the sorted LDS tile
-//
-// LDS (dynamic, 16-B aligned):
-//   stage_k [T]       keys in tile-sorted order
-//   stage_v [T]       values in tile-sorted order (pairs only)
-//   s_cnt   [4][256]  per-wave digit counts -> per-wave running offsets
-//   s_gofs  [256]     global dst of local slot 0 of digit d (base + excl - localStart)
-//   s_misc  [8]       tile id, scan scratch
-template <int KT, int VB, int KPT, typename ST>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void thrs_pass(
+//      tile aggregate; local exclusive scan -> per-wave running offsets
+//   C  rank item by item (wave64 ballot match + per-wave running counters):
+//      every key gets its final slot in the tile's sorted order
+//   D  decoupled look-back (window of kLookWindow rows per round trip)
+//      -> global offset of digit d
+//   E  ROUNDS x { scatter keys whose slot falls in this round into the LDS
+//      stage, coalesced write-out of the stage }
+template <int KT, int VB, typename ST, bool ATOMIC_RANK>
+__global__ __launch_bounds__((PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::THREADS))
+__attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::WPE))) void thrs_pass(
     const typename KeyTraits<KT>::U* __restrict__ keysIn, typename KeyTraits<KT>::U* __restrict__ keysOut,
     const typename ValueWord<VB>::T* __restrict__ valsIn, typename ValueWord<VB>::T* __restrict__ valsOut,
     uint32_t n, typename KeyTraits<KT>::U orderMask, int shift, const uint32_t* __restrict__ digitBase,
@@ -272,13 +298,15 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     uint32_t* __restrict__ errFlag, uint64_t* __restrict__ stamps) {
   using U = typename KeyTraits<KT>::U;
   using VW = typename ValueWord<VB>::T;
-  constexpr uint32_t T = kThreads * KPT;
-  constexpr uint32_t CHUNK = 64 * KPT;
+  using G = PassGeom<sizeof(U), VB>;
+  constexpr int WAVES = G::WAVES, KPT = G::KPT, ROUNDS = G::ROUNDS, THREADS = G::THREADS;
+  constexpr uint32_t T = G::TILE, STAGE = G::STAGE, CHUNK = 64 * KPT;
+  constexpr int STAGE_SHIFT = __builtin_ctz(STAGE);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   U* stage_k = reinterpret_cast<U*>(smem);
-  VW* stage_v = reinterpret_cast<VW*>(smem + T * sizeof(U));
-  uint32_t* s_cnt = reinterpret_cast<uint32_t*>(smem + T * sizeof(U) + (VB ? T * VB : 0));
-  uint32_t* s_gofs = s_cnt + kWaves * kBins;
+  VW* stage_v = reinterpret_cast<VW*>(smem + STAGE * sizeof(U));
+  uint32_t* s_cnt = reinterpret_cast<uint32_t*>(smem + STAGE * (sizeof(U) + VB));  // [WAVES][256]
+  uint32_t* s_gofs = s_cnt + WAVES * kBins;
   uint32_t* s_misc = s_gofs + kBins;
 
   // Diagnostic builds (-DTHRS_STAMPS) record s_memrealtime (100 MHz) per
@@ -299,9 +327,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
   const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
 
   // ---- A: dynamic tile id (start order, so every tile we wait on is resident)
-  if (tid == 0) s_misc[0] = atomicAdd(tileCounter, 1u);
-#pragma unroll
-  for (int i = 0; i < kWaves; ++i) s_cnt[i * kBins + tid] = 0;
+  if (tid == 0) {
+    s_misc[0] = atomicAdd(tileCounter, 1u);
+    s_misc[1] = s_misc[2] = s_misc[3] = 0;  // diagnostic maxima (THRS_STAMPS)
+  }
+  for (uint32_t i = tid; i < (uint32_t)(WAVES * kBins); i += THREADS) s_cnt[i] = 0;
   lds_barrier();
   const uint32_t tile = s_misc[0];
 #ifdef THRS_STAMPS
@@ -338,15 +368,16 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
       else v[j] = VW{};
     }
   }
-  const uint32_t myBase = digitBase[tid];  // global base of digit `tid`, used in D
+  const uint32_t d = tid & 255u;
+  const uint32_t myBase = digitBase[d];  // global base of digit d, used in D
 
   auto digit_of = [&](U key, int j) -> uint32_t {
-    uint32_t d = (uint32_t)((KeyTraits<KT>::bits(key) ^ orderMask) >> shift) & 0xFFu;
-    if (!full) d = (w * CHUNK + j * 64 + lane < valid) ? d : 0xFFu;  // padding sorts after every real key
-    return d;
+    uint32_t dd = (uint32_t)((KeyTraits<KT>::bits(key) ^ orderMask) >> shift) & 0xFFu;
+    if (!full) dd = (w * CHUNK + j * 64 + lane < valid) ? dd : 0xFFu;  // padding sorts after every real key
+    return dd;
   };
 
-  // ---- B: per-wave histogram (order-free LDS atomics)
+  // ---- B: per-wave histogram (order-free LDS atomics) -> tile counts
   uint32_t* cnt = s_cnt + w * kBins;
 #pragma unroll
   for (int j = 0; j < KPT; ++j)
@@ -354,117 +385,147 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
   lds_barrier();
   THRS_STAMP(2);
 
-  const uint32_t d = tid;
-  const uint32_t c0 = s_cnt[0 * kBins + d], c1 = s_cnt[1 * kBins + d];
-  const uint32_t c2 = s_cnt[2 * kBins + d], c3 = s_cnt[3 * kBins + d];
-  const uint32_t tot = c0 + c1 + c2 + c3;
-  const uint32_t realTot = (d == 255u) ? tot - (T - valid) : tot;
+  uint32_t tot = 0, realTot = 0;
   ST* myStatus = status + (uint64_t)tile * kBins + d;
-  if (tile != 0) store_agent(myStatus, Status<ST>::agg(realTot));
-  else store_agent(myStatus, Status<ST>::pre(realTot));
-  ST look = 0;
-  if (tile != 0) look = load_agent(status + (uint64_t)(tile - 1) * kBins + d);
-
-  // local exclusive scan over digits (wave scan + 4 wave totals through LDS)
-  const uint32_t incl = wave_incl_scan(tot, lane);
-  if (lane == 63) s_misc[4 + w] = incl;
-  lds_barrier();
-  const uint32_t w0 = s_misc[4], w1 = s_misc[5], w2 = s_misc[6];
-  const uint32_t localStart = incl - tot + (w > 0 ? w0 : 0u) + (w > 1 ? w1 : 0u) + (w > 2 ? w2 : 0u);
-  s_cnt[0 * kBins + d] = localStart;
-  s_cnt[1 * kBins + d] = localStart + c0;
-  s_cnt[2 * kBins + d] = localStart + c0 + c1;
-  s_cnt[3 * kBins + d] = localStart + c0 + c1 + c2;
+  if (tid < 256) {
+#pragma unroll
+    for (int ww = 0; ww < WAVES; ++ww) tot += s_cnt[ww * kBins + d];
+    realTot = (d == 255u) ? tot - (T - valid) : tot;
+    if (tile != 0) store_agent(myStatus, Status<ST>::agg(realTot));
+    else store_agent(myStatus, Status<ST>::pre(realTot));
+  }
+  // local exclusive scan over the 256 digits (waves 0-3)
+  uint32_t localStart = 0;
+  {
+    const uint32_t incl = wave_incl_scan(tot, lane);
+    if (tid < 256 && lane == 63) s_misc[4 + w] = incl;
+    lds_barrier();
+    if (tid < 256) {
+      const uint32_t w0 = s_misc[4], w1 = s_misc[5], w2 = s_misc[6];
+      localStart = incl - tot + (w > 0 ? w0 : 0u) + (w > 1 ? w1 : 0u) + (w > 2 ? w2 : 0u);
+      uint32_t run = localStart;
+#pragma unroll
+      for (int ww = 0; ww < WAVES; ++ww) {
+        const uint32_t c = s_cnt[ww * kBins + d];
+        s_cnt[ww * kBins + d] = run;
+        run += c;
+      }
+    }
+  }
   lds_barrier();
   THRS_STAMP(3);
 
-  // ---- C: stable rank = running per-wave offset + peers in lower lanes; the
-  // slot is final, so the key goes straight into the sorted LDS tile
+  // ---- C: stable rank = running per-wave offset + same-digit keys in lower
+  // lanes of the item.  ATOMIC_RANK: one ds_add_rtn_u32 per key -- with every
+  // lane active, conflicting lanes of one LDS atomic are serviced in lane
+  // order on gfx950, so the returned counter IS the stable slot (verified at
+  // run time per device by thrs_probe_lds_order; otherwise the ballot match).
+  uint32_t sl[(KPT + 1) / 2];  // final slots, two 16-bit halves per register
+#pragma unroll
+  for (int j = 0; j < (KPT + 1) / 2; ++j) sl[j] = 0;
 #pragma unroll
   for (int j = 0; j < KPT; ++j) {
     pin(k[j]);  // keep item j's digit/address math inside iteration j (register pressure)
     const uint32_t dj = digit_of(k[j], j);
-    uint32_t mlo, mhi;
-    match_digit(dj, mlo, mhi);
-    const uint32_t c = cnt[dj];
-    const uint32_t slot = __builtin_amdgcn_mbcnt_hi(mhi, __builtin_amdgcn_mbcnt_lo(mlo, c));
-    cnt[dj] = __builtin_popcount(mhi) + __builtin_popcount(mlo) + c;
-    stage_k[slot] = k[j];
-    if constexpr (VB != 0) stage_v[slot] = v[j];
+    uint32_t slot;
+    if constexpr (ATOMIC_RANK) {
+      slot = __hip_atomic_fetch_add(&cnt[dj], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else {
+      uint32_t mlo, mhi;
+      match_digit(dj, mlo, mhi);
+      const uint32_t c = cnt[dj];
+      slot = __builtin_amdgcn_mbcnt_hi(mhi, __builtin_amdgcn_mbcnt_lo(mlo, c));
+      cnt[dj] = __builtin_popcount(mhi) + __builtin_popcount(mlo) + c;
+    }
+    sl[j / 2] |= slot << (16 * (j & 1));
+    pin(sl[j / 2]);  // materialise the slot now (else it is sunk to phase E, keeping masks alive)
     __builtin_amdgcn_sched_barrier(0);
   }
   THRS_STAMP(4);
 
-  // ---- D: finish the decoupled look-back for digit d.  Walks read a window
-  // of kLookWindow predecessors per round trip; a not-yet-published word stops
-  // the window and is re-polled.
-  uint32_t excl = 0;
+  // ---- D: decoupled look-back for digit d, kLookWindow rows per round trip;
+  // a not-yet-published word stops the window and is re-polled.
+  if (tid < 256) {
+    uint32_t excl = 0;
 #ifdef THRS_STAMPS
-  uint32_t dbgRounds = 0;
-  if (tid == 0) { s_misc[1] = 0; s_misc[2] = 0; s_misc[3] = 0; }
+    uint32_t dbgRounds = 0;
 #endif
-  if (tile != 0) {
-    int64_t j = (int64_t)tile - 1;  // next predecessor to consume
-    uint32_t spins = 0;
-    ST win[kLookWindow];
-    win[0] = look;
-    int have = 1;
-    while (true) {
-      bool done = false, stall = false;
+    if (tile != 0) {
+      int64_t j = (int64_t)tile - 1;  // next predecessor to consume
+      uint32_t spins = 0;
+      while (true) {
+        ST win[kLookWindow];
+        // 32-bit byte offsets from the uniform base -> saddr loads, one VGPR each
+        const uint32_t off0 = ((uint32_t)j * kBins + d) * (uint32_t)sizeof(ST);
 #pragma unroll
-      for (int q = 0; q < kLookWindow; ++q) {
-        if (q < have && !done && !stall) {
-          const ST sw = win[q];
-          if (sw == 0) {
-            stall = true;
-          } else {
-            excl += Status<ST>::val(sw);
-            if (Status<ST>::is_pre(sw)) done = true;
-            else --j;
+        for (int q = 0; q < kLookWindow; ++q)
+          win[q] = (j - q >= 0) ? load_agent(reinterpret_cast<const ST*>(reinterpret_cast<const char*>(status) +
+                                                                         (off0 - (uint32_t)q * kBins * sizeof(ST))))
+                                : (ST)0;
+#ifdef THRS_STAMPS
+        ++dbgRounds;
+#endif
+        bool done = false, stall = false;
+#pragma unroll
+        for (int q = 0; q < kLookWindow; ++q) {
+          if (!done && !stall) {
+            const ST sw = win[q];
+            if (sw == 0) {
+              stall = true;
+            } else {
+              excl += Status<ST>::val(sw);
+              if (Status<ST>::is_pre(sw)) done = true;
+              else --j;
+            }
           }
         }
-      }
-      if (done) break;
-      if (stall) {
-        if (++spins > (1u << 22)) {  // bounded spin: never hang the GPU
-          atomicOr(errFlag, 1u);
-          break;
+        if (done) break;
+        if (stall) {
+          if (++spins > (1u << 22)) {  // bounded spin: never hang the GPU
+            atomicOr(errFlag, 1u);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
         }
-        __builtin_amdgcn_s_sleep(1);
       }
+      store_agent(myStatus, Status<ST>::pre(excl + realTot));
 #ifdef THRS_STAMPS
-      ++dbgRounds;
+      atomicMax(&s_misc[1], dbgRounds);
+      atomicMax(&s_misc[2], spins);
+      atomicMax(&s_misc[3], (uint32_t)(tile - 1 - j));
 #endif
-      // (re)load the next window [j, j-1, ...] (j >= 0: tile 0 is always a prefix)
-#pragma unroll
-      for (int q = 0; q < kLookWindow; ++q)
-        if (j - q >= 0) win[q] = load_agent(status + (uint64_t)(j - q) * kBins + d);
-      have = (int)min<int64_t>(kLookWindow, j + 1);
     }
-    store_agent(myStatus, Status<ST>::pre(excl + realTot));
-#ifdef THRS_STAMPS
-    atomicMax(&s_misc[1], dbgRounds);
-    atomicMax(&s_misc[2], spins);
-    atomicMax(&s_misc[3], (uint32_t)(tile - 1 - j));
-#endif
+    s_gofs[d] = myBase + excl - localStart;
+    if (statusNext) statusNext[(uint64_t)tile * kBins + d] = 0;  // ready for the next pass
   }
-  s_gofs[d] = myBase + excl - localStart;
-  if (statusNext) statusNext[(uint64_t)tile * kBins + d] = 0;  // ready for the next pass
   lds_barrier();
   THRS_STAMP(5);
 
-  // ---- E: coalesced write-out: sorted slot i -> s_gofs[digit] + i
+  // ---- E: ROUNDS x (scatter this round's slots into the stage, write it out)
+#pragma unroll 1
+  for (int r = 0; r < ROUNDS; ++r) {
 #pragma unroll
-  for (int j = 0; j < KPT; ++j) {
-    const uint32_t i = j * kThreads + tid;
-    if (full || i < valid) {
-      const U key = stage_k[i];
-      const uint32_t dd = (uint32_t)((KeyTraits<KT>::bits(key) ^ orderMask) >> shift) & 0xFFu;
-      const uint32_t dst = s_gofs[dd] + i;
-      keysOut[dst] = key;
-      if constexpr (VB != 0) valsOut[dst] = stage_v[i];
+    for (int j = 0; j < KPT; ++j) {
+      const uint32_t slot = (sl[j / 2] >> (16 * (j & 1))) & 0xFFFFu;
+      if ((slot >> STAGE_SHIFT) == (uint32_t)r) {
+        stage_k[slot & (STAGE - 1)] = k[j];
+        if constexpr (VB != 0) stage_v[slot & (STAGE - 1)] = v[j];
+      }
     }
-    if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);  // bound live 64-bit store addresses
+    lds_barrier();
+#pragma unroll
+    for (int j = 0; j < (int)(STAGE / THREADS); ++j) {
+      const uint32_t i = j * THREADS + tid;
+      const uint32_t slot = (uint32_t)r * STAGE + i;
+      if (full || slot < valid) {
+        const U key = stage_k[i];
+        const uint32_t dd = (uint32_t)((KeyTraits<KT>::bits(key) ^ orderMask) >> shift) & 0xFFu;
+        const uint32_t dst = s_gofs[dd] + slot;
+        keysOut[dst] = key;
+        if constexpr (VB != 0) valsOut[dst] = stage_v[i];
+      }
+    }
+    if (r + 1 < ROUNDS) lds_barrier();
   }
 #ifdef THRS_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -474,6 +535,36 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
                                       ((uint64_t)min(s_misc[3], 65535u) << 24) | ((uint64_t)s_misc[2] << 40);
 #endif
 #undef THRS_STAMP
+}
+
+// ================================================================ self-probe
+// Does ds_add_rtn_u32 hand out values in lane order when several lanes of one
+// fully active wave hit the same LDS word?  Compared against the ballot-match
+// rank over random, heavily conflicting and all-equal digit patterns.
+// *bad counts disagreeing lanes (0 => ATOMIC_RANK is safe on this device).
+__global__ __launch_bounds__(256) void thrs_probe_lds_order(uint32_t* bad, int iters) {
+  __shared__ uint32_t cnt[4][kBins];
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t b = 0;
+  uint64_t x = (blockIdx.x * 256ull + threadIdx.x + 1) * 0x9E3779B97F4A7C15ull;
+  for (int it = 0; it < iters; ++it) {
+    for (uint32_t i = lane; i < (uint32_t)kBins; i += 64) cnt[w][i] = (uint32_t)it;
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    x ^= x >> 31;
+    x *= 0xBF58476D1CE4E5B9ull;
+    x ^= x >> 29;
+    uint32_t d = (uint32_t)(x >> 24) & 0xFFu;
+    const int mode = it & 3;
+    if (mode == 1) d &= 0x3u;
+    if (mode == 2) d = 0x5Au;
+    if (mode == 3) d &= 0x1Fu;
+    uint32_t mlo, mhi;
+    match_digit(d, mlo, mhi);
+    const uint32_t want = (uint32_t)it + __builtin_amdgcn_mbcnt_hi(mhi, __builtin_amdgcn_mbcnt_lo(mlo, 0u));
+    const uint32_t got = __hip_atomic_fetch_add(&cnt[w][d], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    b += got != want;
+  }
+  if (b) atomicAdd(bad, b);
 }
 
 }  // namespace thrs_dev

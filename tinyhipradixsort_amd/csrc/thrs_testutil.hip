@@ -124,6 +124,18 @@ __global__ void k_pairs(int keyType, int desc, int valueBytes, const void* keysI
   if (halves) atomicAdd(&out[4], halves);
 }
 
+// Calibration copies for rocprofv3 byte counters (FETCH_SIZE/WRITE_SIZE are
+// only calibrated for 16-B streaming accesses on gfx950): known byte counts at
+// 4-B and 16-B per lane.
+__global__ void k_copy_u32(uint32_t* __restrict__ dst, const uint32_t* __restrict__ src, uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    dst[i] = src[i];
+}
+__global__ void k_copy_u128(uint4* __restrict__ dst, const uint4* __restrict__ src, uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    dst[i] = src[i];
+}
+
 inline int grid_for(uint64_t n) {
   uint64_t g = (n + 255) / 256;
   if (g > 8192) g = 8192;
@@ -145,6 +157,14 @@ THRS_API int thrsu_fill_keys(int keyType, void* out, uint64_t n, uint64_t start,
 THRS_API int thrsu_iota(int valueBytes, void* out, uint64_t n, uint64_t start, hipStream_t stream) {
   if (!n) return THRS_SUCCESS;
   hipLaunchKernelGGL(k_iota, dim3(grid_for(n)), dim3(256), 0, stream, valueBytes, out, n, start);
+  return ok(hipGetLastError());
+}
+
+THRS_API int thrsu_copy(void* dst, const void* src, uint64_t bytes, int width16, hipStream_t stream) {
+  if (width16)
+    hipLaunchKernelGGL(k_copy_u128, dim3(4096), dim3(256), 0, stream, (uint4*)dst, (const uint4*)src, bytes / 16);
+  else
+    hipLaunchKernelGGL(k_copy_u32, dim3(4096), dim3(256), 0, stream, (uint32_t*)dst, (const uint32_t*)src, bytes / 4);
   return ok(hipGetLastError());
 }
 

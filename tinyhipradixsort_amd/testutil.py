@@ -23,7 +23,8 @@ def tlib() -> ctypes.CDLL:
         L.thrsu_check_sorted.argtypes = [i32, i32, vp, u64, i32, i32, ull_p, vp]
         L.thrsu_fingerprint.argtypes = [i32, vp, u64, ull_p, vp]
         L.thrsu_check_pairs.argtypes = [i32, i32, i32, vp, vp, vp, u64, i32, i32, ull_p, vp]
-        for f in ("thrsu_fill_keys", "thrsu_iota", "thrsu_check_sorted", "thrsu_fingerprint", "thrsu_check_pairs"):
+        L.thrsu_copy.argtypes = [vp, vp, u64, i32, vp]
+        for f in ("thrsu_copy", "thrsu_fill_keys", "thrsu_iota", "thrsu_check_sorted", "thrsu_fingerprint", "thrsu_check_pairs"):
             getattr(L, f).restype = i32
         _tl = L
     return _tl
@@ -75,3 +76,8 @@ def expected_index_fingerprint(n: int) -> tuple[int, int]:
             z = z ^ (z >> np.uint64(31))
         x ^= int(np.bitwise_xor.reduce(z)) if z.size else 0
     return s, x
+
+
+def copy(dst, src, nbytes: int, width16: bool = True, stream=None):
+    """Streaming copy with 16-B (or 4-B) lanes: rocprofv3 byte-counter calibration."""
+    _check(tlib().thrsu_copy(_ptr(dst), _ptr(src), nbytes, int(width16), _stream(stream)))
