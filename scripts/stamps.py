@@ -23,7 +23,7 @@ import tinyhipradixsort_amd as T  # noqa: E402
 from tinyhipradixsort_amd import testutil as TU  # noqa: E402
 from sweep import WL, load  # noqa: E402
 
-NAMES = ["tileid", "load+hist", "agg+scan", "rank+scatter", "lookback_rest", "writeout"]
+NAMES = ["tileid", "load+hist", "agg+scan", "rank", "lookback", "writeout"]
 
 
 def main():
