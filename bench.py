@@ -57,6 +57,8 @@ def parse():
     p.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--quiet", action="store_true")
+    p.add_argument("--force-dist", action="store_true",
+                   help="run the bucket-exchange path even at world size 1 (RCCL smoke test)")
     return p.parse_args()
 
 
@@ -119,8 +121,13 @@ def main():
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     torch.cuda.set_device(local_rank)
     dist = None
-    if world > 1:
+    use_dist = world > 1 or args.force_dist
+    if use_dist:
         import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
     import tinyhipradixsort_amd as T
@@ -137,7 +144,7 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    if world == 1:
+    if not use_dist:
         cfg = T.RadixSort.Config(keyType=T.KeyType(kt), valueType={0: T.ValueType.U32, 4: T.ValueType.U32,
                                                                    8: T.ValueType.U64, 16: T.ValueType.U128}[vb])
         rs = T.RadixSort([], cfg)
@@ -197,11 +204,56 @@ def main():
         phase = None
     else:
         from tinyhipradixsort_amd import dist as D
-        sorter = D.DistributedRadixSort(key_type=kt, value_bytes=vb, n_local_max=n, group=None)
-        prof, recycled, elapsed, phase = sorter.bench(n, steps, warmup, args.pool)
+        vt = None if not vb else {4: T.ValueType.U32, 8: T.ValueType.U64, 16: T.ValueType.U128}[vb]
+        sorter = D.DistributedRadixSort(key_type=kt, value_type=vt)
+        # inputs: rank r of step i holds draws (i*world + r)*n + 1 .. of the
+        # splitmix64 stream; values = global index.  The exchange sort is out
+        # of place (inputs are never modified), so a pool of 2 stays fresh.
+        pool = max(1, min(2, args.pool))
+        keys, vals = [], []
+        for i in range(pool):
+            kbuf = torch.empty(n * kb, dtype=torch.uint8, device="cuda")
+            TU.fill_keys(kt, kbuf, n, start=(i * world + rank) * n)
+            keys.append(kbuf)
+            if vb:
+                vbuf = torch.empty(n * vb, dtype=torch.uint8, device="cuda")
+                TU.iota(vb, vbuf, n, start=rank * n)
+                vals.append(vbuf)
+        torch.cuda.synchronize()
+        out = None
+
+        def step(i, timings=None):
+            j = i % pool
+            return sorter.sort(keys[j], n, vals[j] if vb else None, 0, kb * 8, timings=timings)
+
+        for i in range(warmup):
+            out = step(i)
+        phase_s = {}
+        out = step(0, phase_s)                     # untimed per-phase breakdown (synchronising)
+        del out
+        torch.cuda.synchronize()
+        T.profile_enable(True)
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            out = step(warmup + i)
+        torch.cuda.synchronize()
+        barrier()
+        t1 = time.perf_counter()
+        prof = T.profile_read()
+        T.profile_enable(False)
+        ko, _vo, n_out = out
+        bad = TU.count_unsorted(kt, ko, n_out, 0, kb * 8)
+        if bad:
+            raise SystemExit(f"bench: rank {rank} output is not sorted ({bad} inversions)")
+        recycled = False
+        elapsed = t1 - t0
         scaling = "weak"
         global_keys = n * world
         parallelism = f"bucket-exchange x{world} (RCCL all_gather + all_to_all)"
+        phase = {k: round(v * 1e3, 3) for k, v in phase_s.items()}
+        phase["n_out_rank0"] = n_out if rank == 0 else None
 
     # max over ranks
     el = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
@@ -236,7 +288,7 @@ def main():
         out = {"metric": METRIC, "value": round(value, 3), "unit": "Gkeys/s", "n_gpus": world, "steps": steps,
                "warmup": warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
                "scaling": scaling, "vs_baseline": None, "dtype": DTYPE[kt], "data": "synthetic",
-               "config": {"workload": WORKLOADS[wl][3] if world == 1 else
+               "config": {"workload": WORKLOADS[wl][3] if not use_dist else
                           f"{DTYPE[kt]} keys, {n} per GPU x {world} GPUs, bucket-exchange sort",
                           "keys_per_gpu": n, "global_keys": global_keys, "key": DTYPE[kt],
                           "value": None if not vb else f"{vb}B index payload", "bits": [0, kb * 8],

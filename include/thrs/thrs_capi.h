@@ -89,6 +89,19 @@ int thrs_sort_keys(const thrs_config* config, void* inputKeyBuffer, uint32_t num
 int thrs_sort_pairs(const thrs_config* config, void* inputKeyBuffer, void* inputValueBuffer, uint32_t numberOfInputs,
                     void* temporaryBuffer, int startBits, int endBits, hipStream_t stream);
 
+/* Multi-GPU building block (no reference counterpart -- the reference is
+ * single-GPU): ONE stable LSD pass by the 8-bit digit at
+ * bitLocation (the reference's per-pass digit, tinyhipradixsort.hpp:862-867,
+ * kernel.cu:56-77 transform and descending flip), OUT OF PLACE keysIn ->
+ * keysOut (valuesIn -> valuesOut when valuesIn != NULL), plus the digit's 256
+ * bucket counts, in output order, written to the device array counts[256].
+ * After it, bucket d occupies keysOut[sum(counts[0..d)) .. +counts[d]), in
+ * input order -- the send segments of the bucket exchange.  temporaryBuffer
+ * needs the pSumBuffer bytes of thrs_get_temporary_buffer_bytes(n). */
+int thrs_partition_pass(const thrs_config* config, const void* keysIn, const void* valuesIn, uint32_t numberOfInputs,
+                        void* temporaryBuffer, void* keysOut, void* valuesOut, int bitLocation, uint32_t* counts,
+                        hipStream_t stream);
+
 /* Synchronising debug check: THRS_ERROR_LOOKBACK_TIMEOUT if any look-back of
  * the last sort that used `temporaryBuffer` gave up its bounded spin (no
  * reference counterpart; the reference would hang instead). */

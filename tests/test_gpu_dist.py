@@ -1,0 +1,118 @@
+"""GPU side of the bucket exchange (tinyhipradixsort_amd/dist.py):
+
+* thrs_partition_pass (the partition step) against the oracle: output ==
+  a stable argsort by the digit, counts == the digit's bincount;
+* a 2-rank exchange with the real HIP local steps, both ranks on cuda:0 (the
+  one-GPU box): gloo carries the collectives through host memory, the
+  partition and the local sort run in libthrs.so; expected = ONE oracle LSD
+  sort of the concatenation (global index payload -> stability checked).
+RCCL itself is exercised by bench.py --gpus N (torch.distributed.run)."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from oracle import oracle as O  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+NP_KEY = {O.U32: np.uint32, O.U64: np.uint64, O.F32: np.uint32, O.F64: np.uint64}
+
+
+@pytest.mark.parametrize("kt,vb,desc,bit,n", [
+    (O.U32, 0, False, 24, 100003), (O.U32, 4, False, 0, 70001), (O.F32, 4, True, 24, 65536 + 3),
+    (O.U64, 8, False, 56, 50000), (O.F64, 16, False, 40, 33333), (O.U32, 4, False, 8, 1),
+])
+def test_partition_pass_vs_oracle(gpu, kt, vb, desc, bit, n):
+    import tinyhipradixsort_amd as T
+    torch = gpu
+    k = O.randomize_np(kt, O.splitmix64_stream(7, n))
+    v = np.arange(n * max(vb, 1), dtype=np.uint8).reshape(n, max(vb, 1))[:, :vb] if vb else None
+    cfg = T.RadixSort.Config(keyType=T.KeyType(kt),
+                             valueType={0: T.ValueType.U32, 4: T.ValueType.U32, 8: T.ValueType.U64,
+                                        16: T.ValueType.U128}[vb],
+                             sortOrder=T.SortOrder.Descending if desc else T.SortOrder.Ascending)
+    rs = T.RadixSort([], cfg)
+    kd = torch.from_numpy(k.view(np.uint8).copy()).cuda()
+    vd = torch.from_numpy(np.ascontiguousarray(v).reshape(-1).copy()).cuda() if vb else None
+    ko, vo = torch.empty_like(kd), (torch.empty_like(vd) if vb else None)
+    counts = torch.empty(256, dtype=torch.int32, device="cuda")
+    tmp = torch.empty(rs.getTemporaryBufferBytes(n).pSumBuffer, dtype=torch.uint8, device="cuda")
+    rs.partitionPass(kd, vd, n, tmp, ko, vo, bit, counts)
+    torch.cuda.synchronize()
+    rs.checkDeviceError(tmp)
+    d = ((O.key_bits_np(kt, k, desc) >> np.uint64(bit)) & np.uint64(0xFF)).astype(np.int64)
+    order = np.argsort(d, kind="stable")
+    assert np.array_equal(counts.cpu().numpy().astype(np.int64), np.bincount(d, minlength=256))
+    assert np.array_equal(ko.cpu().numpy().view(NP_KEY[kt]), k[order])
+    if vb:
+        assert np.array_equal(vo.cpu().numpy().reshape(n, vb), v[order])
+    # the input is untouched (out of place)
+    assert np.array_equal(kd.cpu().numpy().view(NP_KEY[kt]), k)
+
+
+def test_partition_pass_rejects(gpu):
+    import tinyhipradixsort_amd as T
+    torch = gpu
+    rs = T.RadixSort([], T.RadixSort.Config())
+    kd = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    counts = torch.empty(256, dtype=torch.int32, device="cuda")
+    tmp = torch.empty(rs.getTemporaryBufferBytes(16).pSumBuffer, dtype=torch.uint8, device="cuda")
+    with pytest.raises(T.ThrsError):
+        rs.partitionPass(kd, None, 16, tmp, kd, None, 0, counts)       # in place
+    with pytest.raises(T.ThrsError):
+        rs.partitionPass(kd, None, 16, tmp, torch.empty_like(kd), None, 32, counts)   # past the key width
+
+
+def _worker(rank, world, port, out_dir):
+    import torch
+    import torch.distributed as dist
+    from tinyhipradixsort_amd import dist as D
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        cases = [(O.U32, 4, [300001, 250007], 0, 32, False), (O.F32, 0, [65536 * 3, 1000], 0, 32, True),
+                 (O.U64, 8, [120000, 90001], 16, 48, False)]
+        for ci, (kt, vb, sizes, s, e, desc) in enumerate(cases):
+            glob = O.randomize_np(kt, O.splitmix64_stream(ci * 10 ** 6, sum(sizes)))
+            lo = sum(sizes[:rank])
+            kd = torch.from_numpy(glob[lo:lo + sizes[rank]].view(np.uint8).copy()).cuda()
+            vd = None
+            if vb:
+                idx = np.arange(lo, lo + sizes[rank], dtype=np.uint32 if vb == 4 else np.uint64)
+                vd = torch.from_numpy(idx.view(np.uint8).copy()).cuda()
+            sorter = D.DistributedRadixSort(kt, None if not vb else {4: 0, 8: 1}[vb], int(desc))
+            ko, vo, n_out = sorter.sort(kd, sizes[rank], vd, s, e)
+            torch.cuda.synchronize()
+            np.save(os.path.join(out_dir, f"c{ci}_r{rank}_k.npy"), ko.cpu().numpy()[:n_out * O.KEY_BYTES[kt]])
+            if vb:
+                np.save(os.path.join(out_dir, f"c{ci}_r{rank}_v.npy"), vo.cpu().numpy()[:n_out * vb])
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_ranks_one_gpu(gpu, tmp_path):
+    import torch.multiprocessing as mp
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    mp.spawn(_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    cases = [(O.U32, 4, [300001, 250007], 0, 32, False), (O.F32, 0, [65536 * 3, 1000], 0, 32, True),
+             (O.U64, 8, [120000, 90001], 16, 48, False)]
+    for ci, (kt, vb, sizes, s, e, desc) in enumerate(cases):
+        glob = O.randomize_np(kt, O.splitmix64_stream(ci * 10 ** 6, sum(sizes)))
+        idx = np.arange(sum(sizes), dtype=np.uint32 if vb == 4 else np.uint64) if vb else None
+        ek, ev = O.lsd_sort(kt, glob, idx, s, e, desc)
+        gk = np.concatenate([np.load(tmp_path / f"c{ci}_r{r}_k.npy") for r in range(2)]).view(NP_KEY[kt])
+        assert np.array_equal(gk, ek), ci
+        if vb:
+            gv = np.concatenate([np.load(tmp_path / f"c{ci}_r{r}_v.npy") for r in range(2)]).view(idx.dtype)
+            assert np.array_equal(gv, ev), ci
+        # balanced to a bucket's granularity on uniform input
+        n0 = np.load(tmp_path / f"c{ci}_r0_k.npy").size // O.KEY_BYTES[kt]
+        assert abs(n0 - sum(sizes) / 2) < sum(sizes) * 0.02

@@ -66,6 +66,7 @@ def lib() -> ctypes.CDLL:
         L.thrs_sort_keys.argtypes = [ctypes.POINTER(_CConfig), vp, u32, vp, i32, i32, vp]
         L.thrs_sort_pairs.argtypes = [ctypes.POINTER(_CConfig), vp, vp, u32, vp, i32, i32, vp]
         L.thrs_check_device_error.argtypes = [vp, vp]
+        L.thrs_partition_pass.argtypes = [ctypes.POINTER(_CConfig), vp, vp, u32, vp, vp, vp, i32, vp, vp]
         L.thrs_malloc.argtypes = [ctypes.POINTER(vp), i64]
         L.thrs_free.argtypes = [vp]
         L.thrs_memcpy_htod_async.argtypes = [vp, vp, u64, vp]
@@ -78,7 +79,7 @@ def lib() -> ctypes.CDLL:
         L.thrs_profile_read.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32),
                                         ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32)]
         L.thrs_rank_mode.restype = i32
-        for f in ("thrs_profile_enable", "thrs_profile_read", "thrs_get_temporary_buffer_bytes", "thrs_sort_keys", "thrs_sort_pairs", "thrs_check_device_error",
+        for f in ("thrs_profile_enable", "thrs_profile_read", "thrs_get_temporary_buffer_bytes", "thrs_sort_keys", "thrs_sort_pairs", "thrs_check_device_error", "thrs_partition_pass",
                   "thrs_malloc", "thrs_free", "thrs_memcpy_htod_async", "thrs_memcpy_dtoh", "thrs_memcpy_dtod_async",
                   "thrs_stream_create", "thrs_stream_destroy", "thrs_stream_synchronize"):
             getattr(L, f).restype = i32
@@ -280,6 +281,15 @@ class RadixSort:
         _check(lib().thrs_sort_pairs(ctypes.byref(self._c()), _ptr(inputKeyBuffer), _ptr(inputValueBuffer),
                                      int(numberOfInputs), _ptr(temporaryBuffer), int(startBits), int(endBits),
                                      _stream(stream)))
+
+    def partitionPass(self, inputKeyBuffer, inputValueBuffer, numberOfInputs: int, temporaryBuffer, outputKeyBuffer,
+                      outputValueBuffer, bitLocation: int, counts, stream=None):
+        """One stable out-of-place pass by the digit at bitLocation plus its 256
+        bucket counts (device u32[256]); thrs_partition_pass, the bucket
+        exchange's partition step (no reference counterpart)."""
+        _check(lib().thrs_partition_pass(ctypes.byref(self._c()), _ptr(inputKeyBuffer), _ptr(inputValueBuffer),
+                                         int(numberOfInputs), _ptr(temporaryBuffer), _ptr(outputKeyBuffer),
+                                         _ptr(outputValueBuffer), int(bitLocation), _ptr(counts), _stream(stream)))
 
     def checkDeviceError(self, temporaryBuffer, stream=None):
         """Synchronising: raises if a look-back spin bound was hit in the last sort."""

@@ -179,9 +179,14 @@ hipError_t allow_lds(F kernel, size_t bytes) {
                              (int)bytes);
 }
 
+// One launch sequence: histogram (+ scan) of all nPass digits, then nPass
+// ping-pong passes.  Sort mode (counts == nullptr): the result is copied back
+// into keys/vals after an odd pass count.  Partition mode (counts != nullptr,
+// nPass == 1, thrs_partition_pass): the pass writes keyOutBuf/valOutBuf, which
+// are the caller's, and the digit's 256 bucket counts go to `counts`.
 template <int KT, int VB, typename ST>
 int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, void* valOutBuf, int startBits, int nPass,
-             bool desc, const Plan& plan, hipStream_t stream) {
+             bool desc, const Plan& plan, hipStream_t stream, uint32_t* counts = nullptr) {
   using U = typename KeyTraits<KT>::U;
   using VW = typename ValueWord<VB>::T;
   using G = PassGeom<sizeof(U), VB>;
@@ -211,6 +216,8 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     hipLaunchKernelGGL(thrs_hist<KT>, dim3(grid), dim3(kHistThreads), lds, stream, static_cast<const U*>(keys), n,
                        orderMask, startBits, nPass, vec, hist);
     hipLaunchKernelGGL(thrs_scan, dim3(1), dim3(kThreads), 0, stream, hist, base, nPass);
+    if (counts && hipMemcpyAsync(counts, hist, kBins * sizeof(uint32_t), hipMemcpyDeviceToDevice, stream) != hipSuccess)
+      return THRS_ERROR_HIP;
   }
 
   const size_t lds = G::LDS_BYTES;
@@ -231,7 +238,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     std::swap(vin, vout);
   }
   if (hipGetLastError() != hipSuccess) return THRS_ERROR_HIP;
-  if (nPass & 1) {  // result must end in the caller's buffers (hpp:936-943), stream-ordered here
+  if ((nPass & 1) && !counts) {  // result must end in the caller's buffers (hpp:936-943), stream-ordered here
     if (hipMemcpyAsync(keys, keyOut, (size_t)n * sizeof(U), hipMemcpyDeviceToDevice, stream) != hipSuccess)
       return THRS_ERROR_HIP;
     if (VB && hipMemcpyAsync(vals, valOut, (size_t)n * VB, hipMemcpyDeviceToDevice, stream) != hipSuccess)
@@ -242,20 +249,20 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
 
 template <int KT, int VB>
 int run_st(void* keys, void* vals, uint32_t n, void* tmp, void* ko, void* vo, int startBits, int nPass, bool desc,
-           const Plan& plan, hipStream_t stream) {
+           const Plan& plan, hipStream_t stream, uint32_t* counts) {
   if (plan.wideStatus)
-    return run_sort<KT, VB, uint64_t>(keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, stream);
-  return run_sort<KT, VB, uint32_t>(keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, stream);
+    return run_sort<KT, VB, uint64_t>(keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, stream, counts);
+  return run_sort<KT, VB, uint32_t>(keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, stream, counts);
 }
 
 template <int KT>
 int run_vb(int vb, void* keys, void* vals, uint32_t n, void* tmp, void* ko, void* vo, int startBits, int nPass,
-           bool desc, const Plan& plan, hipStream_t stream) {
+           bool desc, const Plan& plan, hipStream_t stream, uint32_t* counts = nullptr) {
   switch (vb) {
-    case 0: return run_st<KT, 0>(keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, stream);
-    case 4: return run_st<KT, 4>(keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, stream);
-    case 8: return run_st<KT, 8>(keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, stream);
-    case 16: return run_st<KT, 16>(keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, stream);
+    case 0: return run_st<KT, 0>(keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, stream, counts);
+    case 4: return run_st<KT, 4>(keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, stream, counts);
+    case 8: return run_st<KT, 8>(keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, stream, counts);
+    case 16: return run_st<KT, 16>(keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, stream, counts);
   }
   return THRS_ERROR_INVALID_VALUE;
 }
@@ -306,6 +313,31 @@ int sort_impl(const thrs_config* cfg, void* keys, void* vals, bool pairs, uint32
   return THRS_ERROR_INVALID_VALUE;
 }
 
+int partition_impl(const thrs_config* cfg, const void* keysIn, const void* valsIn, uint32_t n, void* tmp,
+                   void* keysOut, void* valsOut, int bitLocation, uint32_t* counts, hipStream_t stream) {
+  if (!cfg || !valid_key(cfg->keyType)) return THRS_ERROR_INVALID_VALUE;
+  if (cfg->sortOrder != THRS_ORDER_ASCENDING && cfg->sortOrder != THRS_ORDER_DESCENDING) return THRS_ERROR_INVALID_VALUE;
+  const bool pairs = valsIn != nullptr;
+  if (pairs && (!valid_value(cfg->valueType) || !valsOut)) return THRS_ERROR_INVALID_VALUE;
+  const int kb = key_bytes_of(cfg->keyType);
+  if (bitLocation < 0 || bitLocation >= kb * 8 || !counts || !tmp) return THRS_ERROR_INVALID_VALUE;
+  if (n == 0) return hipMemsetAsync(counts, 0, kBins * sizeof(uint32_t), stream) == hipSuccess ? THRS_SUCCESS
+                                                                                                : THRS_ERROR_HIP;
+  if (!keysIn || !keysOut || keysIn == keysOut || (pairs && valsIn == valsOut)) return THRS_ERROR_INVALID_VALUE;
+  const int vb = pairs ? value_bytes_of(cfg->valueType) : 0;
+  const Plan plan = make_plan(cfg->keyType, vb, n);
+  const bool desc = cfg->sortOrder == THRS_ORDER_DESCENDING;
+  void* ki = const_cast<void*>(keysIn);
+  void* vi = const_cast<void*>(valsIn);
+  switch (cfg->keyType) {
+    case THRS_KEY_U32: return run_vb<0>(vb, ki, vi, n, tmp, keysOut, valsOut, bitLocation, 1, desc, plan, stream, counts);
+    case THRS_KEY_U64: return run_vb<1>(vb, ki, vi, n, tmp, keysOut, valsOut, bitLocation, 1, desc, plan, stream, counts);
+    case THRS_KEY_F32: return run_vb<2>(vb, ki, vi, n, tmp, keysOut, valsOut, bitLocation, 1, desc, plan, stream, counts);
+    case THRS_KEY_F64: return run_vb<3>(vb, ki, vi, n, tmp, keysOut, valsOut, bitLocation, 1, desc, plan, stream, counts);
+  }
+  return THRS_ERROR_INVALID_VALUE;
+}
+
 }  // namespace
 
 #define THRS_API __attribute__((visibility("default")))
@@ -342,6 +374,12 @@ THRS_API int thrs_sort_keys(const thrs_config* config, void* keys, uint32_t n, v
 THRS_API int thrs_sort_pairs(const thrs_config* config, void* keys, void* values, uint32_t n, void* tmp, int startBits,
                     int endBits, hipStream_t stream) {
   return sort_impl(config, keys, values, true, n, tmp, startBits, endBits, stream);
+}
+
+THRS_API int thrs_partition_pass(const thrs_config* config, const void* keysIn, const void* valuesIn, uint32_t n,
+                                 void* tmp, void* keysOut, void* valuesOut, int bitLocation, uint32_t* counts,
+                                 hipStream_t stream) {
+  return partition_impl(config, keysIn, valuesIn, n, tmp, keysOut, valuesOut, bitLocation, counts, stream);
 }
 
 THRS_API int thrs_check_device_error(void* tmp, hipStream_t stream) {
