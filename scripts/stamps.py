@@ -48,7 +48,7 @@ def main():
     tile = int(L.thrs_debug_tile_keys(kt, vb))
     ntiles = (n + tile - 1) // tile
     passes = kb
-    stamps = torch.zeros(passes * ntiles * 8, dtype=torch.int64, device="cuda")
+    stamps = torch.zeros(passes * ntiles * 24, dtype=torch.int64, device="cuda")
     s = torch.cuda.current_stream()
     for it in range(2):
         TU.fill_keys(kt, keys, n, start=it * n)
@@ -64,7 +64,7 @@ def main():
         torch.cuda.synchronize()
         assert rc == 0
     L.thrs_debug_set_stamps(None)
-    st = stamps.cpu().numpy().reshape(passes, ntiles, 8)
+    st = stamps.cpu().numpy().reshape(passes, ntiles, 24)
     report = {"n": n, "tile": tile, "ntiles": ntiles, "passes": []}
     for p in range(passes):
         a_ = st[p].astype(np.int64)
@@ -85,7 +85,40 @@ def main():
         rounds = (a_[:, 7] >> 8) & 0xFFFF
         depth = (a_[:, 7] >> 24) & 0xFFFF
         stalls = (a_[:, 7] >> 40) & 0xFFFFFF
-        report["passes"].append({"pass": p, "kernel_span_us": round(float(span), 1),
+        # look-back dynamics: lag = tile id -> own prefix published; age of the
+        # predecessor prefix that ended the walk, at the moment the walk ended
+        lag = (a_[:, 5] - a_[:, 1]) * 0.01
+        ids = np.arange(ntiles)
+        pred = ids - 1 - depth
+        ok = (pred >= 0) & (ids > 0)
+        age = (a_[ids[ok], 5] - a_[pred[ok], 5]) * 0.01
+        if age.size == 0:
+            age = np.zeros(1)
+        walk_start = (a_[:, 4] - a_[:, 0]) * 0.01
+        frontier = {"lag_med_us": round(float(np.median(lag)), 2), "lag_p90_us": round(float(np.percentile(lag, 90)), 2),
+                    "found_prefix_age_med_us": round(float(np.median(age)), 2),
+                    "found_prefix_age_p10_us": round(float(np.percentile(age, 10)), 2),
+                    "walk_start_after_entry_med_us": round(float(np.median(walk_start)), 2),
+                    "tiles_per_us": round(ntiles / float(span), 2)}
+        walk = {}
+
+        def q(x):
+            return {"med_us": round(float(np.median(x)), 3), "p90_us": round(float(np.percentile(x, 90)), 3)}
+        if (a_[:, 16] > 0).any():
+            m = (a_[:, 16] > 0) & (a_[:, 17] > 0) & (a_[:, 18] > 0)
+            walk = {"rank_end_to_walk_issue": q((a_[m, 16] - a_[m, 4]) * 0.01),
+                    "first_window_roundtrip": q((a_[m, 17] - a_[m, 16]) * 0.01),
+                    "rest_of_walk": q((a_[m, 18] - a_[m, 17]) * 0.01),
+                    "walk_end_to_barrier": q((a_[m, 5] - a_[m, 18]) * 0.01)}
+        we, ba = a_[:, 8:12], a_[:, 12:16]
+        m = (we > 0).all(axis=1) & (ba > 0).all(axis=1)
+        if m.any():
+            walk["walk_end_per_wave_med_after_rank"] = [round(float(np.median((we[m, i] - a_[m, 4]) * 0.01)), 2)
+                                                        for i in range(4)]
+            walk["barrier_arrival_per_wave_med_after_rank"] = [
+                round(float(np.median((ba[m, i] - a_[m, 4]) * 0.01)), 2) for i in range(4)]
+            walk["barrier_release_after_rank"] = q((a_[m, 5] - a_[m, 4]) * 0.01)
+        report["passes"].append({"pass": p, "kernel_span_us": round(float(span), 1), "frontier": frontier, "walk": walk,
                                  "tile_life_med_us": round(float(np.median(life)), 2),
                                  "tile_life_p90_us": round(float(np.percentile(life, 90)), 2),
                                  "phases": dur, "inflight_samples": inflight,

@@ -64,8 +64,11 @@ struct Plan {
   uint64_t tileKeys;  // keys per tile of the pass kernel
   uint64_t nTiles;
   bool wideStatus;    // 64-bit look-back words (n >= 2^31)
-  uint64_t statusBytes;
-  uint64_t scratchBytes;
+  uint64_t statusBytes;   // per-tile rows [nTiles][256]
+  uint64_t gaBytes;       // group aggregates [nGroups][256] u32 (kGroup > 0)
+  uint64_t gpBytes;       // group prefixes   [nGroups][256] status words
+  uint64_t setBytes;      // one look-back table set = status + ga + gp
+  uint64_t scratchBytes;  // header + 2 sets (ping-pong between passes)
 };
 
 Plan make_plan(int keyType, int valueBytesOrZero, uint32_t n) {
@@ -76,7 +79,11 @@ Plan make_plan(int keyType, int valueBytesOrZero, uint32_t n) {
   p.nTiles = std::max<uint64_t>(1, ((uint64_t)n + p.tileKeys - 1) / p.tileKeys);
   p.wideStatus = (uint64_t)n >= (1ull << 31);
   p.statusBytes = round_up(p.nTiles * kBins * (p.wideStatus ? 8 : 4), kAlign);
-  p.scratchBytes = kHeaderBytes + 2 * p.statusBytes;
+  const uint64_t nGroups = kGroup > 0 ? (p.nTiles + kGroup - 1) / kGroup : 0;
+  p.gaBytes = round_up(nGroups * kBins * 4, kAlign);
+  p.gpBytes = round_up(nGroups * kBins * (p.wideStatus ? 8 : 4), kAlign);
+  p.setBytes = p.statusBytes + p.gaBytes + p.gpBytes;
+  p.scratchBytes = kHeaderBytes + 2 * p.setBytes;
   return p;
 }
 
@@ -196,15 +203,24 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   uint32_t* base = reinterpret_cast<uint32_t*>(scratch + kBaseOff);
   uint32_t* counters = reinterpret_cast<uint32_t*>(scratch + kCounterOff);
   uint32_t* err = reinterpret_cast<uint32_t*>(scratch + kErrOff);
-  ST* status[2] = {reinterpret_cast<ST*>(scratch + kHeaderBytes),
-                   reinterpret_cast<ST*>(scratch + kHeaderBytes + plan.statusBytes)};
+  // table sets: [status | ga | gp] x 2; pass p uses set p&1 and clears its
+  // rows of set (p+1)&1 for the next pass
+  ST* status[2];
+  GroupTables<ST> grp[2];
+  for (int i = 0; i < 2; ++i) {
+    char* set = scratch + kHeaderBytes + i * plan.setBytes;
+    status[i] = reinterpret_cast<ST*>(set);
+    grp[i].ga = reinterpret_cast<uint32_t*>(set + plan.statusBytes);
+    grp[i].gp = reinterpret_cast<ST*>(set + plan.statusBytes + plan.gaBytes);
+    grp[i].nTiles = (uint32_t)plan.nTiles;
+  }
   U* keyOut = static_cast<U*>(keyOutBuf);
   VW* valOut = static_cast<VW*>(valOutBuf);
 
   const U orderMask = desc ? (U)~(U)0 : (U)0;
 
   // header (histograms, tile counters, error word) + first status table
-  if (hipMemsetAsync(scratch, 0, kHeaderBytes + plan.statusBytes, stream) != hipSuccess) return THRS_ERROR_HIP;
+  if (hipMemsetAsync(scratch, 0, kHeaderBytes + plan.setBytes, stream) != hipSuccess) return THRS_ERROR_HIP;
 
   {  // histograms of every pass in one read of the keys
     ProfScope prof(stream, 0);
@@ -229,11 +245,15 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   VW* vin = static_cast<VW*>(vals);
   VW* vout = valOut;
   for (int p = 0; p < nPass; ++p) {
-    ST* next = (p + 1 < nPass) ? status[(p + 1) & 1] : nullptr;
+    const bool more = p + 1 < nPass;
+    ST* next = more ? status[(p + 1) & 1] : nullptr;
+    GroupTables<ST> g = grp[p & 1];
+    g.gaNext = more ? grp[(p + 1) & 1].ga : nullptr;
+    g.gpNext = more ? grp[(p + 1) & 1].gp : nullptr;
     ProfScope prof(stream, 1);
     hipLaunchKernelGGL(kernel, dim3((uint32_t)plan.nTiles), dim3(G::THREADS), lds, stream, kin, kout, vin, vout, n,
-                       orderMask, startBits + 8 * p, base + p * kBins, status[p & 1], next, counters + p, err,
-                       g_stamps ? g_stamps + (uint64_t)p * plan.nTiles * 8 : nullptr);
+                       orderMask, startBits + 8 * p, base + p * kBins, status[p & 1], next, counters + p, err, g,
+                       g_stamps ? g_stamps + (uint64_t)p * plan.nTiles * kStampSlots : nullptr);
     std::swap(kin, kout);
     std::swap(vin, vout);
   }
@@ -421,7 +441,7 @@ THRS_API int thrs_profile_read(double* histMs, int* histLaunches, double* passMs
 }
 
 // Diagnostic hook, not part of the drop-in boundary: in -DTHRS_STAMPS builds
-// the pass kernel writes per-tile phase timestamps to buf[(pass*nTiles+tile)*8+i].
+// the pass kernel writes per-tile phase timestamps to buf[(pass*nTiles+tile)*16+i].
 THRS_API int thrs_debug_set_stamps(void* buf) {
   g_stamps = static_cast<uint64_t*>(buf);
   return THRS_SUCCESS;

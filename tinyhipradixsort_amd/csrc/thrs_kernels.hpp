@@ -244,6 +244,42 @@ __device__ __forceinline__ void lds_barrier() {
 #define THRS_LOOK_WINDOW 8
 #endif
 constexpr int kLookWindow = THRS_LOOK_WINDOW;
+// Two-level look-back (THRS_GROUP = tiles per group, 0 = flat per-tile chain).
+// Every tile adds its digit counts to its group's aggregate row with one
+// fire-and-forget atomic per digit; the word also counts arrivals, so a reader
+// knows when the aggregate is complete:  ga = count | arrivals << 20.
+// The last tile of a group publishes the group's inclusive prefix (gp).  A
+// walker sums the rows of its own group's earlier tiles, then walks GROUP
+// rows (kGroupWindow per round trip): a group prefix ends the walk, a complete
+// aggregate skips THRS_GROUP tiles at once.  The walk depth in rows falls by
+// about THRS_GROUP (docs/EXPERIMENTS.md).
+#ifndef THRS_GROUP
+#define THRS_GROUP 16
+#endif
+#ifndef THRS_GROUP_WINDOW
+#define THRS_GROUP_WINDOW 8
+#endif
+constexpr int kGroup = THRS_GROUP;
+constexpr int kStampSlots = 24;  // THRS_STAMPS diagnostics: u64 slots per tile
+constexpr int kGroupWindow = THRS_GROUP_WINDOW;
+constexpr uint32_t kArrival = 1u << 20;
+template <typename ST> struct GroupTables {
+  uint32_t* ga;      // [nGroups][256] count | arrivals << 20   (this pass)
+  ST* gp;            // [nGroups][256] Status<ST>::pre(inclusive prefix)
+  uint32_t* gaNext;  // next pass's tables, cleared by each group's last tile
+  ST* gpNext;
+  uint32_t nTiles;
+};
+
+#ifndef THRS_LATE_CLEAR
+#define THRS_LATE_CLEAR 1
+#endif
+#ifndef THRS_PUB_BY_WALKERS
+#define THRS_PUB_BY_WALKERS 0
+#endif
+#ifndef THRS_EARLY_WINDOW
+#define THRS_EARLY_WINDOW 0
+#endif
 
 // Tile configuration per (key bytes, value bytes).  A tile is what one
 // workgroup holds in REGISTERS (THREADS x KPT keys) and publishes one status
@@ -275,6 +311,7 @@ template <int KB, int VB> struct PassGeom {
   static constexpr uint32_t STAGE = TILE / ROUNDS;
   static constexpr uint32_t LDS_BYTES = STAGE * (KB + VB) + (WAVES + 1) * kBins * 4 + 16 * 4;
   static_assert(TILE <= 65536, "slots are kept as 16-bit halves");
+  static_assert(kGroup == 0 || (uint64_t)kGroup * TILE < kArrival, "group counts must fit below the arrival bits");
   static_assert((STAGE & (STAGE - 1)) == 0 && STAGE % THREADS == 0, "stage must be a power of two");
 };
 
@@ -288,35 +325,157 @@ template <int KB, int VB> struct PassGeom {
 //      -> global offset of digit d
 //   E  ROUNDS x { scatter keys whose slot falls in this round into the LDS
 //      stage, coalesced write-out of the stage }
+__device__ __forceinline__ uint32_t xcc_id() {
+  uint32_t x;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+  return x;
+}
+
+// Two-level look-back for digit d of `tile` (THRS_GROUP > 0); writes the
+// digit's global write offset to s_gofs[d] and, from the group's last tile,
+// publishes the group's inclusive prefix.
+template <typename ST>
+__device__ __forceinline__ void group_lookback(const ST* __restrict__ status, const GroupTables<ST>& grp, uint32_t tile,
+                                               uint32_t d, uint32_t realTot, uint32_t myBase, uint32_t localStart,
+                                               uint32_t* s_gofs, uint32_t* s_misc, uint32_t* errFlag,
+                                               uint64_t* __restrict__ stamps) {
+#ifdef THRS_STAMPS
+  // slot 16: first window issued, 17: first window consumed, 18: walk done (digit 0's thread)
+  const bool st0 = stamps && d == 0;
+  if (st0) stamps[(uint64_t)tile * kStampSlots + 16] = __builtin_amdgcn_s_memrealtime();
+#else
+  (void)stamps;
+#endif
+  const uint32_t g = tile / kGroup, gstart = g * kGroup;
+  const uint32_t gend = min(gstart + (uint32_t)kGroup, grp.nTiles);
+  uint32_t inGroup = 0, excl = 0, spins = 0, rounds = 0;
+  uint32_t jt = gstart;         // next earlier tile of this group to add (ascending)
+  int32_t jg = (int32_t)g - 1;  // next earlier group to add (descending); -1 = done
+  int32_t found = -1;           // group whose prefix ended the walk (diagnostics)
+  while (jt < tile || jg >= 0) {
+    ST wt[8];
+    ST wp[kGroupWindow];
+    uint32_t wa[kGroupWindow];
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      wt[q] = (jt + q < tile) ? load_agent(status + (uint64_t)(jt + q) * kBins + d) : (ST)0;
+#pragma unroll
+    for (int q = 0; q < kGroupWindow; ++q) {
+      const bool in = jg - q >= 0;
+      wp[q] = in ? load_agent(grp.gp + (uint64_t)(jg - q) * kBins + d) : (ST)0;
+      wa[q] = in ? load_agent(grp.ga + (uint64_t)(jg - q) * kBins + d) : 0u;
+    }
+    ++rounds;
+    bool stall = false;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      if (!stall && jt < tile) {
+        if (wt[q] == 0) stall = true;
+        else {
+          inGroup += Status<ST>::val(wt[q]);
+          ++jt;
+        }
+      }
+    }
+    bool gstop = false;
+#pragma unroll
+    for (int q = 0; q < kGroupWindow; ++q) {
+      if (!gstop && jg >= 0) {
+        if (wp[q] != 0) {  // inclusive prefix of group jg: done
+          excl += Status<ST>::val(wp[q]);
+          found = jg;
+          jg = -1;
+        } else {
+          const uint32_t members = min((uint32_t)kGroup, grp.nTiles - (uint32_t)jg * kGroup);
+          if ((wa[q] >> 20) == members) {
+            excl += wa[q] & (kArrival - 1);
+            --jg;
+          } else {
+            gstop = true;
+            stall = true;
+          }
+        }
+      }
+    }
+#ifdef THRS_STAMPS
+    if (st0 && rounds == 1) {
+      uint32_t dep = inGroup + excl;
+      pin(dep);
+      stamps[(uint64_t)tile * kStampSlots + 17] = __builtin_amdgcn_s_memrealtime() + (dep & 0);
+    }
+#endif
+    if (stall && (jt < tile || jg >= 0)) {
+      if (++spins > (1u << 22)) {  // bounded spin: never hang the GPU
+        atomicOr(errFlag, 1u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  excl += inGroup;
+#ifdef THRS_STAMPS
+  if (stamps && (d & 63) == 0) {  // slots 8..11: walk end of waves 0..3
+    uint32_t dep = excl;
+    pin(dep);
+    const uint64_t tnow = __builtin_amdgcn_s_memrealtime();
+    stamps[(uint64_t)tile * kStampSlots + 8 + (d >> 6)] = tnow + (uint64_t)(dep == 0xFFFFFFFFu);
+  }
+#endif
+  s_gofs[d] = myBase + excl - localStart;
+  if (tile == gend - 1) {
+    store_agent(grp.gp + (uint64_t)g * kBins + d, Status<ST>::pre(excl + realTot));
+#if !THRS_LATE_CLEAR
+    if (grp.gaNext) {
+      grp.gaNext[(uint64_t)g * kBins + d] = 0;
+      grp.gpNext[(uint64_t)g * kBins + d] = 0;
+    }
+#endif
+  }
+#ifdef THRS_STAMPS
+  atomicMax(&s_misc[1], rounds);
+  atomicMax(&s_misc[2], spins);
+  atomicMax(&s_misc[3], (uint32_t)(tile - gstart) + (uint32_t)((int32_t)g - 1 - found) * kGroup);
+#else
+  (void)s_misc;
+  (void)rounds;
+  (void)found;
+#endif
+}
+
+// Everything one workgroup does for one tile (phases A-E below).
+//   tile        global tile index (rows of the status table, key range)
+//   chainStart  first tile of this tile's look-back chain: tile == chainStart
+//               publishes its prefix directly
+//   myBase      (thread d < 256) global output base of digit d for the chain
+// Returns after the tile's last store is issued.
 template <int KT, int VB, typename ST, bool ATOMIC_RANK>
-__global__ __launch_bounds__((PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::THREADS))
-__attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::WPE))) void thrs_pass(
+__device__ __forceinline__ void pass_tile(
     const typename KeyTraits<KT>::U* __restrict__ keysIn, typename KeyTraits<KT>::U* __restrict__ keysOut,
     const typename ValueWord<VB>::T* __restrict__ valsIn, typename ValueWord<VB>::T* __restrict__ valsOut,
-    uint32_t n, typename KeyTraits<KT>::U orderMask, int shift, const uint32_t* __restrict__ digitBase,
-    ST* __restrict__ status, ST* __restrict__ statusNext, uint32_t* __restrict__ tileCounter,
-    uint32_t* __restrict__ errFlag, uint64_t* __restrict__ stamps) {
+    uint32_t n, typename KeyTraits<KT>::U orderMask, int shift, uint32_t myBase, ST* __restrict__ status,
+    ST* __restrict__ statusNext, uint32_t* __restrict__ errFlag, uint32_t tile, uint32_t chainStart,
+    const GroupTables<ST>& grp, unsigned char* smem, uint64_t* __restrict__ stamps) {
   using U = typename KeyTraits<KT>::U;
   using VW = typename ValueWord<VB>::T;
   using G = PassGeom<sizeof(U), VB>;
   constexpr int WAVES = G::WAVES, KPT = G::KPT, ROUNDS = G::ROUNDS, THREADS = G::THREADS;
   constexpr uint32_t T = G::TILE, STAGE = G::STAGE, CHUNK = 64 * KPT;
   constexpr int STAGE_SHIFT = __builtin_ctz(STAGE);
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  // threads [PUB_LO, PUB_LO+256) publish the tile's status row (see phase B)
+  constexpr uint32_t PUB_LO = (WAVES >= 8 && !THRS_PUB_BY_WALKERS) ? 256u : 0u;
   U* stage_k = reinterpret_cast<U*>(smem);
   VW* stage_v = reinterpret_cast<VW*>(smem + STAGE * sizeof(U));
   uint32_t* s_cnt = reinterpret_cast<uint32_t*>(smem + STAGE * (sizeof(U) + VB));  // [WAVES][256]
   uint32_t* s_gofs = s_cnt + WAVES * kBins;
   uint32_t* s_misc = s_gofs + kBins;
-
+  const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   // Diagnostic builds (-DTHRS_STAMPS) record s_memrealtime (100 MHz) per
-  // phase for every tile into stamps[tile*8 + i]; normal builds compile none.
+  // phase for every tile into stamps[tile*kStampSlots + i]; normal builds compile none.
 #ifdef THRS_STAMPS
 #define THRS_STAMP(i)                                                                                  \
   do {                                                                                                 \
-    if (stamps && threadIdx.x == 0) stamps[(uint64_t)tile * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+    if (stamps && threadIdx.x == 0) stamps[(uint64_t)tile * kStampSlots + (i)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
-  const uint64_t t_entry = __builtin_amdgcn_s_memrealtime();
 #else
 #define THRS_STAMP(i) \
   do {                \
@@ -324,24 +483,6 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
   (void)stamps;
 #endif
 
-  const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-
-  // ---- A: dynamic tile id (start order, so every tile we wait on is resident)
-  if (tid == 0) {
-    s_misc[0] = atomicAdd(tileCounter, 1u);
-    s_misc[1] = s_misc[2] = s_misc[3] = 0;  // diagnostic maxima (THRS_STAMPS)
-  }
-  for (uint32_t i = tid; i < (uint32_t)(WAVES * kBins); i += THREADS) s_cnt[i] = 0;
-  lds_barrier();
-  const uint32_t tile = s_misc[0];
-#ifdef THRS_STAMPS
-  if (stamps && tid == 0) {
-    stamps[(uint64_t)tile * 8 + 0] = t_entry;
-    uint32_t xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    stamps[(uint64_t)tile * 8 + 7] = xcc;
-  }
-#endif
   THRS_STAMP(1);
   const uint64_t tileBase = (uint64_t)tile * T;
   const uint32_t valid = (uint32_t)min((uint64_t)T, (uint64_t)n - tileBase);
@@ -369,7 +510,6 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
     }
   }
   const uint32_t d = tid & 255u;
-  const uint32_t myBase = digitBase[d];  // global base of digit d, used in D
 
   auto digit_of = [&](U key, int j) -> uint32_t {
     uint32_t dd = (uint32_t)((KeyTraits<KT>::bits(key) ^ orderMask) >> shift) & 0xFFu;
@@ -391,9 +531,41 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
 #pragma unroll
     for (int ww = 0; ww < WAVES; ++ww) tot += s_cnt[ww * kBins + d];
     realTot = (d == 255u) ? tot - (T - valid) : tot;
-    if (tile != 0) store_agent(myStatus, Status<ST>::agg(realTot));
-    else store_agent(myStatus, Status<ST>::pre(realTot));
   }
+  // Publish the tile aggregate (and the group atomic) from waves 4-7: vmcnt
+  // counts stores too on gfx9-family parts, so if the walkers (waves 0-3)
+  // issued these write-through stores, their first wait on a look-back load
+  // would also wait for the stores' acknowledgement -- several us under load.
+  if (PUB_LO <= tid && tid < PUB_LO + 256) {
+    const uint32_t dp = tid - PUB_LO;
+    uint32_t t2 = 0;
+#pragma unroll
+    for (int ww = 0; ww < WAVES; ++ww) t2 += s_cnt[ww * kBins + dp];
+    const uint32_t real2 = (dp == 255u) ? t2 - (T - valid) : t2;
+    ST* pub = status + (uint64_t)tile * kBins + dp;
+    if (tile != chainStart) store_agent(pub, Status<ST>::agg(real2));
+    else store_agent(pub, Status<ST>::pre(real2));
+    if constexpr (kGroup > 0)
+      __hip_atomic_fetch_add(&grp.ga[(uint64_t)(tile / kGroup) * kBins + dp], real2 + kArrival, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // Look-back window loader: rows j, j-1, ... of column d.  32-bit byte offsets
+  // from the uniform base -> saddr loads, one VGPR each.
+  ST win[kLookWindow];
+  int64_t j = (int64_t)tile - 1;  // next predecessor to consume
+  auto issue_window = [&]() __attribute__((always_inline)) {
+    const uint32_t off0 = ((uint32_t)j * kBins + d) * (uint32_t)sizeof(ST);
+#pragma unroll
+    for (int q = 0; q < kLookWindow; ++q)
+      win[q] = (j - q >= (int64_t)chainStart)
+                   ? load_agent(reinterpret_cast<const ST*>(reinterpret_cast<const char*>(status) +
+                                                            (off0 - (uint32_t)q * kBins * sizeof(ST))))
+                   : (ST)0;
+  };
+#if THRS_EARLY_WINDOW
+  // first window in flight during the local scan and the rank (phase C)
+  if (tid < 256 && tile != chainStart) issue_window();
+#endif
   // local exclusive scan over the 256 digits (waves 0-3)
   uint32_t localStart = 0;
   {
@@ -443,25 +615,33 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
   }
   THRS_STAMP(4);
 
+
   // ---- D: decoupled look-back for digit d, kLookWindow rows per round trip;
   // a not-yet-published word stops the window and is re-polled.
-  if (tid < 256) {
+  if constexpr (kGroup > 0) {
+    if (tid < 256) group_lookback<ST>(status, grp, tile, d, realTot, myBase, localStart, s_gofs, s_misc, errFlag, stamps);
+#if !THRS_LATE_CLEAR
+    if (tid < 256 && statusNext) statusNext[(uint64_t)tile * kBins + d] = 0;  // ready for the next pass
+#endif
+#ifdef THRS_STAMPS
+    if (stamps && lane == 0 && w < 4) {  // slots 12..15: waves 0..3 arrive at the post-walk barrier
+      uint32_t dep = s_gofs[d & 255];
+      pin(dep);
+      const uint64_t tnow = __builtin_amdgcn_s_memrealtime();
+      stamps[(uint64_t)tile * kStampSlots + 12 + w] = tnow + (uint64_t)(dep == 0xFFFFFFFFu);
+    }
+#endif
+  } else if (tid < 256) {
     uint32_t excl = 0;
 #ifdef THRS_STAMPS
     uint32_t dbgRounds = 0;
 #endif
-    if (tile != 0) {
-      int64_t j = (int64_t)tile - 1;  // next predecessor to consume
+    if (tile != chainStart) {
       uint32_t spins = 0;
+      bool pending = THRS_EARLY_WINDOW;  // the first window is already in flight
       while (true) {
-        ST win[kLookWindow];
-        // 32-bit byte offsets from the uniform base -> saddr loads, one VGPR each
-        const uint32_t off0 = ((uint32_t)j * kBins + d) * (uint32_t)sizeof(ST);
-#pragma unroll
-        for (int q = 0; q < kLookWindow; ++q)
-          win[q] = (j - q >= 0) ? load_agent(reinterpret_cast<const ST*>(reinterpret_cast<const char*>(status) +
-                                                                         (off0 - (uint32_t)q * kBins * sizeof(ST))))
-                                : (ST)0;
+        if (!pending) issue_window();
+        pending = false;
 #ifdef THRS_STAMPS
         ++dbgRounds;
 #endif
@@ -496,7 +676,9 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
 #endif
     }
     s_gofs[d] = myBase + excl - localStart;
+#if !THRS_LATE_CLEAR
     if (statusNext) statusNext[(uint64_t)tile * kBins + d] = 0;  // ready for the next pass
+#endif
   }
   lds_barrier();
   THRS_STAMP(5);
@@ -527,15 +709,68 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
     }
     if (r + 1 < ROUNDS) lds_barrier();
   }
+#if THRS_LATE_CLEAR
+  // Clear this tile's rows of the next pass's tables only now: a store issued
+  // before the look-back barrier waits for room in the CU's in-order vector
+  // memory queue (behind the other workgroup's loads) and holds the barrier.
+  if (tid < 256) {
+    if (statusNext) statusNext[(uint64_t)tile * kBins + d] = 0;
+    if constexpr (kGroup > 0) {
+      const uint32_t gend = min((tile / kGroup + 1) * (uint32_t)kGroup, grp.nTiles);
+      if (grp.gaNext && tile == gend - 1) {
+        grp.gaNext[(uint64_t)(tile / kGroup) * kBins + d] = 0;
+        grp.gpNext[(uint64_t)(tile / kGroup) * kBins + d] = 0;
+      }
+    }
+  }
+#endif
 #ifdef THRS_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   THRS_STAMP(6);
   if (stamps && tid == 0)  // slot 7: xcc | max rounds << 8 | max depth << 24 | max stalls << 40
-    stamps[(uint64_t)tile * 8 + 7] |= ((uint64_t)min(s_misc[1], 65535u) << 8) |
+    stamps[(uint64_t)tile * kStampSlots + 7] |= ((uint64_t)min(s_misc[1], 65535u) << 8) |
                                       ((uint64_t)min(s_misc[3], 65535u) << 24) | ((uint64_t)s_misc[2] << 40);
 #endif
 #undef THRS_STAMP
 }
+
+
+// One workgroup per tile, tile ids in start order (dynamic): the chain is the
+// whole tile range and status words go through the agent scope.
+template <int KT, int VB, typename ST, bool ATOMIC_RANK>
+__global__ __launch_bounds__((PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::THREADS))
+__attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::WPE))) void thrs_pass(
+    const typename KeyTraits<KT>::U* __restrict__ keysIn, typename KeyTraits<KT>::U* __restrict__ keysOut,
+    const typename ValueWord<VB>::T* __restrict__ valsIn, typename ValueWord<VB>::T* __restrict__ valsOut,
+    uint32_t n, typename KeyTraits<KT>::U orderMask, int shift, const uint32_t* __restrict__ digitBase,
+    ST* __restrict__ status, ST* __restrict__ statusNext, uint32_t* __restrict__ tileCounter,
+    uint32_t* __restrict__ errFlag, GroupTables<ST> grp, uint64_t* __restrict__ stamps) {
+  using G = PassGeom<sizeof(typename KeyTraits<KT>::U), VB>;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint32_t* s_cnt = reinterpret_cast<uint32_t*>(smem + G::STAGE * (sizeof(typename KeyTraits<KT>::U) + VB));
+  uint32_t* s_misc = s_cnt + (G::WAVES + 1) * kBins;
+#ifdef THRS_STAMPS
+  const uint64_t t_entry = __builtin_amdgcn_s_memrealtime();
+#endif
+  const uint32_t tid = threadIdx.x;
+  if (tid == 0) {
+    s_misc[0] = atomicAdd(tileCounter, 1u);
+    s_misc[1] = s_misc[2] = s_misc[3] = 0;  // diagnostic maxima (THRS_STAMPS)
+  }
+  for (uint32_t i = tid; i < (uint32_t)(G::WAVES * kBins); i += G::THREADS) s_cnt[i] = 0;
+  const uint32_t myBase = digitBase[tid & 255u];
+  lds_barrier();
+  const uint32_t tile = s_misc[0];
+#ifdef THRS_STAMPS
+  if (stamps && tid == 0) {
+    stamps[(uint64_t)tile * kStampSlots + 0] = t_entry;
+    stamps[(uint64_t)tile * kStampSlots + 7] = xcc_id();
+  }
+#endif
+  pass_tile<KT, VB, ST, ATOMIC_RANK>(keysIn, keysOut, valsIn, valsOut, n, orderMask, shift, myBase, status,
+                                            statusNext, errFlag, tile, 0, grp, smem, stamps);
+}
+
 
 // ================================================================ self-probe
 // Does ds_add_rtn_u32 hand out values in lane order when several lanes of one
