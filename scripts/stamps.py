@@ -65,6 +65,8 @@ def main():
         assert rc == 0
     L.thrs_debug_set_stamps(None)
     st = stamps.cpu().numpy().reshape(passes, ntiles, 24)
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    np.save(os.path.join(ROOT, "gpurun_out", "stamps_pass0.npy"), st[0])
     report = {"n": n, "tile": tile, "ntiles": ntiles, "passes": []}
     for p in range(passes):
         a_ = st[p].astype(np.int64)
@@ -104,8 +106,8 @@ def main():
 
         def q(x):
             return {"med_us": round(float(np.median(x)), 3), "p90_us": round(float(np.percentile(x, 90)), 3)}
-        if (a_[:, 16] > 0).any():
-            m = (a_[:, 16] > 0) & (a_[:, 17] > 0) & (a_[:, 18] > 0)
+        m = (a_[:, 16] > 0) & (a_[:, 17] > 0) & (a_[:, 18] > 0)
+        if m.any():
             walk = {"rank_end_to_walk_issue": q((a_[m, 16] - a_[m, 4]) * 0.01),
                     "first_window_roundtrip": q((a_[m, 17] - a_[m, 16]) * 0.01),
                     "rest_of_walk": q((a_[m, 18] - a_[m, 17]) * 0.01),

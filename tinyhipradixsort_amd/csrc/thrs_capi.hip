@@ -26,6 +26,10 @@
 #include "thrs/thrs_capi.h"
 #include "thrs_kernels.hpp"
 
+#ifndef THRS_PIPE
+#define THRS_PIPE 0
+#endif
+
 using namespace thrs_dev;
 
 namespace {
@@ -237,7 +241,19 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   }
 
   const size_t lds = G::LDS_BYTES;
-  auto kernel = probe_rank_mode(stream) ? thrs_pass<KT, VB, ST, true> : thrs_pass<KT, VB, ST, false>;
+  const bool atomicRank = probe_rank_mode(stream) != 0;
+  auto kernel = atomicRank ? thrs_pass<KT, VB, ST, true> : thrs_pass<KT, VB, ST, false>;
+  uint32_t grid = (uint32_t)plan.nTiles;
+#if THRS_PIPE
+  if constexpr (G::ROUNDS == 1) {  // persistent: as many workgroups as fit at once
+    kernel = atomicRank ? thrs_pass_pipe<KT, VB, ST, true> : thrs_pass_pipe<KT, VB, ST, false>;
+    if (allow_lds(kernel, lds) != hipSuccess) return THRS_ERROR_HIP;
+    int perCU = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, kernel, G::THREADS, lds) != hipSuccess || perCU < 1)
+      perCU = 1;
+    grid = (uint32_t)std::min<uint64_t>(plan.nTiles, (uint64_t)perCU * cu_count());
+  }
+#endif
   if (allow_lds(kernel, lds) != hipSuccess) return THRS_ERROR_HIP;
 
   U* kin = static_cast<U*>(keys);
@@ -251,7 +267,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     g.gaNext = more ? grp[(p + 1) & 1].ga : nullptr;
     g.gpNext = more ? grp[(p + 1) & 1].gp : nullptr;
     ProfScope prof(stream, 1);
-    hipLaunchKernelGGL(kernel, dim3((uint32_t)plan.nTiles), dim3(G::THREADS), lds, stream, kin, kout, vin, vout, n,
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(G::THREADS), lds, stream, kin, kout, vin, vout, n,
                        orderMask, startBits + 8 * p, base + p * kBins, status[p & 1], next, counters + p, err, g,
                        g_stamps ? g_stamps + (uint64_t)p * plan.nTiles * kStampSlots : nullptr);
     std::swap(kin, kout);

@@ -261,7 +261,16 @@ constexpr int kLookWindow = THRS_LOOK_WINDOW;
 #endif
 constexpr int kGroup = THRS_GROUP;
 constexpr int kStampSlots = 24;  // THRS_STAMPS diagnostics: u64 slots per tile
+#ifdef THRS_STAMPS
+constexpr uint32_t kStampLds = kStampSlots * 8;
+#else
+constexpr uint32_t kStampLds = 0;
+#endif
 constexpr int kGroupWindow = THRS_GROUP_WINDOW;
+#ifndef THRS_TILE_WINDOW
+#define THRS_TILE_WINDOW 8
+#endif
+constexpr int kTileWindow = THRS_TILE_WINDOW;  // own-group tile rows per round trip
 constexpr uint32_t kArrival = 1u << 20;
 template <typename ST> struct GroupTables {
   uint32_t* ga;      // [nGroups][256] count | arrivals << 20   (this pass)
@@ -271,6 +280,12 @@ template <typename ST> struct GroupTables {
   uint32_t nTiles;
 };
 
+#ifndef THRS_RELOAD_KEYS
+#define THRS_RELOAD_KEYS 0
+#endif
+#ifndef THRS_WO_BATCH
+#define THRS_WO_BATCH 8
+#endif
 #ifndef THRS_LATE_CLEAR
 #define THRS_LATE_CLEAR 1
 #endif
@@ -309,7 +324,7 @@ template <int KB, int VB> struct PassGeom {
   static constexpr int THREADS = 64 * WAVES;
   static constexpr uint32_t TILE = (uint32_t)THREADS * KPT;
   static constexpr uint32_t STAGE = TILE / ROUNDS;
-  static constexpr uint32_t LDS_BYTES = STAGE * (KB + VB) + (WAVES + 1) * kBins * 4 + 16 * 4;
+  static constexpr uint32_t LDS_BYTES = STAGE * (KB + VB) + (WAVES + 1) * kBins * 4 + 16 * 4 + kStampLds;
   static_assert(TILE <= 65536, "slots are kept as 16-bit halves");
   static_assert(kGroup == 0 || (uint64_t)kGroup * TILE < kArrival, "group counts must fit below the arrival bits");
   static_assert((STAGE & (STAGE - 1)) == 0 && STAGE % THREADS == 0, "stage must be a power of two");
@@ -331,44 +346,52 @@ __device__ __forceinline__ uint32_t xcc_id() {
   return x;
 }
 
-// Two-level look-back for digit d of `tile` (THRS_GROUP > 0); writes the
+// Two-level look-back for digit d of one tile (THRS_GROUP > 0).  issue()
+// sends one round of status loads (this group's earlier tile rows + a window
+// of group rows); finish() consumes rounds until the walk ends, writes the
 // digit's global write offset to s_gofs[d] and, from the group's last tile,
-// publishes the group's inclusive prefix.
+// publishes the group's inclusive prefix.  The first round may be issued
+// early (THRS_EARLY_WINDOW: right after the tile aggregate) so its round trip
+// overlaps the local scan and the rank.
 template <typename ST>
-__device__ __forceinline__ void group_lookback(const ST* __restrict__ status, const GroupTables<ST>& grp, uint32_t tile,
-                                               uint32_t d, uint32_t realTot, uint32_t myBase, uint32_t localStart,
-                                               uint32_t* s_gofs, uint32_t* s_misc, uint32_t* errFlag,
-                                               uint64_t* __restrict__ stamps) {
-#ifdef THRS_STAMPS
-  // slot 16: first window issued, 17: first window consumed, 18: walk done (digit 0's thread)
-  const bool st0 = stamps && d == 0;
-  if (st0) stamps[(uint64_t)tile * kStampSlots + 16] = __builtin_amdgcn_s_memrealtime();
-#else
-  (void)stamps;
-#endif
-  const uint32_t g = tile / kGroup, gstart = g * kGroup;
-  const uint32_t gend = min(gstart + (uint32_t)kGroup, grp.nTiles);
+struct GroupWalk {
+  const ST* status;
+  const GroupTables<ST>* grp;
+  uint32_t tile, d, g, gstart, gend;
   uint32_t inGroup = 0, excl = 0, spins = 0, rounds = 0;
-  uint32_t jt = gstart;         // next earlier tile of this group to add (ascending)
-  int32_t jg = (int32_t)g - 1;  // next earlier group to add (descending); -1 = done
-  int32_t found = -1;           // group whose prefix ended the walk (diagnostics)
-  while (jt < tile || jg >= 0) {
-    ST wt[8];
-    ST wp[kGroupWindow];
-    uint32_t wa[kGroupWindow];
+  uint32_t jt;        // next earlier tile of this group to add (ascending)
+  int32_t jg;         // next earlier group to add (descending); -1 = done
+  int32_t found = -1; // group whose prefix ended the walk (diagnostics)
+  ST wt[kTileWindow];
+  ST wp[kGroupWindow];
+  uint32_t wa[kGroupWindow];
+
+  __device__ __forceinline__ GroupWalk(const ST* st, const GroupTables<ST>& gt, uint32_t t, uint32_t dd)
+      : status(st), grp(&gt), tile(t), d(dd) {
+    g = t / kGroup;
+    gstart = g * kGroup;
+    gend = min(gstart + (uint32_t)kGroup, gt.nTiles);
+    jt = gstart;
+    jg = (int32_t)g - 1;
+  }
+  __device__ __forceinline__ bool walking() const { return jt < tile || jg >= 0; }
+  __device__ __forceinline__ void issue() {
 #pragma unroll
-    for (int q = 0; q < 8; ++q)
+    for (int q = 0; q < kTileWindow; ++q)
       wt[q] = (jt + q < tile) ? load_agent(status + (uint64_t)(jt + q) * kBins + d) : (ST)0;
 #pragma unroll
     for (int q = 0; q < kGroupWindow; ++q) {
       const bool in = jg - q >= 0;
-      wp[q] = in ? load_agent(grp.gp + (uint64_t)(jg - q) * kBins + d) : (ST)0;
-      wa[q] = in ? load_agent(grp.ga + (uint64_t)(jg - q) * kBins + d) : 0u;
+      wp[q] = in ? load_agent(grp->gp + (uint64_t)(jg - q) * kBins + d) : (ST)0;
+      wa[q] = in ? load_agent(grp->ga + (uint64_t)(jg - q) * kBins + d) : 0u;
     }
     ++rounds;
+  }
+  // consume the issued round; true if something was not published yet
+  __device__ __forceinline__ bool consume() {
     bool stall = false;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
+    for (int q = 0; q < kTileWindow; ++q) {
       if (!stall && jt < tile) {
         if (wt[q] == 0) stall = true;
         else {
@@ -386,7 +409,7 @@ __device__ __forceinline__ void group_lookback(const ST* __restrict__ status, co
           found = jg;
           jg = -1;
         } else {
-          const uint32_t members = min((uint32_t)kGroup, grp.nTiles - (uint32_t)jg * kGroup);
+          const uint32_t members = min((uint32_t)kGroup, grp->nTiles - (uint32_t)jg * kGroup);
           if ((wa[q] >> 20) == members) {
             excl += wa[q] & (kArrival - 1);
             --jg;
@@ -397,50 +420,66 @@ __device__ __forceinline__ void group_lookback(const ST* __restrict__ status, co
         }
       }
     }
-#ifdef THRS_STAMPS
-    if (st0 && rounds == 1) {
-      uint32_t dep = inGroup + excl;
-      pin(dep);
-      stamps[(uint64_t)tile * kStampSlots + 17] = __builtin_amdgcn_s_memrealtime() + (dep & 0);
-    }
-#endif
-    if (stall && (jt < tile || jg >= 0)) {
-      if (++spins > (1u << 22)) {  // bounded spin: never hang the GPU
-        atomicOr(errFlag, 1u);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
+    return stall;
   }
-  excl += inGroup;
+  __device__ __forceinline__ void finish(bool issued, uint32_t realTot, uint32_t myBase, uint32_t localStart,
+                                         uint32_t* s_gofs, uint32_t* s_misc, uint32_t* errFlag,
+                                         uint64_t* __restrict__ stamps) {
 #ifdef THRS_STAMPS
-  if (stamps && (d & 63) == 0) {  // slots 8..11: walk end of waves 0..3
-    uint32_t dep = excl;
-    pin(dep);
-    const uint64_t tnow = __builtin_amdgcn_s_memrealtime();
-    stamps[(uint64_t)tile * kStampSlots + 8 + (d >> 6)] = tnow + (uint64_t)(dep == 0xFFFFFFFFu);
-  }
-#endif
-  s_gofs[d] = myBase + excl - localStart;
-  if (tile == gend - 1) {
-    store_agent(grp.gp + (uint64_t)g * kBins + d, Status<ST>::pre(excl + realTot));
-#if !THRS_LATE_CLEAR
-    if (grp.gaNext) {
-      grp.gaNext[(uint64_t)g * kBins + d] = 0;
-      grp.gpNext[(uint64_t)g * kBins + d] = 0;
-    }
-#endif
-  }
-#ifdef THRS_STAMPS
-  atomicMax(&s_misc[1], rounds);
-  atomicMax(&s_misc[2], spins);
-  atomicMax(&s_misc[3], (uint32_t)(tile - gstart) + (uint32_t)((int32_t)g - 1 - found) * kGroup);
+    // slot 16: walk (re)starts here, 17: first window consumed, 18: walk done (digit 0's thread)
+    const bool st0 = stamps && d == 0;
+    uint64_t* s_stamp = reinterpret_cast<uint64_t*>(s_misc + 16);
+    if (st0) s_stamp[16] = __builtin_amdgcn_s_memrealtime();
 #else
-  (void)s_misc;
-  (void)rounds;
-  (void)found;
+    (void)stamps;
 #endif
-}
+    while (walking()) {
+      if (!issued) issue();
+      issued = false;
+      const bool stall = consume();
+#ifdef THRS_STAMPS
+      if (st0 && rounds == 1) {
+        uint32_t dep = inGroup + excl;
+        pin(dep);
+        s_stamp[17] = __builtin_amdgcn_s_memrealtime() + (uint64_t)(dep == 0xFFFFFFFFu);
+      }
+#endif
+      if (stall && walking()) {
+        if (++spins > (1u << 22)) {  // bounded spin: never hang the GPU
+          atomicOr(errFlag, 1u);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    const uint32_t total = excl + inGroup;
+#ifdef THRS_STAMPS
+    if (stamps && (d & 63) == 0) {  // slots 8..11: walk end of waves 0..3
+      uint32_t dep = total;
+      pin(dep);
+      const uint64_t tnow = __builtin_amdgcn_s_memrealtime();
+      s_stamp[8 + (d >> 6)] = tnow + (uint64_t)(dep == 0xFFFFFFFFu);
+    }
+    if ((d & 63) == 0) {  // one lane per wave: a divergent atomicMax would compile to a 64-step loop
+      atomicMax(&s_misc[1], rounds);
+      atomicMax(&s_misc[2], spins);
+      atomicMax(&s_misc[3], (uint32_t)(tile - gstart) + (uint32_t)((int32_t)g - 1 - found) * kGroup);
+    }
+#else
+    (void)s_misc;
+#endif
+    s_gofs[d] = myBase + total - localStart;
+    if (tile == gend - 1) {
+      store_agent(grp->gp + (uint64_t)g * kBins + d, Status<ST>::pre(total + realTot));
+#if !THRS_LATE_CLEAR
+      if (grp->gaNext) {
+        grp->gaNext[(uint64_t)g * kBins + d] = 0;
+        grp->gpNext[(uint64_t)g * kBins + d] = 0;
+      }
+#endif
+    }
+  }
+};
 
 // Everything one workgroup does for one tile (phases A-E below).
 //   tile        global tile index (rows of the status table, key range)
@@ -448,13 +487,52 @@ __device__ __forceinline__ void group_lookback(const ST* __restrict__ status, co
 //               publishes its prefix directly
 //   myBase      (thread d < 256) global output base of digit d for the chain
 // Returns after the tile's last store is issued.
-template <int KT, int VB, typename ST, bool ATOMIC_RANK>
+// Load one tile's keys (and values) into registers: item j of lane l of wave
+// w is key w*64*KPT + j*64 + l of the tile (blocked by wave, striped by lane),
+// which is the order the stable rank walks.  Keys past n read as 0.
+template <int KT, int VB>
+__device__ __forceinline__ void load_tile(const typename KeyTraits<KT>::U* __restrict__ keysIn,
+                                          const typename ValueWord<VB>::T* __restrict__ valsIn, uint32_t n,
+                                          uint32_t tile,
+                                          typename KeyTraits<KT>::U (&k)[PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::KPT],
+                                          typename ValueWord<VB>::T (&v)[VB ? PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::KPT : 1]) {
+  using U = typename KeyTraits<KT>::U;
+  using VW = typename ValueWord<VB>::T;
+  using G = PassGeom<sizeof(U), VB>;
+  constexpr int KPT = G::KPT;
+  constexpr uint32_t T = G::TILE, CHUNK = 64 * KPT;
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t tileBase = (uint64_t)tile * T;
+  const uint32_t valid = (uint32_t)min((uint64_t)T, (uint64_t)n - tileBase);
+  const uint64_t chunkBase = tileBase + w * CHUNK;
+  int32_t lim = (int32_t)valid - (int32_t)(w * CHUNK + lane);  // item j is real iff j*64 < lim
+  pin(reinterpret_cast<uint32_t&>(lim));
+  if (valid == T) {
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) k[j] = keysIn[chunkBase + j * 64 + lane];
+  } else {
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) k[j] = (j * 64 < lim) ? keysIn[chunkBase + j * 64 + lane] : (U)0;
+  }
+  if constexpr (VB != 0) {
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) v[j] = (valid == T || j * 64 < lim) ? valsIn[chunkBase + j * 64 + lane] : VW{};
+  }
+}
+
+struct NoMid {
+  __device__ __forceinline__ void operator()() const {}
+};
+
+template <int KT, int VB, typename ST, bool ATOMIC_RANK, typename Mid>
 __device__ __forceinline__ void pass_tile(
     const typename KeyTraits<KT>::U* __restrict__ keysIn, typename KeyTraits<KT>::U* __restrict__ keysOut,
     const typename ValueWord<VB>::T* __restrict__ valsIn, typename ValueWord<VB>::T* __restrict__ valsOut,
     uint32_t n, typename KeyTraits<KT>::U orderMask, int shift, uint32_t myBase, ST* __restrict__ status,
     ST* __restrict__ statusNext, uint32_t* __restrict__ errFlag, uint32_t tile, uint32_t chainStart,
-    const GroupTables<ST>& grp, unsigned char* smem, uint64_t* __restrict__ stamps) {
+    const GroupTables<ST>& grp, unsigned char* smem, uint64_t* __restrict__ stamps,
+    typename KeyTraits<KT>::U (&k)[PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::KPT],
+    typename ValueWord<VB>::T (&v)[VB ? PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::KPT : 1], Mid mid) {
   using U = typename KeyTraits<KT>::U;
   using VW = typename ValueWord<VB>::T;
   using G = PassGeom<sizeof(U), VB>;
@@ -469,12 +547,16 @@ __device__ __forceinline__ void pass_tile(
   uint32_t* s_gofs = s_cnt + WAVES * kBins;
   uint32_t* s_misc = s_gofs + kBins;
   const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+#ifdef THRS_STAMPS
+  uint64_t* s_stamp = reinterpret_cast<uint64_t*>(s_misc + 16);  // flushed once per tile (a global
+                                                                  // store mid-tile would perturb timing)
+#endif
   // Diagnostic builds (-DTHRS_STAMPS) record s_memrealtime (100 MHz) per
   // phase for every tile into stamps[tile*kStampSlots + i]; normal builds compile none.
 #ifdef THRS_STAMPS
 #define THRS_STAMP(i)                                                                                  \
   do {                                                                                                 \
-    if (stamps && threadIdx.x == 0) stamps[(uint64_t)tile * kStampSlots + (i)] = __builtin_amdgcn_s_memrealtime(); \
+    if (stamps && threadIdx.x == 0) s_stamp[(i)] = __builtin_amdgcn_s_memrealtime();                     \
   } while (0)
 #else
 #define THRS_STAMP(i) \
@@ -487,33 +569,15 @@ __device__ __forceinline__ void pass_tile(
   const uint64_t tileBase = (uint64_t)tile * T;
   const uint32_t valid = (uint32_t)min((uint64_t)T, (uint64_t)n - tileBase);
   const bool full = valid == T;
-  const uint64_t chunkBase = tileBase + w * CHUNK;
-
-  U k[KPT];
-  if (full) {
-#pragma unroll
-    for (int j = 0; j < KPT; ++j) k[j] = keysIn[chunkBase + j * 64 + lane];
-  } else {
-#pragma unroll
-    for (int j = 0; j < KPT; ++j) {
-      const uint32_t local = w * CHUNK + j * 64 + lane;
-      k[j] = (local < valid) ? keysIn[chunkBase + j * 64 + lane] : (U)0;
-    }
-  }
-  VW v[VB ? KPT : 1];
-  if constexpr (VB != 0) {
-#pragma unroll
-    for (int j = 0; j < KPT; ++j) {
-      const uint32_t local = w * CHUNK + j * 64 + lane;
-      if (full || local < valid) v[j] = valsIn[chunkBase + j * 64 + lane];
-      else v[j] = VW{};
-    }
-  }
   const uint32_t d = tid & 255u;
 
+  // partial tile: item j is real iff j*64 < lim (one register; pinned so the
+  // per-item positions are never hoisted into 32 live registers)
+  int32_t lim = (int32_t)valid - (int32_t)(w * CHUNK + lane);
+  pin(reinterpret_cast<uint32_t&>(lim));
   auto digit_of = [&](U key, int j) -> uint32_t {
     uint32_t dd = (uint32_t)((KeyTraits<KT>::bits(key) ^ orderMask) >> shift) & 0xFFu;
-    if (!full) dd = (w * CHUNK + j * 64 + lane < valid) ? dd : 0xFFu;  // padding sorts after every real key
+    if (!full) dd = (j * 64 < lim) ? dd : 0xFFu;  // padding sorts after every real key
     return dd;
   };
 
@@ -549,6 +613,12 @@ __device__ __forceinline__ void pass_tile(
       __hip_atomic_fetch_add(&grp.ga[(uint64_t)(tile / kGroup) * kBins + dp], real2 + kArrival, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
   }
+  GroupWalk<ST> gw(status, grp, tile, d);
+  if constexpr (kGroup > 0) {
+#if THRS_EARLY_WINDOW
+    if (tid < 256 && tile != 0) gw.issue();  // first round in flight during the scan and the rank
+#endif
+  }
   // Look-back window loader: rows j, j-1, ... of column d.  32-bit byte offsets
   // from the uniform base -> saddr loads, one VGPR each.
   ST win[kLookWindow];
@@ -564,7 +634,8 @@ __device__ __forceinline__ void pass_tile(
   };
 #if THRS_EARLY_WINDOW
   // first window in flight during the local scan and the rank (phase C)
-  if (tid < 256 && tile != chainStart) issue_window();
+  if constexpr (kGroup == 0)
+    if (tid < 256 && tile != chainStart) issue_window();
 #endif
   // local exclusive scan over the 256 digits (waves 0-3)
   uint32_t localStart = 0;
@@ -614,12 +685,23 @@ __device__ __forceinline__ void pass_tile(
     __builtin_amdgcn_sched_barrier(0);
   }
   THRS_STAMP(4);
+  if constexpr (ROUNDS == 1) {
+    // one LDS round: place the tile in sorted order now, freeing the key
+    // registers before the walk (the post-walk barrier orders it for E)
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) {
+      const uint32_t slot = (sl[j / 2] >> (16 * (j & 1))) & 0xFFFFu;
+      stage_k[slot] = k[j];
+      if constexpr (VB != 0) stage_v[slot] = v[j];
+    }
+  }
 
 
   // ---- D: decoupled look-back for digit d, kLookWindow rows per round trip;
   // a not-yet-published word stops the window and is re-polled.
   if constexpr (kGroup > 0) {
-    if (tid < 256) group_lookback<ST>(status, grp, tile, d, realTot, myBase, localStart, s_gofs, s_misc, errFlag, stamps);
+    if (tid < 256) gw.finish(THRS_EARLY_WINDOW && tile != 0, realTot, myBase, localStart, s_gofs, s_misc, errFlag,
+                             stamps);
 #if !THRS_LATE_CLEAR
     if (tid < 256 && statusNext) statusNext[(uint64_t)tile * kBins + d] = 0;  // ready for the next pass
 #endif
@@ -628,7 +710,7 @@ __device__ __forceinline__ void pass_tile(
       uint32_t dep = s_gofs[d & 255];
       pin(dep);
       const uint64_t tnow = __builtin_amdgcn_s_memrealtime();
-      stamps[(uint64_t)tile * kStampSlots + 12 + w] = tnow + (uint64_t)(dep == 0xFFFFFFFFu);
+      s_stamp[12 + w] = tnow + (uint64_t)(dep == 0xFFFFFFFFu);
     }
 #endif
   } else if (tid < 256) {
@@ -638,7 +720,7 @@ __device__ __forceinline__ void pass_tile(
 #endif
     if (tile != chainStart) {
       uint32_t spins = 0;
-      bool pending = THRS_EARLY_WINDOW;  // the first window is already in flight
+      bool pending = THRS_EARLY_WINDOW && kGroup == 0;  // the first window is already in flight
       while (true) {
         if (!pending) issue_window();
         pending = false;
@@ -670,9 +752,11 @@ __device__ __forceinline__ void pass_tile(
       }
       store_agent(myStatus, Status<ST>::pre(excl + realTot));
 #ifdef THRS_STAMPS
-      atomicMax(&s_misc[1], dbgRounds);
-      atomicMax(&s_misc[2], spins);
-      atomicMax(&s_misc[3], (uint32_t)(tile - 1 - j));
+      if ((d & 63) == 0) {
+        atomicMax(&s_misc[1], dbgRounds);
+        atomicMax(&s_misc[2], spins);
+        atomicMax(&s_misc[3], (uint32_t)(tile - 1 - j));
+      }
 #endif
     }
     s_gofs[d] = myBase + excl - localStart;
@@ -683,18 +767,38 @@ __device__ __forceinline__ void pass_tile(
   lds_barrier();
   THRS_STAMP(5);
 
+  mid();  // persistent kernel: take the next tile and start its loads (k/v are free)
+
   // ---- E: ROUNDS x (scatter this round's slots into the stage, write it out)
 #pragma unroll 1
   for (int r = 0; r < ROUNDS; ++r) {
+    if constexpr (ROUNDS > 1) {
+      // keep slot-derived addresses inside the round (else they are hoisted
+      // out of the round loop as 32 live registers and spilled)
 #pragma unroll
-    for (int j = 0; j < KPT; ++j) {
-      const uint32_t slot = (sl[j / 2] >> (16 * (j & 1))) & 0xFFFFu;
-      if ((slot >> STAGE_SHIFT) == (uint32_t)r) {
-        stage_k[slot & (STAGE - 1)] = k[j];
-        if constexpr (VB != 0) stage_v[slot & (STAGE - 1)] = v[j];
+      for (int j = 0; j < (KPT + 1) / 2; ++j) pin(sl[j]);
+#if THRS_RELOAD_KEYS
+      // re-read this round's keys from the tile's input (L2 / Infinity Cache
+      // hits) rather than holding KPT keys in registers across the walk
+      const uint64_t chunkBase = (uint64_t)tile * T + w * CHUNK;
+#endif
+#pragma unroll
+      for (int j = 0; j < KPT; ++j) {
+        const uint32_t slot = (sl[j / 2] >> (16 * (j & 1))) & 0xFFFFu;
+        if ((slot >> STAGE_SHIFT) == (uint32_t)r) {
+#if THRS_RELOAD_KEYS
+          // padding items of a partial tile (j*64 >= lim) lie past n: never read them
+          const bool real = full || j * 64 < lim;
+          stage_k[slot & (STAGE - 1)] = real ? keysIn[chunkBase + j * 64 + lane] : (U)0;
+          if constexpr (VB != 0) stage_v[slot & (STAGE - 1)] = real ? valsIn[chunkBase + j * 64 + lane] : VW{};
+#else
+          stage_k[slot & (STAGE - 1)] = k[j];
+          if constexpr (VB != 0) stage_v[slot & (STAGE - 1)] = v[j];
+#endif
+        }
       }
+      lds_barrier();
     }
-    lds_barrier();
 #pragma unroll
     for (int j = 0; j < (int)(STAGE / THREADS); ++j) {
       const uint32_t i = j * THREADS + tid;
@@ -706,6 +810,9 @@ __device__ __forceinline__ void pass_tile(
         keysOut[dst] = key;
         if constexpr (VB != 0) valsOut[dst] = stage_v[i];
       }
+      // bound the batch the scheduler hoists (LDS reads + 64-bit addresses):
+      // in the persistent kernel the next tile's keys are live here
+      if ((j % THRS_WO_BATCH) == THRS_WO_BATCH - 1) __builtin_amdgcn_sched_barrier(0);
     }
     if (r + 1 < ROUNDS) lds_barrier();
   }
@@ -728,8 +835,10 @@ __device__ __forceinline__ void pass_tile(
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   THRS_STAMP(6);
   if (stamps && tid == 0)  // slot 7: xcc | max rounds << 8 | max depth << 24 | max stalls << 40
-    stamps[(uint64_t)tile * kStampSlots + 7] |= ((uint64_t)min(s_misc[1], 65535u) << 8) |
-                                      ((uint64_t)min(s_misc[3], 65535u) << 24) | ((uint64_t)s_misc[2] << 40);
+    s_stamp[7] |= ((uint64_t)min(s_misc[1], 65535u) << 8) | ((uint64_t)min(s_misc[3], 65535u) << 24) |
+                  ((uint64_t)s_misc[2] << 40);
+  lds_barrier();
+  if (stamps && tid < (uint32_t)kStampSlots) stamps[(uint64_t)tile * kStampSlots + tid] = s_stamp[tid];
 #endif
 #undef THRS_STAMP
 }
@@ -763,12 +872,77 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
   const uint32_t tile = s_misc[0];
 #ifdef THRS_STAMPS
   if (stamps && tid == 0) {
-    stamps[(uint64_t)tile * kStampSlots + 0] = t_entry;
-    stamps[(uint64_t)tile * kStampSlots + 7] = xcc_id();
+    uint64_t* s_stamp = reinterpret_cast<uint64_t*>(s_misc + 16);
+    for (int i = 0; i < kStampSlots; ++i) s_stamp[i] = 0;
+    s_stamp[0] = t_entry;
+    s_stamp[7] = xcc_id();
   }
 #endif
+  typename KeyTraits<KT>::U k[G::KPT];
+  typename ValueWord<VB>::T v[VB ? G::KPT : 1];
+  load_tile<KT, VB>(keysIn, valsIn, n, tile, k, v);
   pass_tile<KT, VB, ST, ATOMIC_RANK>(keysIn, keysOut, valsIn, valsOut, n, orderMask, shift, myBase, status,
-                                            statusNext, errFlag, tile, 0, grp, smem, stamps);
+                                     statusNext, errFlag, tile, 0, grp, smem, stamps, k, v, NoMid{});
+}
+
+// Persistent form (THRS_PIPE): a fixed grid of workgroups loops over tiles.
+// Between a tile's walk and its write-out the workgroup takes the next tile id
+// and issues that tile's loads, so they are in flight while the stage drains
+// (the tile's own prefix is published as early as in thrs_pass).  Needs a
+// single LDS round (the tile sits in the stage, not in registers, during the
+// walk).  Every tile id handed out belongs to a running workgroup, so every
+// walk terminates.
+template <int KT, int VB, typename ST, bool ATOMIC_RANK>
+__global__ __launch_bounds__((PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::THREADS))
+__attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::WPE))) void thrs_pass_pipe(
+    const typename KeyTraits<KT>::U* __restrict__ keysIn, typename KeyTraits<KT>::U* __restrict__ keysOut,
+    const typename ValueWord<VB>::T* __restrict__ valsIn, typename ValueWord<VB>::T* __restrict__ valsOut,
+    uint32_t n, typename KeyTraits<KT>::U orderMask, int shift, const uint32_t* __restrict__ digitBase,
+    ST* __restrict__ status, ST* __restrict__ statusNext, uint32_t* __restrict__ tileCounter,
+    uint32_t* __restrict__ errFlag, GroupTables<ST> grp, uint64_t* __restrict__ stamps) {
+  using U = typename KeyTraits<KT>::U;
+  using VW = typename ValueWord<VB>::T;
+  using G = PassGeom<sizeof(U), VB>;
+  static_assert(G::ROUNDS == 1, "the persistent pass keeps a whole tile in the LDS stage");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint32_t* s_cnt = reinterpret_cast<uint32_t*>(smem + G::STAGE * (sizeof(U) + VB));
+  uint32_t* s_misc = s_cnt + (G::WAVES + 1) * kBins;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t nTiles = (uint32_t)(((uint64_t)n + G::TILE - 1) / G::TILE);
+  if (tid == 0) s_misc[0] = atomicAdd(tileCounter, 1u);
+  for (uint32_t i = tid; i < (uint32_t)(G::WAVES * kBins); i += G::THREADS) s_cnt[i] = 0;
+  const uint32_t myBase = digitBase[tid & 255u];
+  lds_barrier();
+  uint32_t tile = s_misc[0];
+  if (tile >= nTiles) return;
+  U k[G::KPT];
+  VW v[VB ? G::KPT : 1];
+  load_tile<KT, VB>(keysIn, valsIn, n, tile, k, v);
+  for (;;) {
+#ifdef THRS_STAMPS
+    if (stamps && tid == 0) {
+      uint64_t* s_stamp = reinterpret_cast<uint64_t*>(s_misc + 16);
+      for (int i = 0; i < kStampSlots; ++i) s_stamp[i] = 0;
+      s_stamp[0] = __builtin_amdgcn_s_memrealtime();
+      s_stamp[7] = xcc_id();
+      s_misc[1] = s_misc[2] = s_misc[3] = 0;
+    }
+#endif
+    uint32_t next = 0xFFFFFFFFu;
+    auto mid = [&]() __attribute__((always_inline)) {
+      if (tid == 0) s_misc[8] = atomicAdd(tileCounter, 1u);
+      lds_barrier();
+      next = s_misc[8];
+      if (next < nTiles) load_tile<KT, VB>(keysIn, valsIn, n, next, k, v);
+    };
+    pass_tile<KT, VB, ST, ATOMIC_RANK>(keysIn, keysOut, valsIn, valsOut, n, orderMask, shift, myBase, status,
+                                       statusNext, errFlag, tile, 0, grp, smem, stamps, k, v, mid);
+    // every wave is past its write-out: the stage, s_gofs and s_cnt are free
+    for (uint32_t i = tid; i < (uint32_t)(G::WAVES * kBins); i += G::THREADS) s_cnt[i] = 0;
+    lds_barrier();
+    tile = next;
+    if (tile >= nTiles) break;
+  }
 }
 
 
