@@ -26,6 +26,8 @@
 template <int THREADS, int KPT>
 __global__ __launch_bounds__(THREADS) void scatter_runs(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
                                                        uint32_t n) {
+  extern __shared__ uint32_t dummy_lds[];  // occupancy control only
+  if (n == 0) dummy_lds[threadIdx.x] = 0;
   constexpr uint32_t T = THREADS * KPT, RUN = T / 256;
   const uint32_t tile = blockIdx.x;
   const uint32_t regionKeys = n / 256;
@@ -48,15 +50,18 @@ __global__ void copy4(const uint4* __restrict__ a, uint4* __restrict__ b, size_t
 }
 
 template <int THREADS, int KPT>
-double time_scatter(const uint32_t* in, uint32_t* out, uint32_t n, int reps) {
+double time_scatter(const uint32_t* in, uint32_t* out, uint32_t n, int reps, size_t lds = 0) {
   constexpr uint32_t T = THREADS * KPT;
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  hipLaunchKernelGGL((scatter_runs<THREADS, KPT>), dim3(n / T), dim3(THREADS), 0, 0, in, out, n);
+  if (lds > 65536)
+    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(scatter_runs<THREADS, KPT>),
+                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL((scatter_runs<THREADS, KPT>), dim3(n / T), dim3(THREADS), lds, 0, in, out, n);
   CK(hipEventRecord(e0, 0));
   for (int r = 0; r < reps; ++r)
-    hipLaunchKernelGGL((scatter_runs<THREADS, KPT>), dim3(n / T), dim3(THREADS), 0, 0, in, out, n);
+    hipLaunchKernelGGL((scatter_runs<THREADS, KPT>), dim3(n / T), dim3(THREADS), lds, 0, in, out, n);
   CK(hipEventRecord(e1, 0));
   CK(hipEventSynchronize(e1));
   float ms;
@@ -79,6 +84,9 @@ int main() {
   rep("run32_tile8K_256thr", time_scatter<256, 32>(in, out, n, reps));
   rep("run64_tile16K_512thr", time_scatter<512, 32>(in, out, n, reps));
   rep("run64_tile16K_1024thr", time_scatter<1024, 16>(in, out, n, reps));
+  rep("run64_tile16K_512thr_lds73K(2WG/CU)", time_scatter<512, 32>(in, out, n, reps, 73 * 1024));
+  rep("run64_tile16K_512thr_lds50K(3WG/CU)", time_scatter<512, 32>(in, out, n, reps, 50 * 1024));
+  rep("run64_tile16K_512thr_lds150K(1WG/CU)", time_scatter<512, 32>(in, out, n, reps, 150 * 1024));
   rep("run128_tile32K_1024thr", time_scatter<1024, 32>(in, out, n, reps));
   rep("run256_tile64K_1024thr", time_scatter<1024, 64>(in, out, n, reps));
   {

@@ -310,13 +310,40 @@ template <> struct PassCfg<4, 0> {
   static constexpr int CFG[4] = {THRS_K4V0_CFG};  // waves, keys/thread, rounds, min waves per SIMD
   static constexpr int WAVES = CFG[0], KPT = CFG[1], ROUNDS = CFG[2], WPE = CFG[3];
 };
-template <> struct PassCfg<4, 4> { static constexpr int WAVES = 16, KPT = 16, ROUNDS = 4, WPE = 4; };
-template <> struct PassCfg<4, 8> { static constexpr int WAVES = 16, KPT = 16, ROUNDS = 8, WPE = 4; };
-template <> struct PassCfg<4, 16> { static constexpr int WAVES = 16, KPT = 8, ROUNDS = 8, WPE = 4; };
-template <> struct PassCfg<8, 0> { static constexpr int WAVES = 16, KPT = 16, ROUNDS = 4, WPE = 4; };
-template <> struct PassCfg<8, 4> { static constexpr int WAVES = 16, KPT = 16, ROUNDS = 8, WPE = 4; };
-template <> struct PassCfg<8, 8> { static constexpr int WAVES = 16, KPT = 16, ROUNDS = 8, WPE = 4; };
-template <> struct PassCfg<8, 16> { static constexpr int WAVES = 16, KPT = 8, ROUNDS = 8, WPE = 4; };
+#ifndef THRS_K4V4_CFG
+#define THRS_K4V4_CFG 16, 16, 4, 4
+#endif
+#ifndef THRS_K4V8_CFG
+#define THRS_K4V8_CFG 16, 16, 8, 4
+#endif
+#ifndef THRS_K4V16_CFG
+#define THRS_K4V16_CFG 16, 8, 8, 4
+#endif
+#ifndef THRS_K8V0_CFG
+#define THRS_K8V0_CFG 8, 16, 1, 4
+#endif
+#ifndef THRS_K8V4_CFG
+#define THRS_K8V4_CFG 16, 16, 8, 4
+#endif
+#ifndef THRS_K8V8_CFG
+#define THRS_K8V8_CFG 8, 16, 2, 4
+#endif
+#ifndef THRS_K8V16_CFG
+#define THRS_K8V16_CFG 16, 8, 8, 4
+#endif
+#define THRS_PASS_CFG(KB_, VB_, MACRO)                                           \
+  template <> struct PassCfg<KB_, VB_> {                                          \
+    static constexpr int CFG[4] = {MACRO};                                        \
+    static constexpr int WAVES = CFG[0], KPT = CFG[1], ROUNDS = CFG[2], WPE = CFG[3]; \
+  };
+THRS_PASS_CFG(4, 4, THRS_K4V4_CFG)
+THRS_PASS_CFG(4, 8, THRS_K4V8_CFG)
+THRS_PASS_CFG(4, 16, THRS_K4V16_CFG)
+THRS_PASS_CFG(8, 0, THRS_K8V0_CFG)
+THRS_PASS_CFG(8, 4, THRS_K8V4_CFG)
+THRS_PASS_CFG(8, 8, THRS_K8V8_CFG)
+THRS_PASS_CFG(8, 16, THRS_K8V16_CFG)
+#undef THRS_PASS_CFG
 
 template <int KB, int VB> struct PassGeom {
   static constexpr int WAVES = PassCfg<KB, VB>::WAVES, KPT = PassCfg<KB, VB>::KPT, ROUNDS = PassCfg<KB, VB>::ROUNDS;
@@ -832,7 +859,9 @@ __device__ __forceinline__ void pass_tile(
   }
 #endif
 #ifdef THRS_STAMPS
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifndef THRS_STAMPS_NOWAIT
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // slot 6 = stores drained (NOWAIT: issued)
+#endif
   THRS_STAMP(6);
   if (stamps && tid == 0)  // slot 7: xcc | max rounds << 8 | max depth << 24 | max stalls << 40
     s_stamp[7] |= ((uint64_t)min(s_misc[1], 65535u) << 8) | ((uint64_t)min(s_misc[3], 65535u) << 24) |
