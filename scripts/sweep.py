@@ -48,6 +48,8 @@ def main():
     ap.add_argument("--n", type=int, default=None)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--vendor", action="store_true", help="also time hipcub::DeviceRadixSort")
+    ap.add_argument("--iota", action="store_true",
+                    help="keys = 0..n-1 (u32): every pass sees exactly T/256 keys per digit per tile")
     ap.add_argument("--nocheck", default="", help="comma list of EXPERIMENT variants whose output is knowingly wrong")
     ap.add_argument("variants", nargs="*")
     a = ap.parse_args()
@@ -85,7 +87,10 @@ def main():
         res["hipcub"] = {"ms": [], "pass_ms": [], "hist_ms": []}
     for r in range(a.rounds + 1):
         for name, L in libs:
-            TU.fill_keys(kt, keys, n, start=r * n)
+            if a.iota:
+                TU.iota(kb, keys, n)
+            else:
+                TU.fill_keys(kt, keys, n, start=r * n)
             if vb:
                 TU.iota(vb, vals, n)
             fp = TU.fingerprint(kt, keys, n) if r == 1 else None

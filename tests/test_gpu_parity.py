@@ -144,6 +144,17 @@ def test_cpp_port_of_reference_unittest(gpu):
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
 
 
+@pytest.mark.parametrize("xb", ["1", "0"])
+def test_cpp_port_with_claim_mode_forced(gpu, xb):
+    """The same UTEST matrix with the XCD-block tile claims (thrs_pass_xb)
+    forced on for every configuration and size (THRS_XB=1), and forced off
+    (THRS_XB=0): by default they only run for 4-byte keys at n >= 2^29."""
+    exe = os.path.join(ROOT, "tests", "cpp", "unittest_thrs")
+    env = dict(os.environ, THRS_XB=xb)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=900, env=env)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
+
+
 def test_concurrent_sorts_on_distinct_temps(gpu):
     """Per-call state lives in the caller's temp buffer: two sorts on two
     streams at once (the reference's module-global g_iterator would race)."""

@@ -29,6 +29,9 @@
 #ifndef THRS_PIPE
 #define THRS_PIPE 0
 #endif
+#ifndef THRS_XB
+#define THRS_XB 1
+#endif
 
 using namespace thrs_dev;
 
@@ -72,7 +75,8 @@ struct Plan {
   uint64_t gaBytes;       // group aggregates [nGroups][256] u32 (kGroup > 0)
   uint64_t gpBytes;       // group prefixes   [nGroups][256] status words
   uint64_t setBytes;      // one look-back table set = status + ga + gp
-  uint64_t scratchBytes;  // header + 2 sets (ping-pong between passes)
+  uint64_t claimBytes;    // per pass: XCD-block claim state (tickets, block counter, 8 block tables)
+  uint64_t scratchBytes;  // header + 2 sets (ping-pong between passes) + 8 claim areas
 };
 
 Plan make_plan(int keyType, int valueBytesOrZero, uint32_t n) {
@@ -87,7 +91,9 @@ Plan make_plan(int keyType, int valueBytesOrZero, uint32_t n) {
   p.gaBytes = round_up(nGroups * kBins * 4, kAlign);
   p.gpBytes = round_up(nGroups * kBins * (p.wideStatus ? 8 : 4), kAlign);
   p.setBytes = p.statusBytes + p.gaBytes + p.gpBytes;
-  p.scratchBytes = kHeaderBytes + 2 * p.setBytes;
+  const uint64_t nXb = (p.nTiles + kXcdBlock - 1) / kXcdBlock + 16;  // table stride (see xb_claim)
+  p.claimBytes = round_up((16 + 8 * nXb) * 4, kAlign);
+  p.scratchBytes = kHeaderBytes + 2 * p.setBytes + 8 * p.claimBytes;
   return p;
 }
 
@@ -183,6 +189,18 @@ int probe_rank_mode(hipStream_t stream) {
   return g_rank_mode[dev];
 }
 
+// THRS_XB=1 / THRS_XB=0 in the environment: force XCD-block claims on / off
+// for every configuration (-1 = size/type heuristic).  Read once.
+int xb_override() {
+  static const int v = [] {
+    const char* e = getenv("THRS_XB");
+    if (e && !strcmp(e, "1")) return 1;
+    if (e && !strcmp(e, "0")) return 0;
+    return -1;
+  }();
+  return v;
+}
+
 template <typename F>
 hipError_t allow_lds(F kernel, size_t bytes) {
   if (bytes <= 65536) return hipSuccess;
@@ -225,6 +243,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
 
   // header (histograms, tile counters, error word) + first status table
   if (hipMemsetAsync(scratch, 0, kHeaderBytes + plan.setBytes, stream) != hipSuccess) return THRS_ERROR_HIP;
+  char* claim = scratch + kHeaderBytes + 2 * plan.setBytes;  // 8 per-pass claim areas
 
   {  // histograms of every pass in one read of the keys
     ProfScope prof(stream, 0);
@@ -244,6 +263,19 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   const bool atomicRank = probe_rank_mode(stream) != 0;
   auto kernel = atomicRank ? thrs_pass<KT, VB, ST, true> : thrs_pass<KT, VB, ST, false>;
   uint32_t grid = (uint32_t)plan.nTiles;
+  // XCD-block claims (thrs_pass_xb) pay off where runs are short and the
+  // grid is large: 4-byte keys without values, n >= 2^29 (docs/EXPERIMENTS.md
+  // row 19: +4-6% there, neutral at 2^28, -2..-6% for pairs / f32 at 2^28).
+  const int xbEnv = xb_override();  // THRS_XB=1 / 0 in the environment forces it on / off (tests)
+  const bool useXb = xbEnv >= 0 ? xbEnv == 1 : (THRS_XB && sizeof(U) == 4 && VB == 0 && n >= (1u << 29));
+  if (useXb) {
+    kernel = atomicRank ? thrs_pass_xb<KT, VB, ST, true> : thrs_pass_xb<KT, VB, ST, false>;
+    if (allow_lds(kernel, lds) != hipSuccess) return THRS_ERROR_HIP;
+    int perCU = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, kernel, G::THREADS, lds) != hipSuccess || perCU < 1)
+      perCU = 1;
+    grid = (uint32_t)std::min<uint64_t>(plan.nTiles, (uint64_t)perCU * cu_count());
+  }
 #if THRS_PIPE
   if constexpr (G::ROUNDS == 1) {  // persistent: as many workgroups as fit at once
     kernel = atomicRank ? thrs_pass_pipe<KT, VB, ST, true> : thrs_pass_pipe<KT, VB, ST, false>;
@@ -255,6 +287,8 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   }
 #endif
   if (allow_lds(kernel, lds) != hipSuccess) return THRS_ERROR_HIP;
+  if (useXb && hipMemsetAsync(claim, 0, (size_t)nPass * plan.claimBytes, stream) != hipSuccess)
+    return THRS_ERROR_HIP;
 
   U* kin = static_cast<U*>(keys);
   U* kout = keyOut;
@@ -268,7 +302,9 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     g.gpNext = more ? grp[(p + 1) & 1].gp : nullptr;
     ProfScope prof(stream, 1);
     hipLaunchKernelGGL(kernel, dim3(grid), dim3(G::THREADS), lds, stream, kin, kout, vin, vout, n,
-                       orderMask, startBits + 8 * p, base + p * kBins, status[p & 1], next, counters + p, err, g,
+                       orderMask, startBits + 8 * p, base + p * kBins, status[p & 1], next,
+                       useXb ? reinterpret_cast<uint32_t*>(claim + p * plan.claimBytes) : counters + p,
+                       err, g,
                        g_stamps ? g_stamps + (uint64_t)p * plan.nTiles * kStampSlots : nullptr);
     std::swap(kin, kout);
     std::swap(vin, vout);

@@ -726,7 +726,14 @@ __device__ __forceinline__ void pass_tile(
 
   // ---- D: decoupled look-back for digit d, kLookWindow rows per round trip;
   // a not-yet-published word stops the window and is re-polled.
+#ifdef THRS_FAKE_WALK
+  // EXPERIMENT ONLY (wrong output): no look-back; offsets approximated from
+  // this tile's own counts (uniform keys -> nearly the real write pattern)
+  if (tid < 256) s_gofs[d] = myBase + tile * realTot - localStart;
+  if (false) {
+#else
   if constexpr (kGroup > 0) {
+#endif
     if (tid < 256) gw.finish(THRS_EARLY_WINDOW && tile != 0, realTot, myBase, localStart, s_gofs, s_misc, errFlag,
                              stamps);
 #if !THRS_LATE_CLEAR
@@ -833,7 +840,11 @@ __device__ __forceinline__ void pass_tile(
       if (full || slot < valid) {
         const U key = stage_k[i];
         const uint32_t dd = (uint32_t)((KeyTraits<KT>::bits(key) ^ orderMask) >> shift) & 0xFFu;
+#ifdef THRS_FAKE_WALK
+        const uint32_t dst = min(s_gofs[dd] + slot, n - 1);  // stay in bounds
+#else
         const uint32_t dst = s_gofs[dd] + slot;
+#endif
         keysOut[dst] = key;
         if constexpr (VB != 0) valsOut[dst] = stage_v[i];
       }
@@ -892,7 +903,12 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
 #endif
   const uint32_t tid = threadIdx.x;
   if (tid == 0) {
+#if defined(THRS_FAKE_WALK) && defined(THRS_FAKE_STATIC_TILE)
+    s_misc[0] = blockIdx.x;  // EXPERIMENT ONLY: no walk, so no wait: static ids cannot deadlock
+    (void)tileCounter;
+#else
     s_misc[0] = atomicAdd(tileCounter, 1u);
+#endif
     s_misc[1] = s_misc[2] = s_misc[3] = 0;  // diagnostic maxima (THRS_STAMPS)
   }
   for (uint32_t i = tid; i < (uint32_t)(G::WAVES * kBins); i += G::THREADS) s_cnt[i] = 0;
@@ -974,6 +990,108 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
   }
 }
 
+
+// ============================================================ XCD-block claims
+// Tiles are claimed in BLOCKS of kXcdBlock consecutive tiles, one open block
+// per XCD, so neighbouring tiles -- whose digit runs share the 128-B lines at
+// their boundaries -- are written through the same L2, which merges the two
+// partial halves before write-back.  (Consecutive tiles on different XCDs
+// leave two partial line writes each, which HBM with ECC serves as
+// read-modify-write: scripts/abut_probe.hip measured 2.7 vs 4.1 TB/s.)
+// Lock-free claims: the k-th claim on XCD x gets offset k % B of that XCD's
+// (k / B)-th block; the claimer with offset 0 opens the XCD's NEXT block (one
+// global atomic on the block counter) and publishes it in the XCD's block
+// table, so a claim costs one ticket atomic and one load of an entry that was
+// published about B claims earlier.
+// Deadlock-free without any placement assumption: blocks are opened in global
+// order and each XCD claims its blocks in order, so the lowest unpublished
+// tile is either held by a running workgroup or is the next tile of an opened
+// block of some XCD, whose workgroups hold only lower (published) tiles and
+// come back for it; an opened block always belongs to an XCD with running
+// workgroups, which claim through it before they can see the DONE entry.
+#ifndef THRS_XCD_BLOCK
+#define THRS_XCD_BLOCK 8
+#endif
+constexpr uint32_t kXcdBlock = THRS_XCD_BLOCK;
+constexpr uint32_t kXbDone = 0xFFFFFFFFu;
+
+// claimState: [0..7] per-XCD tickets, [8] global block counter, [16..]
+// per-XCD block tables of `stride` entries (0 = not yet published,
+// kXbDone = no more blocks, else block + 1)
+__device__ __forceinline__ void xb_open(uint32_t* gblock, uint32_t* entry, uint32_t nBlocks) {
+  const uint32_t nb = atomicAdd(gblock, 1u);
+  store_agent(entry, nb < nBlocks ? nb + 1 : kXbDone);
+}
+
+__device__ __forceinline__ uint32_t xb_claim(uint32_t* claimState, uint32_t stride, uint32_t nTiles,
+                                             uint32_t* errFlag) {
+  const uint32_t x = xcc_id() & 7u;
+  const uint32_t nBlocks = (nTiles + kXcdBlock - 1) / kXcdBlock;
+  uint32_t* gblock = claimState + 8;
+  uint32_t* tab = claimState + 16 + x * stride;
+  const uint32_t k = atomicAdd(&claimState[x], 1u);
+  const uint32_t j = k / kXcdBlock, o = k % kXcdBlock;
+  if (j + 1 >= stride) return kXbDone;  // cannot happen with stride = nBlocks + slack; never write past the table
+  if (k == 0) xb_open(gblock, &tab[0], nBlocks);  // first claim on this XCD: its first block
+  if (o == 0) xb_open(gblock, &tab[j + 1], nBlocks);  // open the next block ahead
+  uint32_t e = load_agent(&tab[j]);
+  for (uint32_t spin = 0; e == 0; ++spin) {
+    if (spin > (1u << 22)) {  // bounded: never hang the GPU
+      atomicOr(errFlag, 2u);
+      return kXbDone;
+    }
+    __builtin_amdgcn_s_sleep(1);
+    e = load_agent(&tab[j]);
+  }
+  if (e == kXbDone) return kXbDone;
+  const uint32_t tile = (e - 1) * kXcdBlock + o;
+  return tile < nTiles ? tile : kXbDone;
+}
+
+// Persistent form with XCD-block claims (THRS_XB): one tile per iteration,
+// exactly the work of thrs_pass.
+template <int KT, int VB, typename ST, bool ATOMIC_RANK>
+__global__ __launch_bounds__((PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::THREADS))
+__attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::WPE))) void thrs_pass_xb(
+    const typename KeyTraits<KT>::U* __restrict__ keysIn, typename KeyTraits<KT>::U* __restrict__ keysOut,
+    const typename ValueWord<VB>::T* __restrict__ valsIn, typename ValueWord<VB>::T* __restrict__ valsOut,
+    uint32_t n, typename KeyTraits<KT>::U orderMask, int shift, const uint32_t* __restrict__ digitBase,
+    ST* __restrict__ status, ST* __restrict__ statusNext, uint32_t* __restrict__ claimState,
+    uint32_t* __restrict__ errFlag, GroupTables<ST> grp, uint64_t* __restrict__ stamps) {
+  using U = typename KeyTraits<KT>::U;
+  using VW = typename ValueWord<VB>::T;
+  using G = PassGeom<sizeof(U), VB>;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint32_t* s_cnt = reinterpret_cast<uint32_t*>(smem + G::STAGE * (sizeof(U) + VB));
+  uint32_t* s_misc = s_cnt + (G::WAVES + 1) * kBins;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t nTiles = (uint32_t)(((uint64_t)n + G::TILE - 1) / G::TILE);
+  const uint32_t myBase = digitBase[tid & 255u];
+  U k[G::KPT];
+  VW v[VB ? G::KPT : 1];
+  for (;;) {
+    if (tid == 0) {
+      s_misc[0] = xb_claim(claimState, (nTiles + kXcdBlock - 1) / kXcdBlock + 16, nTiles, errFlag);
+#ifdef THRS_STAMPS
+      if (stamps && s_misc[0] != kXbDone) {
+        uint64_t* s_stamp = reinterpret_cast<uint64_t*>(s_misc + 16);
+        for (int i = 0; i < kStampSlots; ++i) s_stamp[i] = 0;
+        s_stamp[0] = __builtin_amdgcn_s_memrealtime();
+        s_stamp[7] = xcc_id();
+        s_misc[1] = s_misc[2] = s_misc[3] = 0;
+      }
+#endif
+    }
+    for (uint32_t i = tid; i < (uint32_t)(G::WAVES * kBins); i += G::THREADS) s_cnt[i] = 0;
+    lds_barrier();
+    const uint32_t tile = s_misc[0];
+    if (tile == kXbDone) break;
+    load_tile<KT, VB>(keysIn, valsIn, n, tile, k, v);
+    pass_tile<KT, VB, ST, ATOMIC_RANK>(keysIn, keysOut, valsIn, valsOut, n, orderMask, shift, myBase, status,
+                                       statusNext, errFlag, tile, 0, grp, smem, stamps, k, v, NoMid{});
+    lds_barrier();  // stage, s_gofs and s_misc[0] are reused by the next tile
+  }
+}
 
 // ================================================================ self-probe
 // Does ds_add_rtn_u32 hand out values in lane order when several lanes of one
