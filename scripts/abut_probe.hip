@@ -38,7 +38,12 @@ __global__ __launch_bounds__(THREADS) void abut(const uint32_t* __restrict__ in,
   __shared__ uint32_t s_off[256];
   __shared__ uint32_t s_ls[257];
   const uint32_t b = blockIdx.x;
-  const uint32_t tile = MAP == 0 ? b : (b % 8) * (nT / 8) + b / 8;
+  // MAP 0: round-robin; 1: one contiguous range per XCD; B>1: blocks of B
+  // consecutive tiles per XCD, blocks round-robin over XCDs (thrs_pass_xb)
+  uint32_t tile;
+  if constexpr (MAP == 0) tile = b;
+  else if constexpr (MAP == 1) tile = (b % 8) * (nT / 8) + b / 8;
+  else tile = ((b / 8) / MAP * 8 + (b % 8)) * MAP + (b / 8) % MAP;
   const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   if (tid < 256) {
     s_off[tid] = off[(uint64_t)tile * 256 + tid];
@@ -120,9 +125,11 @@ int main() {
   CK(hipMemcpy(dls, ls.data(), ls.size() * 2, hipMemcpyHostToDevice));
   const double bytes = 2.0 * n * 4;
   for (int rep = 0; rep < 2; ++rep) {
-    double a = run<0>(in, out, doff, dls, nT, 10), b = run<1>(in, out, doff, dls, nT, 10);
-    printf("{\"map\": \"rr\", \"ms\": %.4f, \"GBps\": %.1f}\n", a, bytes / a / 1e6);
-    printf("{\"map\": \"xcd\", \"ms\": %.4f, \"GBps\": %.1f}\n", b, bytes / b / 1e6);
+    const double r[5] = {run<0>(in, out, doff, dls, nT, 10), run<1>(in, out, doff, dls, nT, 10),
+                         run<4>(in, out, doff, dls, nT, 10), run<8>(in, out, doff, dls, nT, 10),
+                         run<32>(in, out, doff, dls, nT, 10)};
+    const char* nm[5] = {"rr", "xcd_contiguous", "xcd_blocks4", "xcd_blocks8", "xcd_blocks32"};
+    for (int i = 0; i < 5; ++i) printf("{\"map\": \"%s\", \"ms\": %.4f, \"GBps\": %.1f}\n", nm[i], r[i], bytes / r[i] / 1e6);
     fflush(stdout);
   }
   return 0;

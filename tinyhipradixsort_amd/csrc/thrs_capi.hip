@@ -249,8 +249,8 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     ProfScope prof(stream, 0);
     const int vec = (reinterpret_cast<uintptr_t>(keys) % 16) == 0;
     const uint64_t want = ((uint64_t)n + kHistThreads * 64 - 1) / (kHistThreads * 64);
-    const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cu_count()));
-    const size_t lds = (size_t)nPass * kBins * (sizeof(U) == 4 ? 32 : 16) * 4;
+    const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cu_count() * THRS_HIST_GRID_MULT));
+    const size_t lds = (size_t)nPass * kBins * hist_copies<(int)sizeof(U)>() * 4;
     if (allow_lds(thrs_hist<KT>, lds) != hipSuccess) return THRS_ERROR_HIP;
     hipLaunchKernelGGL(thrs_hist<KT>, dim3(grid), dim3(kHistThreads), lds, stream, static_cast<const U*>(keys), n,
                        orderMask, startBits, nPass, vec, hist);
@@ -267,7 +267,12 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   // grid is large: 4-byte keys without values, n >= 2^29 (docs/EXPERIMENTS.md
   // row 19: +4-6% there, neutral at 2^28, -2..-6% for pairs / f32 at 2^28).
   const int xbEnv = xb_override();  // THRS_XB=1 / 0 in the environment forces it on / off (tests)
+#ifdef THRS_XB_ALL
+  const bool useXb = true;  // experiment: every configuration
+  (void)xbEnv;
+#else
   const bool useXb = xbEnv >= 0 ? xbEnv == 1 : (THRS_XB && sizeof(U) == 4 && VB == 0 && n >= (1u << 29));
+#endif
   if (useXb) {
     kernel = atomicRank ? thrs_pass_xb<KT, VB, ST, true> : thrs_pass_xb<KT, VB, ST, false>;
     if (allow_lds(kernel, lds) != hipSuccess) return THRS_ERROR_HIP;

@@ -150,6 +150,16 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* s_w
 // 64-bit keys (8 digits) use 16 copies.  Copies are summed once per workgroup
 // and merged with one device-scope atomic per (p, bin).
 constexpr int kHistThreads = 1024;
+#ifndef THRS_HIST_COPIES
+#define THRS_HIST_COPIES 32  // LDS copies per bin for 4-byte keys (8-byte keys: half)
+#endif
+#ifndef THRS_HIST_UNROLL
+#define THRS_HIST_UNROLL 4   // 16-B loads in flight per lane
+#endif
+#ifndef THRS_HIST_GRID_MULT
+#define THRS_HIST_GRID_MULT 1  // workgroups per CU
+#endif
+template <int KB> constexpr int hist_copies() { return KB == 4 ? THRS_HIST_COPIES : THRS_HIST_COPIES / 2; }
 template <int KT>
 __global__ __launch_bounds__(kHistThreads) void thrs_hist(const typename KeyTraits<KT>::U* __restrict__ keys,
                                                           uint32_t n, typename KeyTraits<KT>::U orderMask,
@@ -157,7 +167,7 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist(const typename KeyTrai
                                                           uint32_t* __restrict__ hist) {
   using U = typename KeyTraits<KT>::U;
   constexpr int NP_MAX = sizeof(U);
-  constexpr int COPIES = NP_MAX == 4 ? 32 : 16;
+  constexpr int COPIES = hist_copies<(int)sizeof(U)>();
   extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];  // [nPass][256][COPIES]
   const uint32_t tid = threadIdx.x;
   const uint32_t words = (uint32_t)nPass * kBins * COPIES;
@@ -184,12 +194,13 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist(const typename KeyTrai
     const uint64_t nv = n / PER;
     const uint4* kv = reinterpret_cast<const uint4*>(keys);
     uint64_t i = gtid;
-    for (; i + 3 * gstride < nv; i += 4 * gstride) {
-      uint4 q[4];
+    constexpr int UN = THRS_HIST_UNROLL;
+    for (; i + (UN - 1) * gstride < nv; i += UN * gstride) {
+      uint4 q[UN];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) q[u] = kv[i + u * gstride];
+      for (int u = 0; u < UN; ++u) q[u] = kv[i + u * gstride];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < UN; ++u) {
         if constexpr (sizeof(U) == 4) {
           count(q[u].x); count(q[u].y); count(q[u].z); count(q[u].w);
         } else {
@@ -1014,6 +1025,11 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
 #endif
 constexpr uint32_t kXcdBlock = THRS_XCD_BLOCK;
 constexpr uint32_t kXbDone = 0xFFFFFFFFu;
+#ifndef THRS_XB_OPEN_AT
+#define THRS_XB_OPEN_AT (THRS_XCD_BLOCK / 2)
+#endif
+constexpr uint32_t kXbOpenAt = THRS_XB_OPEN_AT;
+static_assert(kXbOpenAt < kXcdBlock, "open the next block from inside the current one");
 
 // claimState: [0..7] per-XCD tickets, [8] global block counter, [16..]
 // per-XCD block tables of `stride` entries (0 = not yet published,
@@ -1033,7 +1049,10 @@ __device__ __forceinline__ uint32_t xb_claim(uint32_t* claimState, uint32_t stri
   const uint32_t j = k / kXcdBlock, o = k % kXcdBlock;
   if (j + 1 >= stride) return kXbDone;  // cannot happen with stride = nBlocks + slack; never write past the table
   if (k == 0) xb_open(gblock, &tab[0], nBlocks);  // first claim on this XCD: its first block
-  if (o == 0) xb_open(gblock, &tab[j + 1], nBlocks);  // open the next block ahead
+  // open the XCD's next block once this one is partly claimed: early enough
+  // that its claimers find it published, late enough that other XCDs' tiles
+  // do not wait long on a block this XCD has not started
+  if (o == kXbOpenAt) xb_open(gblock, &tab[j + 1], nBlocks);
   uint32_t e = load_agent(&tab[j]);
   for (uint32_t spin = 0; e == 0; ++spin) {
     if (spin > (1u << 22)) {  // bounded: never hang the GPU
