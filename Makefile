@@ -4,7 +4,7 @@ HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -fvisibility=hidden -Iinclude -Wall -Wno-unused-result
 PKG := tinyhipradixsort_amd
-KSRC := $(PKG)/csrc/thrs_capi.hip $(PKG)/csrc/thrs_kernels.hpp include/thrs/thrs_capi.h
+KSRC := $(PKG)/csrc/thrs_capi.hip $(PKG)/csrc/thrs_kernels.hpp $(PKG)/csrc/thrs_hybrid.hpp include/thrs/thrs_capi.h
 
 all: $(PKG)/libthrs.so $(PKG)/libthrs_testutil.so $(PKG)/libthrs_vendor.so tests/cpp/unittest_thrs examples/helloworld oracle
 

@@ -116,6 +116,10 @@ int thrs_check_device_error(void* temporaryBuffer, hipStream_t stream);
  * for use under stream capture. */
 int thrs_profile_enable(int enable);
 int thrs_profile_read(double* histMs, int* histLaunches, double* passMs, int* passLaunches);
+/* Same, for one launch kind: 0 = histogram + scan/plan, 1 = device-wide digit
+ * pass, 2 = local (in-LDS) bucket sort of the 3-pass path, 3 = the 3-pass
+ * path's fallback-only passes (they exit at once unless a bucket overflowed). */
+int thrs_profile_read_kind(int kind, double* ms, int* launches);
 
 /* Rank path of the current device: 1 = one LDS atomic per key (gfx950
  * services conflicting lanes of a fully active wave in lane order; checked by
@@ -123,6 +127,10 @@ int thrs_profile_read(double* histMs, int* histLaunches, double* passMs, int* pa
  * THRS_RANK=ballot|atomic in the environment overrides.  No reference
  * counterpart. */
 int thrs_rank_mode(void);
+
+/* Diagnostic: resident workgroups per CU of the 3-pass path's local bucket
+ * sort kernel (4-byte keys), from the runtime's occupancy calculator. */
+int thrs_debug_local_occupancy(void);
 
 /* == thrs::Buffer (tinyhipradixsort.hpp:501-528): hipMalloc(max(bytes,1)). */
 int thrs_malloc(void** ptr, int64_t bytes);

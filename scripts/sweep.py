@@ -39,6 +39,8 @@ def load(path):
     L.thrs_profile_read.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32),
                                     ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32)]
     L.thrs_check_device_error.argtypes = [vp, vp]
+    if hasattr(L, "thrs_profile_read_kind"):
+        L.thrs_profile_read_kind.argtypes = [i32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32)]
     return L
 
 
@@ -70,7 +72,7 @@ def main():
     keys = torch.empty(n * kb, dtype=torch.uint8, device="cuda")
     vals = torch.empty(max(1, n * vb), dtype=torch.uint8, device="cuda")
     s = torch.cuda.current_stream()
-    res = {name: {"ms": [], "pass_ms": [], "hist_ms": []} for name, _ in libs}
+    res = {name: {"ms": [], "pass_ms": [], "hist_ms": [], "local_ms": []} for name, _ in libs}
     vend = None
     vpath = os.path.join(ROOT, "tinyhipradixsort_amd", "libthrs_vendor.so")
     if a.vendor and os.path.exists(vpath) and kt in (0, 1) and vb in (0, kb):
@@ -84,7 +86,7 @@ def main():
         kb2 = torch.empty(n * kb, dtype=torch.uint8, device="cuda")
         vb2 = torch.empty(max(1, n * vb), dtype=torch.uint8, device="cuda")
         vend = (V, vtmp, kb2, vb2)
-        res["hipcub"] = {"ms": [], "pass_ms": [], "hist_ms": []}
+        res["hipcub"] = {"ms": [], "pass_ms": [], "hist_ms": [], "local_ms": []}
     for r in range(a.rounds + 1):
         for name, L in libs:
             if a.iota:
@@ -109,6 +111,9 @@ def main():
             h, p = ctypes.c_double(), ctypes.c_double()
             nh, np_ = ctypes.c_int(), ctypes.c_int()
             L.thrs_profile_read(ctypes.byref(h), ctypes.byref(nh), ctypes.byref(p), ctypes.byref(np_))
+            lm, nl = ctypes.c_double(), ctypes.c_int()
+            if hasattr(L, "thrs_profile_read_kind"):
+                L.thrs_profile_read_kind(2, ctypes.byref(lm), ctypes.byref(nl))
             L.thrs_profile_enable(0)
             if name not in a.nocheck.split(","):
                 assert L.thrs_check_device_error(tmp.data_ptr(), s.cuda_stream) == 0, name
@@ -119,6 +124,7 @@ def main():
                 res[name]["ms"].append(e0.elapsed_time(e1))
                 res[name]["pass_ms"].append(p.value / max(1, np_.value))
                 res[name]["hist_ms"].append(h.value / max(1, nh.value))
+                res[name]["local_ms"].append(lm.value / max(1, nl.value))
         if vend is not None:
             V, vtmp, kb2, vb2 = vend
             TU.fill_keys(kt, keys, n, start=r * n)
@@ -140,6 +146,7 @@ def main():
                 res["hipcub"]["ms"].append(e0.elapsed_time(e1))
                 res["hipcub"]["pass_ms"].append(float("nan"))
                 res["hipcub"]["hist_ms"].append(float("nan"))
+                res["hipcub"]["local_ms"].append(float("nan"))
     out = []
     for name, d in res.items():
         med = statistics.median(d["ms"])
@@ -147,7 +154,8 @@ def main():
         alg = 2 * n * (kb + vb)
         out.append({"variant": name, "ms_med": round(med, 3), "ms_min": round(min(d["ms"]), 3),
                     "Gkeys_s": round(n / med / 1e6, 2), "pass_ms": round(pm, 4),
-                    "pass_GBps": round(alg / pm / 1e6, 1), "hist_ms": round(statistics.median(d["hist_ms"]), 4)})
+                    "pass_GBps": round(alg / pm / 1e6, 1), "hist_ms": round(statistics.median(d["hist_ms"]), 4),
+                    "local_ms": round(statistics.median(d["local_ms"]), 4)})
         print(json.dumps(out[-1]), flush=True)
 
 

@@ -155,6 +155,48 @@ def test_cpp_port_with_claim_mode_forced(gpu, xb):
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
 
 
+@pytest.mark.parametrize("hy", ["1", "0"])
+def test_cpp_port_with_hybrid_forced(gpu, hy):
+    """The UTEST matrix with the 3-HBM-pass path (bucket passes + local LDS
+    sort, thrs_hybrid.hpp) on (THRS_HYBRID=1, also the default) and off (plain
+    LSD passes for every window)."""
+    exe = os.path.join(ROOT, "tests", "cpp", "unittest_thrs")
+    env = dict(os.environ, THRS_HYBRID=hy)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=900, env=env)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
+
+
+@pytest.mark.parametrize("kt", [O.U32, O.F32])
+@pytest.mark.parametrize("desc", [False, True])
+def test_hybrid_paths_vs_oracle(gpu, kt, desc):
+    """4-byte keys-only sorts with >= 3 digits take the hybrid path: chunked
+    local sort (single- and multi-bucket chunks), and the gated fallback to
+    plain LSD when one bucket exceeds the local capacity (18432 keys) --
+    including an odd number of low passes (window of 3 digits: gated copy)."""
+    torch = gpu
+    rs = make_sorter(kt, 0, desc)
+    dists = {
+        "uniform": lambda k: k,
+        "low20": lambda k: k & np.array(0xFFFFF, k.dtype),        # 16 buckets -> fallback above 295k keys
+        "top_skew": lambda k: k | np.array(0x7F000000, k.dtype),  # top digit fixed
+        "ties": lambda k: k & np.array(0xFF00FF00, k.dtype),
+        "const": lambda k: np.full_like(k, k[0]),
+    }
+    sizes = [1, 100, 18432, 18433, 70001, 300007, 1 << 20]
+    windows = [(0, 32), (8, 32), (0, 24), (4, 28)]
+    j = 0
+    for name, f in dists.items():
+        for n in sizes:
+            for (s, e) in windows:
+                j += 1
+                if j % 2 and n >= 300007 and (s, e) != (0, 32):
+                    continue  # keep the case count bounded
+                keys = f(O.randomize_np(kt, O.splitmix64_stream(7777 * j, n)))
+                k, _ = gpu_sort(torch, rs, {"keys": keys, "values": None}, kt, 0, s, e)
+                ek, _ = O.lsd_sort(kt, keys, None, s, e, desc)
+                assert np.array_equal(k, ek), (name, n, s, e)
+
+
 def test_concurrent_sorts_on_distinct_temps(gpu):
     """Per-call state lives in the caller's temp buffer: two sorts on two
     streams at once (the reference's module-global g_iterator would race)."""

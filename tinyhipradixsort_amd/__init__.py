@@ -78,8 +78,9 @@ def lib() -> ctypes.CDLL:
         L.thrs_profile_enable.argtypes = [i32]
         L.thrs_profile_read.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32),
                                         ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32)]
+        L.thrs_profile_read_kind.argtypes = [i32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32)]
         L.thrs_rank_mode.restype = i32
-        for f in ("thrs_profile_enable", "thrs_profile_read", "thrs_get_temporary_buffer_bytes", "thrs_sort_keys", "thrs_sort_pairs", "thrs_check_device_error", "thrs_partition_pass",
+        for f in ("thrs_profile_enable", "thrs_profile_read", "thrs_profile_read_kind", "thrs_get_temporary_buffer_bytes", "thrs_sort_keys", "thrs_sort_pairs", "thrs_check_device_error", "thrs_partition_pass",
                   "thrs_malloc", "thrs_free", "thrs_memcpy_htod_async", "thrs_memcpy_dtoh", "thrs_memcpy_dtod_async",
                   "thrs_stream_create", "thrs_stream_destroy", "thrs_stream_synchronize"):
             getattr(L, f).restype = i32
@@ -302,8 +303,13 @@ def profile_enable(on: bool = True):
 
 
 def profile_read() -> dict:
-    """Synchronise recorded events; summed ms and launch counts since enable."""
-    h, p = ctypes.c_double(), ctypes.c_double()
-    nh, np_ = ctypes.c_int(), ctypes.c_int()
-    _check(lib().thrs_profile_read(ctypes.byref(h), ctypes.byref(nh), ctypes.byref(p), ctypes.byref(np_)))
-    return {"hist_ms": h.value, "hist_launches": nh.value, "pass_ms": p.value, "pass_launches": np_.value}
+    """Synchronise recorded events; summed ms and launch counts since enable
+    (hist = histogram + scan/plan, pass = device-wide digit passes, local =
+    the 3-pass path's in-LDS bucket sort)."""
+    out = {}
+    for kind, name in ((0, "hist"), (1, "pass"), (2, "local")):
+        ms, n = ctypes.c_double(), ctypes.c_int()
+        _check(lib().thrs_profile_read_kind(kind, ctypes.byref(ms), ctypes.byref(n)))
+        out[name + "_ms"] = ms.value
+        out[name + "_launches"] = n.value
+    return out

@@ -25,6 +25,7 @@
 
 #include "thrs/thrs_capi.h"
 #include "thrs_kernels.hpp"
+#include "thrs_hybrid.hpp"
 
 #ifndef THRS_PIPE
 #define THRS_PIPE 0
@@ -45,6 +46,7 @@ constexpr uint64_t kErrOff = kCounterOff + 8 * 4;      // u32
 constexpr uint64_t kHeaderBytes = 16640;               // 65 * 256
 
 inline uint64_t round_up(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
+constexpr uint64_t round_up_c(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
 
 inline bool valid_key(int k) { return k >= THRS_KEY_U32 && k <= THRS_KEY_F64; }
 inline bool valid_value(int v) { return v >= THRS_VALUE_U32 && v <= THRS_VALUE_U128; }
@@ -76,8 +78,16 @@ struct Plan {
   uint64_t gpBytes;       // group prefixes   [nGroups][256] status words
   uint64_t setBytes;      // one look-back table set = status + ga + gp
   uint64_t claimBytes;    // per pass: XCD-block claim state (tickets, block counter, 8 block tables)
-  uint64_t scratchBytes;  // header + 2 sets (ping-pong between passes) + 8 claim areas
+  uint64_t hybridOff;     // 3-pass path (thrs_hybrid.hpp): bucket histogram, chunk table, meta
+  uint64_t scratchBytes;  // header + 2 sets (ping-pong between passes) + 8 claim areas + hybrid area
 };
+
+// hybrid area: u32 joint[65536] | chunkOff[65537] | chunkB0[65537] | meta[4]
+constexpr uint64_t kJointBytes = kBuckets * 4;
+constexpr uint64_t kChunkOffOff = kJointBytes;
+constexpr uint64_t kChunkB0Off = kChunkOffOff + round_up_c((kBuckets + 1) * 4, 256);
+constexpr uint64_t kMetaOff = kChunkB0Off + round_up_c((kBuckets + 1) * 4, 256);
+constexpr uint64_t kHybridBytes = kMetaOff + 256;
 
 Plan make_plan(int keyType, int valueBytesOrZero, uint32_t n) {
   Plan p{};
@@ -93,7 +103,8 @@ Plan make_plan(int keyType, int valueBytesOrZero, uint32_t n) {
   p.setBytes = p.statusBytes + p.gaBytes + p.gpBytes;
   const uint64_t nXb = (p.nTiles + kXcdBlock - 1) / kXcdBlock + 16;  // table stride (see xb_claim)
   p.claimBytes = round_up((16 + 8 * nXb) * 4, kAlign);
-  p.scratchBytes = kHeaderBytes + 2 * p.setBytes + 8 * p.claimBytes;
+  p.hybridOff = kHeaderBytes + 2 * p.setBytes + 8 * p.claimBytes;
+  p.scratchBytes = p.hybridOff + kHybridBytes;
   return p;
 }
 
@@ -208,11 +219,27 @@ hipError_t allow_lds(F kernel, size_t bytes) {
                              (int)bytes);
 }
 
-// One launch sequence: histogram (+ scan) of all nPass digits, then nPass
-// ping-pong passes.  Sort mode (counts == nullptr): the result is copied back
-// into keys/vals after an odd pass count.  Partition mode (counts != nullptr,
-// nPass == 1, thrs_partition_pass): the pass writes keyOutBuf/valOutBuf, which
-// are the caller's, and the digit's 256 bucket counts go to `counts`.
+// THRS_HYBRID=1 / THRS_HYBRID=0 in the environment: force the 3-HBM-pass path
+// (thrs_hybrid.hpp) on / off wherever it applies (-1 = default: on).
+int hybrid_override() {
+  static const int v = [] {
+    const char* e = getenv("THRS_HYBRID");
+    if (e && !strcmp(e, "1")) return 1;
+    if (e && !strcmp(e, "0")) return 0;
+    return -1;
+  }();
+  return v;
+}
+
+// One launch sequence.  Sort mode (counts == nullptr): the result lands in
+// keys/vals.  Partition mode (counts != nullptr, nPass == 1,
+// thrs_partition_pass): the pass writes keyOutBuf/valOutBuf, which are the
+// caller's, and the digit's 256 bucket counts go to `counts`.
+//   LSD path:    histogram of every digit + scan, nPass ping-pong passes,
+//                copy-back after an odd pass count.
+//   hybrid path: 4-byte keys without values, nPass >= 3 (thrs_hybrid.hpp):
+//                bucket histogram + plan, [low-digit passes + copy, gated on
+//                the fallback flag], the two top-digit passes, local sort.
 template <int KT, int VB, typename ST>
 int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, void* valOutBuf, int startBits, int nPass,
              bool desc, const Plan& plan, hipStream_t stream, uint32_t* counts = nullptr) {
@@ -236,13 +263,26 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     grp[i].gp = reinterpret_cast<ST*>(set + plan.statusBytes + plan.gaBytes);
     grp[i].nTiles = (uint32_t)plan.nTiles;
   }
+  char* hyb = scratch + plan.hybridOff;
+  uint32_t* joint = reinterpret_cast<uint32_t*>(hyb);
+  uint32_t* chunkOff = reinterpret_cast<uint32_t*>(hyb + kChunkOffOff);
+  uint32_t* chunkB0 = reinterpret_cast<uint32_t*>(hyb + kChunkB0Off);
+  uint32_t* meta = reinterpret_cast<uint32_t*>(hyb + kMetaOff);
   U* keyOut = static_cast<U*>(keyOutBuf);
   VW* valOut = static_cast<VW*>(valOutBuf);
 
   const U orderMask = desc ? (U)~(U)0 : (U)0;
+  const int hyEnv = hybrid_override();
+  constexpr bool kHybridType = sizeof(U) == 4 && VB == 0;  // 4-byte keys without values
+  const bool hybrid = kHybridType && !counts && nPass >= 3 && hyEnv != 0;
+  const int nLow = nPass - 2;
 
-  // header (histograms, tile counters, error word) + first status table
-  if (hipMemsetAsync(scratch, 0, kHeaderBytes + plan.setBytes, stream) != hipSuccess) return THRS_ERROR_HIP;
+  // header (histograms, tile counters, error word) + first status table; the
+  // hybrid path with an odd number of (skippable) low passes starts on set 1
+  // too, and zeroes its bucket histogram
+  const uint64_t sets = (hybrid && (nLow & 1)) ? 2 : 1;
+  if (hipMemsetAsync(scratch, 0, kHeaderBytes + sets * plan.setBytes, stream) != hipSuccess) return THRS_ERROR_HIP;
+  if (hybrid && hipMemsetAsync(joint, 0, kJointBytes, stream) != hipSuccess) return THRS_ERROR_HIP;
   char* claim = scratch + kHeaderBytes + 2 * plan.setBytes;  // 8 per-pass claim areas
 
   {  // histograms of every pass in one read of the keys
@@ -250,11 +290,25 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     const int vec = (reinterpret_cast<uintptr_t>(keys) % 16) == 0;
     const uint64_t want = ((uint64_t)n + kHistThreads * 64 - 1) / (kHistThreads * 64);
     const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cu_count() * THRS_HIST_GRID_MULT));
-    const size_t lds = (size_t)nPass * kBins * hist_copies<(int)sizeof(U)>() * 4;
-    if (allow_lds(thrs_hist<KT>, lds) != hipSuccess) return THRS_ERROR_HIP;
-    hipLaunchKernelGGL(thrs_hist<KT>, dim3(grid), dim3(kHistThreads), lds, stream, static_cast<const U*>(keys), n,
-                       orderMask, startBits, nPass, vec, hist);
-    hipLaunchKernelGGL(thrs_scan, dim3(1), dim3(kThreads), 0, stream, hist, base, nPass);
+    if (hybrid) {
+      if (allow_lds(thrs_hist_joint<KT>, kJointLds) != hipSuccess) return THRS_ERROR_HIP;
+      hipLaunchKernelGGL(thrs_hist_joint<KT>, dim3(grid), dim3(kHistThreads), kJointLds, stream,
+                         static_cast<const U*>(keys), n, orderMask, startBits + 8 * nLow, vec, joint);
+      hipLaunchKernelGGL(thrs_plan, dim3(1), dim3(kPlanThreads), 0, stream, joint, n, base + nLow * kBins, chunkOff,
+                         chunkB0, meta, kLocCap, kLocCap / 2);
+      // the low digits' histograms + bases: needed only on the fallback path
+      const size_t lds = (size_t)nLow * kBins * hist_copies<(int)sizeof(U)>() * 4;
+      if (allow_lds(thrs_hist<KT>, lds) != hipSuccess) return THRS_ERROR_HIP;
+      hipLaunchKernelGGL(thrs_hist<KT>, dim3(grid), dim3(kHistThreads), lds, stream, static_cast<const U*>(keys), n,
+                         orderMask, startBits, nLow, vec, hist, meta + kMetaFallback);
+      hipLaunchKernelGGL(thrs_scan, dim3(1), dim3(kThreads), 0, stream, hist, base, nLow, meta + kMetaFallback);
+    } else {
+      const size_t lds = (size_t)nPass * kBins * hist_copies<(int)sizeof(U)>() * 4;
+      if (allow_lds(thrs_hist<KT>, lds) != hipSuccess) return THRS_ERROR_HIP;
+      hipLaunchKernelGGL(thrs_hist<KT>, dim3(grid), dim3(kHistThreads), lds, stream, static_cast<const U*>(keys), n,
+                         orderMask, startBits, nPass, vec, hist, nullptr);
+      hipLaunchKernelGGL(thrs_scan, dim3(1), dim3(kThreads), 0, stream, hist, base, nPass, nullptr);
+    }
     if (counts && hipMemcpyAsync(counts, hist, kBins * sizeof(uint32_t), hipMemcpyDeviceToDevice, stream) != hipSuccess)
       return THRS_ERROR_HIP;
   }
@@ -295,31 +349,74 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   if (useXb && hipMemsetAsync(claim, 0, (size_t)nPass * plan.claimBytes, stream) != hipSuccess)
     return THRS_ERROR_HIP;
 
-  U* kin = static_cast<U*>(keys);
-  U* kout = keyOut;
-  VW* vin = static_cast<VW*>(vals);
-  VW* vout = valOut;
-  for (int p = 0; p < nPass; ++p) {
+  // pass p: digit at startBits + 8p, tables of set p&1; gate != nullptr runs
+  // it only if *gate == 1 (the hybrid path's fallback flag)
+  auto launch_pass = [&](int p, U* kin, U* kout, VW* vin, VW* vout, const uint32_t* gate) {
     const bool more = p + 1 < nPass;
     ST* next = more ? status[(p + 1) & 1] : nullptr;
     GroupTables<ST> g = grp[p & 1];
     g.gaNext = more ? grp[(p + 1) & 1].ga : nullptr;
     g.gpNext = more ? grp[(p + 1) & 1].gp : nullptr;
-    ProfScope prof(stream, 1);
-    hipLaunchKernelGGL(kernel, dim3(grid), dim3(G::THREADS), lds, stream, kin, kout, vin, vout, n,
-                       orderMask, startBits + 8 * p, base + p * kBins, status[p & 1], next,
-                       useXb ? reinterpret_cast<uint32_t*>(claim + p * plan.claimBytes) : counters + p,
-                       err, g,
-                       g_stamps ? g_stamps + (uint64_t)p * plan.nTiles * kStampSlots : nullptr);
-    std::swap(kin, kout);
-    std::swap(vin, vout);
+    ProfScope prof(stream, gate ? 3 : 1);  // gated passes (hybrid fallback) are timed apart
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(G::THREADS), lds, stream, kin, kout, vin, vout, n, orderMask,
+                       startBits + 8 * p, base + p * kBins, status[p & 1], next,
+                       useXb ? reinterpret_cast<uint32_t*>(claim + p * plan.claimBytes) : counters + p, err, g,
+                       g_stamps ? g_stamps + (uint64_t)p * plan.nTiles * kStampSlots : nullptr, gate, 1u);
+  };
+
+  if (!hybrid) {
+    U* kin = static_cast<U*>(keys);
+    U* kout = keyOut;
+    VW* vin = static_cast<VW*>(vals);
+    VW* vout = valOut;
+    for (int p = 0; p < nPass; ++p) {
+      launch_pass(p, kin, kout, vin, vout, nullptr);
+      std::swap(kin, kout);
+      std::swap(vin, vout);
+    }
+    if (hipGetLastError() != hipSuccess) return THRS_ERROR_HIP;
+    if ((nPass & 1) && !counts) {  // result must end in the caller's buffers (hpp:936-943), stream-ordered here
+      if (hipMemcpyAsync(keys, keyOut, (size_t)n * sizeof(U), hipMemcpyDeviceToDevice, stream) != hipSuccess)
+        return THRS_ERROR_HIP;
+      if (VB && hipMemcpyAsync(vals, valOut, (size_t)n * VB, hipMemcpyDeviceToDevice, stream) != hipSuccess)
+        return THRS_ERROR_HIP;
+    }
+    return THRS_SUCCESS;
+  }
+
+  // ---- hybrid: fallback-only low passes, then the two top digits, then local
+  if constexpr (kHybridType) {
+  U* K = static_cast<U*>(keys);
+  {
+    U* kin = K;
+    U* kout = keyOut;
+    for (int p = 0; p < nLow; ++p) {
+      launch_pass(p, kin, kout, nullptr, nullptr, meta + kMetaFallback);
+      std::swap(kin, kout);
+    }
+    if (nLow & 1)  // fallback result is in keyOut: the top-digit passes read K
+      hipLaunchKernelGGL(thrs_copy_gated, dim3(2048), dim3(256), 0, stream, reinterpret_cast<const uint32_t*>(keyOut),
+                         reinterpret_cast<uint32_t*>(K), (uint64_t)n, meta + kMetaFallback, 1u);
+  }
+  launch_pass(nLow, K, keyOut, nullptr, nullptr, nullptr);
+  launch_pass(nLow + 1, keyOut, K, nullptr, nullptr, nullptr);
+  {
+    ProfScope prof(stream, 2);
+    const size_t llds = local_lds_bytes<U>();
+    auto lk = atomicRank ? thrs_local<KT, true> : thrs_local<KT, false>;
+    if (allow_lds(lk, llds) != hipSuccess) return THRS_ERROR_HIP;
+    int perCU = 0;  // persistent: as many workgroups as fit at once
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, lk, kLocThreads, llds) != hipSuccess || perCU < 1)
+      perCU = 1;
+    // never more workgroups than chunks can exist: <= 256 (one per top digit)
+    // + 2 per non-empty bucket, and <= the number of buckets
+    const uint64_t maxChunks = std::min<uint64_t>(kBuckets, 256 + 2 * (uint64_t)n);
+    const uint32_t lgrid = THRS_LOC_PERSIST ? (uint32_t)std::min<uint64_t>(maxChunks, (uint64_t)perCU * cu_count())
+                                            : (uint32_t)maxChunks;
+    hipLaunchKernelGGL(lk, dim3(lgrid), dim3(kLocThreads), llds, stream, K, orderMask, startBits, nLow, chunkOff,
+                       chunkB0, meta);
   }
   if (hipGetLastError() != hipSuccess) return THRS_ERROR_HIP;
-  if ((nPass & 1) && !counts) {  // result must end in the caller's buffers (hpp:936-943), stream-ordered here
-    if (hipMemcpyAsync(keys, keyOut, (size_t)n * sizeof(U), hipMemcpyDeviceToDevice, stream) != hipSuccess)
-      return THRS_ERROR_HIP;
-    if (VB && hipMemcpyAsync(vals, valOut, (size_t)n * VB, hipMemcpyDeviceToDevice, stream) != hipSuccess)
-      return THRS_ERROR_HIP;
   }
   return THRS_SUCCESS;
 }
@@ -480,21 +577,27 @@ THRS_API int thrs_profile_enable(int enable) {
   return THRS_SUCCESS;
 }
 
-THRS_API int thrs_profile_read(double* histMs, int* histLaunches, double* passMs, int* passLaunches) {
+// kind: 0 = histogram + scan/plan, 1 = device-wide digit pass, 2 = local sort
+THRS_API int thrs_profile_read_kind(int kind, double* ms, int* launches) {
   std::lock_guard<std::mutex> g(g_prof_mu);
-  double h = 0, p = 0;
-  int nh = 0, np = 0;
+  double t = 0;
+  int c = 0;
   for (auto& r : g_prof) {
+    if (r.kind != kind) continue;
     if (hipEventSynchronize(r.b) != hipSuccess) return THRS_ERROR_HIP;
-    float ms = 0;
-    if (hipEventElapsedTime(&ms, r.a, r.b) != hipSuccess) return THRS_ERROR_HIP;
-    if (r.kind == 0) { h += ms; ++nh; } else { p += ms; ++np; }
+    float x = 0;
+    if (hipEventElapsedTime(&x, r.a, r.b) != hipSuccess) return THRS_ERROR_HIP;
+    t += x;
+    ++c;
   }
-  if (histMs) *histMs = h;
-  if (histLaunches) *histLaunches = nh;
-  if (passMs) *passMs = p;
-  if (passLaunches) *passLaunches = np;
+  if (ms) *ms = t;
+  if (launches) *launches = c;
   return THRS_SUCCESS;
+}
+
+THRS_API int thrs_profile_read(double* histMs, int* histLaunches, double* passMs, int* passLaunches) {
+  const int rc = thrs_profile_read_kind(0, histMs, histLaunches);
+  return rc ? rc : thrs_profile_read_kind(1, passMs, passLaunches);
 }
 
 // Diagnostic hook, not part of the drop-in boundary: in -DTHRS_STAMPS builds
@@ -507,6 +610,17 @@ THRS_API int thrs_debug_set_stamps(void* buf) {
 // Diagnostic: keys per tile of the pass kernel for (key type, value bytes).
 THRS_API uint64_t thrs_debug_tile_keys(int keyType, int valueBytes) {
   return valid_key(keyType) ? tile_keys(key_bytes_of(keyType), valueBytes) : 0;
+}
+
+// Diagnostic: resident workgroups per CU of the local (in-LDS) bucket sort
+// kernel for 4-byte keys, as the runtime computes it from its LDS and VGPRs.
+THRS_API int thrs_debug_local_occupancy(void) {
+  const size_t lds = local_lds_bytes<uint32_t>();
+  if (allow_lds(thrs_local<0, true>, lds) != hipSuccess) return -1;
+  int perCU = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, thrs_local<0, true>, kLocThreads, lds) != hipSuccess)
+    return -1;
+  return perCU;
 }
 
 // Which rank path the current device uses (1 = LDS-atomic, 0 = ballot match);

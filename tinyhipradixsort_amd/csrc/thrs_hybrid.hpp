@@ -1,0 +1,512 @@
+// thrs_hybrid.hpp -- the 3-HBM-pass path for 4-byte keys (gfx950).
+//
+// The reference sorts by P full passes over HBM (tinyhipradixsort.hpp:862-930),
+// each reading and writing every key.  Here, when the window has P >= 3
+// digits, only the window's TOP two digits get device-wide passes:
+//
+//   thrs_hist_joint  one read of the keys: histogram of the 16-bit BUCKET
+//                    (the top two digits) + the low digits' histograms
+//   thrs_plan        one workgroup: bucket offsets (exclusive scan), the two
+//                    top digits' bases (column / row sums of the bucket
+//                    histogram), CHUNKS of whole consecutive buckets that fit
+//                    one workgroup's LDS, and the fallback flag
+//   thrs_pass x2     the usual onesweep passes for digits P-2 and P-1 (stable
+//                    LSD): the keys end up grouped by bucket in bucket order
+//   thrs_local       one workgroup per chunk: load the chunk (<= kLocCap
+//                    keys) into registers, sort it by the P-2 low digits in
+//                    LDS (stable LSD rounds, same rank as the pass kernel),
+//                    write it back in place -- coalesced, whole lines.
+//
+// HBM traffic: 1 (histogram read) + 2 x 2 (passes) + 2 (local) = 7 N*K vs
+// 1 + 2P = 9 N*K for P = 4, and the local write-out has none of the partial-
+// line read-modify-writes a digit scatter pays.
+//
+// Stability / exactness: the two passes are stable, so within a bucket keys
+// keep their input order; the local LSD rounds are stable; so the result is
+// THE stable sort by the window bits -- bit-identical to P LSD passes.
+//
+// Fallback: a bucket larger than kLocCap (skewed input) cannot be sorted in
+// one workgroup.  thrs_plan then sets meta[kMetaFallback]; the low-digit
+// passes (launched gated on that flag) run first, thrs_local exits at once,
+// and the sequence is the plain P-pass LSD sort.  No host synchronisation.
+#pragma once
+#include "thrs_kernels.hpp"
+
+namespace thrs_dev {
+
+constexpr uint32_t kBuckets = 65536;  // 16-bit bucket = the window's top two digits
+enum { kMetaChunks = 0, kMetaFallback = 1 };
+
+// ------------------------------------------------------------ joint histogram
+// LDS: bucket counts as 15-bit fields, two per word (bits 0-14 | guard 15 |
+// 16-30 | guard 31): 128 KiB for 65536 buckets.  The add that carries a field
+// into its guard bit (field was 0x7FFF) clears the guard again and moves 32768
+// to the global count, so no carry ever reaches the neighbouring field and
+// any skew is counted exactly.  (The two top digits' histograms are the row
+// and column sums of this one: thrs_plan.)
+constexpr uint32_t kJointWords = kBuckets / 2;
+constexpr size_t kJointLds = (size_t)kJointWords * 4;
+
+template <int KT>
+__global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename KeyTraits<KT>::U* __restrict__ keys,
+                                                                uint32_t n, typename KeyTraits<KT>::U orderMask,
+                                                                int bucketShift, int vec,
+                                                                uint32_t* __restrict__ joint) {
+  using U = typename KeyTraits<KT>::U;
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_joint[];
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t i = tid; i < kJointWords; i += kHistThreads) s_joint[i] = 0;
+  __syncthreads();
+
+  auto bucket_of = [&](U k) -> uint32_t {
+    return (uint32_t)((KeyTraits<KT>::bits(k) ^ orderMask) >> bucketShift) & 0xFFFFu;
+  };
+  auto add = [&](uint32_t b) -> uint32_t {
+    return __hip_atomic_fetch_add(&s_joint[b >> 1], 1u << ((b & 1u) << 4), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+  };
+  auto check = [&](uint32_t b, uint32_t old) {
+    const uint32_t sh = (b & 1u) << 4;
+    if (((old >> sh) & 0x7FFFu) == 0x7FFFu) {  // this add set the guard bit
+      __hip_atomic_fetch_sub(&s_joint[b >> 1], 0x8000u << sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      atomicAdd(&joint[b], 0x8000u);
+    }
+  };
+
+  const uint64_t gstride = (uint64_t)gridDim.x * kHistThreads;
+  const uint64_t gtid = (uint64_t)blockIdx.x * kHistThreads + tid;
+  uint64_t tailStart = 0;
+  if (vec) {  // 16-byte loads, 4 in flight per lane (keys base 16-B aligned, checked on host)
+    constexpr int PER = 16 / sizeof(U);
+    constexpr int UN = 4;
+    const uint64_t nv = n / PER;
+    const uint4* kv = reinterpret_cast<const uint4*>(keys);
+    uint64_t i = gtid;
+    for (; i + (UN - 1) * gstride < nv; i += UN * gstride) {
+      uint4 q[UN];
+#pragma unroll
+      for (int u = 0; u < UN; ++u) q[u] = kv[i + u * gstride];
+      uint32_t b[UN * PER], o[UN * PER];
+#pragma unroll
+      for (int u = 0; u < UN; ++u) {
+        if constexpr (sizeof(U) == 4) {
+          b[u * 4 + 0] = bucket_of(q[u].x);
+          b[u * 4 + 1] = bucket_of(q[u].y);
+          b[u * 4 + 2] = bucket_of(q[u].z);
+          b[u * 4 + 3] = bucket_of(q[u].w);
+        } else {
+          b[u * 2 + 0] = bucket_of(((uint64_t)q[u].y << 32) | q[u].x);
+          b[u * 2 + 1] = bucket_of(((uint64_t)q[u].w << 32) | q[u].z);
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < UN * PER; ++e) o[e] = add(b[e]);
+#pragma unroll
+      for (int e = 0; e < UN * PER; ++e) check(b[e], o[e]);
+    }
+    for (; i < nv; i += gstride) {
+      const uint4 q = kv[i];
+      uint32_t b[PER];
+      if constexpr (sizeof(U) == 4) {
+        b[0] = bucket_of(q.x); b[1] = bucket_of(q.y); b[2] = bucket_of(q.z); b[3] = bucket_of(q.w);
+      } else {
+        b[0] = bucket_of(((uint64_t)q.y << 32) | q.x);
+        b[1] = bucket_of(((uint64_t)q.w << 32) | q.z);
+      }
+#pragma unroll
+      for (int e = 0; e < PER; ++e) check(b[e], add(b[e]));
+    }
+    tailStart = nv * PER;
+  }
+  for (uint64_t i = tailStart + gtid; i < n; i += gstride) {
+    const uint32_t b = bucket_of(keys[i]);
+    check(b, add(b));
+  }
+  __syncthreads();
+  for (uint32_t i = tid; i < kBuckets; i += kHistThreads) {
+    const uint32_t c = (s_joint[i >> 1] >> ((i & 1u) << 4)) & 0xFFFFu;
+    if (c) atomicAdd(&joint[i], c);
+  }
+}
+
+// ------------------------------------------------------------------- plan
+// One workgroup of 1024 threads; thread t owns buckets [64t, 64t+64).
+// Chunks: bucket b opens a new chunk iff b % 256 == 0 (a chunk never leaves
+// one top digit, so the bucket is (top digit, second digit) and the second
+// digit minus the chunk's first is < 256), or the chunk's T-window changes
+// (floor(off/T) differs from the previous bucket's), or b or b-1 holds more
+// than T keys.  All buckets of a multi-bucket chunk start inside one T-window
+// and hold <= T keys, so a chunk holds < 2T <= cap keys unless it is a single
+// bucket; a single bucket above cap sets the fallback flag.
+constexpr int kPlanThreads = 1024;
+__device__ __forceinline__ uint32_t block_excl_scan1024(uint32_t v, uint32_t* s_w, uint32_t* total) {
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint32_t inc = wave_incl_scan(v, lane);
+  if (lane == 63) s_w[w] = inc;
+  __syncthreads();
+  uint32_t pre = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < kPlanThreads / 64; ++i) {
+    const uint32_t x = s_w[i];
+    pre += (i < (int)w) ? x : 0u;
+    tot += x;
+  }
+  *total = tot;
+  __syncthreads();
+  return pre + inc - v;
+}
+
+__global__ __launch_bounds__(kPlanThreads) void thrs_plan(const uint32_t* __restrict__ joint, uint32_t n,
+                                                          uint32_t* __restrict__ baseTop /* [2][256]: second, top */,
+                                                          uint32_t* __restrict__ chunkOff,
+                                                          uint32_t* __restrict__ chunkB0, uint32_t* __restrict__ meta,
+                                                          uint32_t cap, uint32_t T) {
+  constexpr int SLICE_ROWS = 32;  // column sums through an LDS transpose, 32 top-digit rows at a time
+  __shared__ uint32_t s_tr[SLICE_ROWS][kBins + 1];
+  __shared__ uint32_t s_last[kPlanThreads], s_w[kPlanThreads / 64], s_row[kBins], s_flag;
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  if (tid == 0) s_flag = 0;
+  constexpr int PER = kBuckets / kPlanThreads;  // 64: thread t owns row t>>2, columns 64(t&3)..+63
+  const uint32_t b0 = tid * PER;
+  uint32_t v[PER];  // 16 x 16-B loads, all in flight at once
+  {
+    const uint4* q = reinterpret_cast<const uint4*>(joint + b0);
+#pragma unroll
+    for (int i = 0; i < PER / 4; ++i) {
+      const uint4 x = q[i];
+      v[4 * i] = x.x; v[4 * i + 1] = x.y; v[4 * i + 2] = x.z; v[4 * i + 3] = x.w;
+    }
+  }
+  uint32_t sum = 0;
+  bool big = false;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    sum += v[i];
+    big |= v[i] > cap;
+  }
+  {  // row (top digit) sums: four consecutive threads
+    uint32_t r = sum + __shfl_xor(sum, 1, 64);
+    r += __shfl_xor(r, 2, 64);
+    if ((tid & 3u) == 0) s_row[tid >> 2] = r;
+  }
+  uint32_t colSum = 0;  // thread c < 256: column (second digit) c
+  for (int sl = 0; sl < kBins / SLICE_ROWS; ++sl) {
+    if ((tid >> 7) == (uint32_t)sl) {
+      const uint32_t row = (tid >> 2) - sl * SLICE_ROWS, col0 = (tid & 3u) * PER;
+#pragma unroll
+      for (int i = 0; i < PER; ++i) s_tr[row][col0 + i] = v[i];
+    }
+    __syncthreads();
+    if (tid < kBins) {
+#pragma unroll 8
+      for (int r = 0; r < SLICE_ROWS; ++r) colSum += s_tr[r][tid];
+    }
+    __syncthreads();
+  }
+  if (big) s_flag = 1;
+  s_last[tid] = v[PER - 1];
+  uint32_t total;
+  const uint32_t excl = block_excl_scan1024(sum, s_w, &total);  // its barriers publish s_last, s_row, s_flag
+  (void)total;
+  {  // bases of the two top digits: [0] second digit (column sums), [1] top digit (row sums)
+    __shared__ uint32_t s_wt[2][4];
+    const uint32_t w = tid >> 6;
+    const uint32_t x0 = tid < kBins ? colSum : 0u, x1 = tid < kBins ? s_row[tid] : 0u;
+    const uint32_t i0 = wave_incl_scan(x0, lane), i1 = wave_incl_scan(x1, lane);
+    if (tid < kBins && lane == 63) {
+      s_wt[0][w] = i0;
+      s_wt[1][w] = i1;
+    }
+    __syncthreads();
+    if (tid < kBins) {
+      uint32_t p0 = 0, p1 = 0;
+      for (uint32_t ww = 0; ww < w; ++ww) {
+        p0 += s_wt[0][ww];
+        p1 += s_wt[1][ww];
+      }
+      baseTop[tid] = p0 + i0 - x0;
+      baseTop[kBins + tid] = p1 + i1 - x1;
+    }
+  }
+
+  // chunk starts
+  auto opens = [&](uint32_t b, uint32_t off, uint32_t sz, uint32_t prevSz) -> bool {
+    return (b & 255u) == 0 || (off / T) != ((off - prevSz) / T) || sz > T || prevSz > T;
+  };
+  uint32_t nOpen = 0;
+  {
+    uint32_t off = excl, prev = tid ? s_last[tid - 1] : 0u;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      nOpen += opens(b0 + i, off, v[i], prev) ? 1u : 0u;
+      off += v[i];
+      prev = v[i];
+    }
+  }
+  uint32_t nChunks;
+  uint32_t c = block_excl_scan1024(nOpen, s_w, &nChunks);
+  {
+    uint32_t off = excl, prev = tid ? s_last[tid - 1] : 0u;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      if (opens(b0 + i, off, v[i], prev)) {
+        chunkOff[c] = off;
+        chunkB0[c] = b0 + i;
+        ++c;
+      }
+      off += v[i];
+      prev = v[i];
+    }
+  }
+  if (tid == kPlanThreads - 1) {
+    chunkOff[nChunks] = n;
+    chunkB0[nChunks] = kBuckets;
+    meta[kMetaChunks] = nChunks;
+    meta[kMetaFallback] = s_flag;
+    meta[2] = 0;  // kMetaClaim: the local sort's chunk counter
+  }
+}
+
+// ------------------------------------------------------------- local sort
+// Persistent workgroups (one per CU, 16 waves), each looping over chunks
+// claimed from a counter; the NEXT chunk's keys are loaded into registers
+// while the current one is sorted in LDS, so HBM traffic and LDS work overlap
+// (the LDS rounds are bank-conflict bound: ~9 random-address LDS ops per key).
+//
+// Per chunk: KPT keys per lane in registers (item j of lane l of wave w =
+// chunk position w*64*KPT + j*64 + l, the order the stable rank walks -- as
+// in pass_tile).  Each round: per-wave digit counts (LDS atomics) -> one wave
+// scans the 256 digits and turns the counts into per-wave running offsets ->
+// rank (lane-ordered ds_add_rtn, or the ballot match) -> scatter into the LDS
+// stage -> reload in stage order.  Rounds 0..nLow-1 sort by the window's low
+// digits; a chunk of several buckets takes one more round on (second digit -
+// chunk's first), which orders its buckets.  The stage then holds the sorted
+// chunk: written back in place, each wave storing 256 contiguous bytes per
+// instruction.
+//
+// Positions past the chunk hold a PADDING key whose digit is 255 in every
+// round: padding sorts after every real key (same digit, later position), so
+// real keys take slots [0, size) and no per-item predicate is needed between
+// the load and the final store.
+#ifndef THRS_LOC_CFG
+#define THRS_LOC_CFG 8, 36  // waves, keys per lane: 2 workgroups per CU
+#endif
+constexpr int kLocCfg[2] = {THRS_LOC_CFG};
+constexpr int kLocWaves = kLocCfg[0], kLocThreads = 64 * kLocWaves, kLocKpt = kLocCfg[1];
+constexpr uint32_t kLocCap = (uint32_t)kLocThreads * kLocKpt;  // 18432 keys
+enum { kMetaClaim = 2 };
+#ifndef THRS_LOC_PERSIST
+#define THRS_LOC_PERSIST 0  // 1: persistent workgroups with next-chunk prefetch; 0: one workgroup per chunk
+#endif
+template <typename U> constexpr size_t local_lds_bytes() {
+  return (size_t)kLocCap * sizeof(U) + (size_t)kLocWaves * kBins * 4;
+}
+
+// raw 4-byte key whose getKeyBits image is y (inverse of KeyTraits::bits, for
+// images that do not come from -0)
+template <int KT> __device__ __forceinline__ uint32_t unbits32(uint32_t y) {
+  if constexpr (KT == 2) return (y & 0x80000000u) ? (y ^ 0x80000000u) : ~y;
+  else return y;
+}
+
+struct LocChunk {
+  uint32_t start, size, b0;
+  int rounds;
+};
+
+template <int KT>
+__device__ __forceinline__ LocChunk loc_chunk(uint32_t c, int nLow, const uint32_t* __restrict__ chunkOff,
+                                              const uint32_t* __restrict__ chunkB0) {
+  LocChunk ch;
+  ch.start = chunkOff[c];
+  ch.size = chunkOff[c + 1] - ch.start;  // <= kLocCap (else the fallback flag is set)
+  const uint32_t bA = chunkB0[c], bB = chunkB0[c + 1];
+  ch.b0 = bA & 0xFFu;
+  ch.rounds = nLow + ((bB - bA > 1u) ? 1 : 0);
+  return ch;
+}
+
+// padding image: ones in every low digit, (b0 - 1) in the second digit (its
+// multi-round digit is 255), zero elsewhere -- bits 24..31 are never a local
+// digit and stay 0, so the image is never 0x7FFFFFFF (the one unbits32 miss)
+template <int KT>
+__device__ __forceinline__ uint32_t loc_pad(uint32_t b0, int nLow, int startBits, uint32_t orderMask) {
+  const uint32_t padT = (((1u << (8 * nLow)) - 1u) << startBits) | (((b0 - 1u) & 0xFFu) << (startBits + 8 * nLow));
+  return unbits32<KT>(padT ^ orderMask);
+}
+
+template <int KT>
+__device__ __forceinline__ void loc_load(typename KeyTraits<KT>::U (&k)[kLocKpt],
+                                         const typename KeyTraits<KT>::U* __restrict__ keys, const LocChunk& ch,
+                                         uint32_t pad) {
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int32_t lim = (int32_t)ch.size - (int32_t)(w * 64 * kLocKpt + lane);
+  pin(reinterpret_cast<uint32_t&>(lim));
+  const typename KeyTraits<KT>::U* src = keys + ch.start + w * 64 * kLocKpt + lane;
+#pragma unroll
+  for (int j = 0; j < kLocKpt; ++j) k[j] = (j * 64 < lim) ? src[j * 64] : pad;
+}
+
+template <int KT, bool ATOMIC_RANK>
+__device__ __forceinline__ void loc_sort_chunk(typename KeyTraits<KT>::U (&k)[kLocKpt],
+                                               typename KeyTraits<KT>::U* __restrict__ keys, const LocChunk& ch,
+                                               typename KeyTraits<KT>::U orderMask, int startBits, int nLow,
+                                               unsigned char* smem) {
+  using U = typename KeyTraits<KT>::U;
+  constexpr int KPT = kLocKpt;
+  constexpr uint32_t CHUNK = 64 * KPT;
+  U* stage = reinterpret_cast<U*>(smem);
+  uint32_t* s_cnt = reinterpret_cast<uint32_t*>(smem + (size_t)kLocCap * sizeof(U));  // [waves][256]
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  uint32_t* cnt = s_cnt + w * kBins;
+  U* stw = stage + w * CHUNK + lane;
+#if defined(THRS_LOC_EXP) && THRS_LOC_EXP == 2
+  const int roundsRun = ch.rounds > 0 ? 1 : 0;  // EXPERIMENT ONLY (wrong output): one round
+#elif defined(THRS_LOC_EXP) && THRS_LOC_EXP == 1
+  const int roundsRun = 0;  // EXPERIMENT ONLY (wrong output): no rounds
+#else
+  const int roundsRun = ch.rounds;
+#endif
+  for (int r = 0; r < roundsRun; ++r) {
+    const int shift = r < nLow ? startBits + 8 * r : startBits + 8 * nLow;
+    const uint32_t sub = r < nLow ? 0u : ch.b0;
+    auto digit_of = [&](U key) -> uint32_t {
+      return ((uint32_t)((KeyTraits<KT>::bits(key) ^ orderMask) >> shift) - sub) & 0xFFu;
+    };
+#pragma unroll
+    for (int i = 0; i < kBins / 64; ++i) cnt[i * 64 + lane] = 0;
+#pragma unroll
+    for (int j = 0; j < KPT; ++j)
+      __hip_atomic_fetch_add(&cnt[digit_of(k[j])], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    lds_barrier();
+    {  // threads d < 256: digit d's total over the waves -> block exclusive scan
+       // (wave totals through stage words: the stage is free between the
+       // reload and the scatter) -> per-wave running offsets
+      uint32_t* s_wt = reinterpret_cast<uint32_t*>(stage);
+      uint32_t c[kLocWaves], tot = 0, inc = 0;
+      if (tid < kBins) {
+#pragma unroll
+        for (int ww = 0; ww < kLocWaves; ++ww) {
+          c[ww] = s_cnt[ww * kBins + tid];
+          tot += c[ww];
+        }
+        inc = wave_incl_scan(tot, lane);
+        if (lane == 63) s_wt[w] = inc;
+      }
+      lds_barrier();
+      if (tid < kBins) {
+        const uint32_t w0 = s_wt[0], w1 = s_wt[1], w2 = s_wt[2];
+        uint32_t run = inc - tot + (w > 0 ? w0 : 0u) + (w > 1 ? w1 : 0u) + (w > 2 ? w2 : 0u);
+#pragma unroll
+        for (int ww = 0; ww < kLocWaves; ++ww) {
+          s_cnt[ww * kBins + tid] = run;
+          run += c[ww];
+        }
+      }
+    }
+    lds_barrier();
+    // rank + scatter (every lane of every item: the rank's wave is fully active)
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) {
+      pin(k[j]);
+      const uint32_t dj = digit_of(k[j]);
+      uint32_t slot;
+      if constexpr (ATOMIC_RANK) {
+        slot = __hip_atomic_fetch_add(&cnt[dj], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      } else {
+        uint32_t mlo, mhi;
+        match_digit(dj, mlo, mhi);
+        const uint32_t cc = cnt[dj];
+        slot = __builtin_amdgcn_mbcnt_hi(mhi, __builtin_amdgcn_mbcnt_lo(mlo, cc));
+        cnt[dj] = __builtin_popcount(mhi) + __builtin_popcount(mlo) + cc;
+      }
+      stage[slot] = k[j];
+#ifndef THRS_LOC_NOSB
+      __builtin_amdgcn_sched_barrier(0);
+#endif
+    }
+    lds_barrier();
+    if (r + 1 < roundsRun) {
+#pragma unroll
+      for (int j = 0; j < KPT; ++j) k[j] = stw[j * 64];
+    }
+  }
+  int32_t lim = (int32_t)ch.size - (int32_t)(w * CHUNK + lane);
+  pin(reinterpret_cast<uint32_t&>(lim));
+  U* src = keys + ch.start + w * CHUNK + lane;
+  if (roundsRun == 0) {
+#pragma unroll
+    for (int j = 0; j < KPT; ++j)
+      if (j * 64 < lim) src[j * 64] = k[j];
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < KPT; ++j)
+    if (j * 64 < lim) src[j * 64] = stw[j * 64];
+}
+
+template <int KT, bool ATOMIC_RANK>
+__global__ __launch_bounds__(kLocThreads) void thrs_local(typename KeyTraits<KT>::U* __restrict__ keys,
+                                                          typename KeyTraits<KT>::U orderMask, int startBits,
+                                                          int nLow, const uint32_t* __restrict__ chunkOff,
+                                                          const uint32_t* __restrict__ chunkB0,
+                                                          uint32_t* __restrict__ meta) {
+  using U = typename KeyTraits<KT>::U;
+  static_assert(sizeof(U) == 4, "the local sort is for 4-byte keys");
+  if (meta[kMetaFallback] != 0) return;  // the plain LSD passes sorted everything
+  const uint32_t nChunks = meta[kMetaChunks];
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+#if !THRS_LOC_PERSIST
+  {
+    const uint32_t c = blockIdx.x;
+    if (c >= nChunks) return;
+    const LocChunk ch = loc_chunk<KT>(c, nLow, chunkOff, chunkB0);
+    if (ch.size == 0) return;
+    U k[kLocKpt];
+    loc_load<KT>(k, keys, ch, loc_pad<KT>(ch.b0, nLow, startBits, (uint32_t)orderMask));
+    loc_sort_chunk<KT, ATOMIC_RANK>(k, keys, ch, orderMask, startBits, nLow, smem);
+    return;
+  }
+#endif
+  // the claimed chunk id is handed over in stage word 0: free between a
+  // chunk's write-out (its reads end at the barrier before the claim) and the
+  // next chunk's first scan (every thread has read the id by then)
+  uint32_t* s_claim = reinterpret_cast<uint32_t*>(smem);
+  auto claim = [&]() -> uint32_t {  // one barrier; callers are past every read of the previous claim
+    if (threadIdx.x == 0) *s_claim = atomicAdd(&meta[kMetaClaim], 1u);
+    lds_barrier();
+    return __builtin_amdgcn_readfirstlane(*s_claim);
+  };
+  uint32_t c = claim();
+  if (c >= nChunks) return;
+  LocChunk ch = loc_chunk<KT>(c, nLow, chunkOff, chunkB0);
+  U k[kLocKpt];
+  loc_load<KT>(k, keys, ch, loc_pad<KT>(ch.b0, nLow, startBits, (uint32_t)orderMask));
+  for (;;) {
+    const uint32_t cn = claim();
+    U kn[kLocKpt];
+    LocChunk chn{};
+    if (cn < nChunks) {  // next chunk's loads in flight during this chunk's LDS rounds
+      chn = loc_chunk<KT>(cn, nLow, chunkOff, chunkB0);
+      loc_load<KT>(kn, keys, chn, loc_pad<KT>(chn.b0, nLow, startBits, (uint32_t)orderMask));
+    }
+    if (ch.size) loc_sort_chunk<KT, ATOMIC_RANK>(k, keys, ch, orderMask, startBits, nLow, smem);
+    if (cn >= nChunks) break;
+    lds_barrier();  // every wave is past the write-out's stage reads
+#pragma unroll
+    for (int j = 0; j < kLocKpt; ++j) k[j] = kn[j];
+    ch = chn;
+  }
+}
+
+// Copy on the fallback path only (odd number of low passes: their result is
+// in the temporary buffer; the two top-digit passes read the caller's).
+__global__ void thrs_copy_gated(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, uint64_t words,
+                                const uint32_t* __restrict__ gate, uint32_t want) {
+  if (*gate != want) return;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += (uint64_t)gridDim.x * blockDim.x)
+    dst[i] = src[i];
+}
+
+}  // namespace thrs_dev

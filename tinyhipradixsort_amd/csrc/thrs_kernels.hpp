@@ -164,8 +164,10 @@ template <int KT>
 __global__ __launch_bounds__(kHistThreads) void thrs_hist(const typename KeyTraits<KT>::U* __restrict__ keys,
                                                           uint32_t n, typename KeyTraits<KT>::U orderMask,
                                                           int startBits, int nPass, int vec,
-                                                          uint32_t* __restrict__ hist) {
+                                                          uint32_t* __restrict__ hist,
+                                                          const uint32_t* __restrict__ gate = nullptr) {
   using U = typename KeyTraits<KT>::U;
+  if (gate && *gate == 0) return;  // fallback-only launch (thrs_hybrid.hpp) not needed
   constexpr int NP_MAX = sizeof(U);
   constexpr int COPIES = hist_copies<(int)sizeof(U)>();
   extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];  // [nPass][256][COPIES]
@@ -232,7 +234,8 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist(const typename KeyTrai
 
 // exclusive scan of each pass's histogram -> global digit bases
 __global__ __launch_bounds__(kThreads) void thrs_scan(const uint32_t* __restrict__ hist, uint32_t* __restrict__ base,
-                                                      int nPass) {
+                                                      int nPass, const uint32_t* __restrict__ gate = nullptr) {
+  if (gate && *gate == 0) return;  // fallback-only launch (thrs_hybrid.hpp) not needed
   __shared__ uint32_t s_w[4];
   for (int p = 0; p < nPass; ++p) {
     uint32_t total;
@@ -904,7 +907,9 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
     const typename ValueWord<VB>::T* __restrict__ valsIn, typename ValueWord<VB>::T* __restrict__ valsOut,
     uint32_t n, typename KeyTraits<KT>::U orderMask, int shift, const uint32_t* __restrict__ digitBase,
     ST* __restrict__ status, ST* __restrict__ statusNext, uint32_t* __restrict__ tileCounter,
-    uint32_t* __restrict__ errFlag, GroupTables<ST> grp, uint64_t* __restrict__ stamps) {
+    uint32_t* __restrict__ errFlag, GroupTables<ST> grp, uint64_t* __restrict__ stamps,
+    const uint32_t* __restrict__ gate, uint32_t gateWant) {
+  if (gate && *gate != gateWant) return;  // pass not needed on this launch path (thrs_plan decides)
   using G = PassGeom<sizeof(typename KeyTraits<KT>::U), VB>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint32_t* s_cnt = reinterpret_cast<uint32_t*>(smem + G::STAGE * (sizeof(typename KeyTraits<KT>::U) + VB));
@@ -955,7 +960,9 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
     const typename ValueWord<VB>::T* __restrict__ valsIn, typename ValueWord<VB>::T* __restrict__ valsOut,
     uint32_t n, typename KeyTraits<KT>::U orderMask, int shift, const uint32_t* __restrict__ digitBase,
     ST* __restrict__ status, ST* __restrict__ statusNext, uint32_t* __restrict__ tileCounter,
-    uint32_t* __restrict__ errFlag, GroupTables<ST> grp, uint64_t* __restrict__ stamps) {
+    uint32_t* __restrict__ errFlag, GroupTables<ST> grp, uint64_t* __restrict__ stamps,
+    const uint32_t* __restrict__ gate, uint32_t gateWant) {
+  if (gate && *gate != gateWant) return;  // pass not needed on this launch path (thrs_plan decides)
   using U = typename KeyTraits<KT>::U;
   using VW = typename ValueWord<VB>::T;
   using G = PassGeom<sizeof(U), VB>;
@@ -1076,7 +1083,9 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
     const typename ValueWord<VB>::T* __restrict__ valsIn, typename ValueWord<VB>::T* __restrict__ valsOut,
     uint32_t n, typename KeyTraits<KT>::U orderMask, int shift, const uint32_t* __restrict__ digitBase,
     ST* __restrict__ status, ST* __restrict__ statusNext, uint32_t* __restrict__ claimState,
-    uint32_t* __restrict__ errFlag, GroupTables<ST> grp, uint64_t* __restrict__ stamps) {
+    uint32_t* __restrict__ errFlag, GroupTables<ST> grp, uint64_t* __restrict__ stamps,
+    const uint32_t* __restrict__ gate, uint32_t gateWant) {
+  if (gate && *gate != gateWant) return;  // pass not needed on this launch path (thrs_plan decides)
   using U = typename KeyTraits<KT>::U;
   using VW = typename ValueWord<VB>::T;
   using G = PassGeom<sizeof(U), VB>;
