@@ -6,9 +6,12 @@ metric: "Gkeys/s and achieved HBM GB/s (% of peak), u32 keys N=2^30, 1/2/4/8 GPU
 * N=1 (default): workload C2 = sortKeys of 2^30 u32 keys, bits [0,32), the
   reference bench's input distribution (splitmix64 from state 0,
   unittest.cpp:544-548), generated on the GPU and resident in HBM before the
-  timed region.  One step = one full sort (histogram + 4 per-digit passes) of a
-  FRESH input buffer (the sort is in place, so every step gets its own
-  pre-generated buffer; see --pool).
+  timed region.  One step = one full sort of a FRESH input buffer (the sort is
+  in place, so every step gets its own pre-generated buffer; see --pool).  For
+  4-byte keys-only sorts the library takes its 3-HBM-pass path: bucket
+  histogram + plan, two device-wide passes for the top two digits, and one
+  in-LDS local sort of every 16-bit bucket; other workloads run
+  histogram + one pass per digit.
 * N>1: launched by torch.distributed.run, one rank per GPU; each rank holds
   2^30 u32 keys (weak scaling) and one step is the bucket-exchange sort of all
   N*2^30 keys (local digit histogram -> RCCL all-gather of counts -> local
@@ -275,10 +278,18 @@ def main():
                 "kernel": "thrs_pass", "avg_launch_ms": round(avg_pass_ms, 4),
                 "alg_bytes_per_launch": alg_bytes,
                 "hist_avg_ms": round(prof["hist_ms"] / max(1, prof["hist_launches"]), 4)}
-        # whole-sort algorithmic rate (B_alg = P*2*N*(K+V))
+        # whole-sort algorithmic rate (B_alg = P*2*N*(K+V) for P 8-bit digits,
+        # SURVEY.md s8(d)) -- the work of P LSD passes, whatever path ran
         passes = kb * 8 // 8
         roof["sort_alg_GBps"] = round(passes * alg_bytes * global_keys / n / (elapsed / steps) / 1e9, 1)
         roof["sort_frac_of_peak"] = round(roof["sort_alg_GBps"] / PEAK_HBM_GBS / max(1, world), 4)
+        roof["pass_launches_per_sort"] = round(prof["pass_launches"] / steps, 2)
+        if prof.get("local_launches"):
+            # the 3-HBM-pass path's local bucket sort: reads and writes every key once
+            lm = prof["local_ms"] / prof["local_launches"]
+            la = alg_bytes / (lm / 1e3) / 1e9
+            roof["local"] = {"kernel": "thrs_local", "avg_launch_ms": round(lm, 4), "achieved": round(la, 1),
+                             "frac": round(la / PEAK_HBM_GBS, 4), "alg_bytes_per_launch": alg_bytes}
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline == "auto":

@@ -19,10 +19,15 @@ import statistics
 import sys
 from collections import defaultdict
 
-FAMILIES = ["thrs_pass", "thrs_hist", "thrs_scan", "k_copy_u128", "k_copy_u32", "k_fill", "k_iota",
-            "k_sorted", "k_fingerprint", "thrs_probe"]
+FAMILIES = ["thrs_pass", "thrs_hist_joint", "thrs_hist", "thrs_scan", "thrs_plan", "thrs_local", "thrs_copy_gated",
+            "k_copy_u128", "k_copy_u32", "k_fill", "k_iota", "k_sorted", "k_fingerprint", "thrs_probe"]
 # dominant global access width per family, for counter calibration
-WIDTH16 = {"thrs_hist": True, "k_copy_u128": True}
+WIDTH16 = {"thrs_hist": True, "thrs_hist_joint": True, "k_copy_u128": True}
+# launches of the 3-HBM-pass path that exit at once unless the fallback flag
+# is set (the low-digit passes and their histogram): reported apart
+GATED = ("thrs_pass", "thrs_hist")
+GATED_NS = 100_000           # shorter than this = a gated launch that exited
+GATED_KIB = 1024             # FETCH_SIZE / WRITE_SIZE below 1 MiB = the same
 GIB = 1 << 30
 
 
@@ -56,7 +61,10 @@ def durations(d):
             name = col(r, "Kernel_Name", "Kernel-Name", "KernelName")
             t0 = int(col(r, "Start_Timestamp", "Start-Timestamp", "BeginNs"))
             t1 = int(col(r, "End_Timestamp", "End-Timestamp", "EndNs"))
-            out[family(name)].append(t1 - t0)
+            fam = family(name)
+            if fam in GATED and t1 - t0 < GATED_NS:
+                fam += "_gated"
+            out[fam].append(t1 - t0)
     return out
 
 
@@ -72,6 +80,8 @@ def counters(d):
             per[(family(name), disp)][cname] += val
     out = defaultdict(lambda: defaultdict(list))
     for (fam, _), cs in per.items():
+        if fam in GATED and all(v < (GATED_KIB if c in ("FETCH_SIZE", "WRITE_SIZE") else 1e5) for c, v in cs.items()):
+            fam += "_gated"
         for c, v in cs.items():
             out[fam][c].append(v)
     return out

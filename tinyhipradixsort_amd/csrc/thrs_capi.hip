@@ -294,6 +294,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
       if (allow_lds(thrs_hist_joint<KT>, kJointLds) != hipSuccess) return THRS_ERROR_HIP;
       hipLaunchKernelGGL(thrs_hist_joint<KT>, dim3(grid), dim3(kHistThreads), kJointLds, stream,
                          static_cast<const U*>(keys), n, orderMask, startBits + 8 * nLow, vec, joint);
+      // chunks: whole buckets; neighbouring buckets below kLocCap/2 keys share one
       hipLaunchKernelGGL(thrs_plan, dim3(1), dim3(kPlanThreads), 0, stream, joint, n, base + nLow * kBins, chunkOff,
                          chunkB0, meta, kLocCap, kLocCap / 2);
       // the low digits' histograms + bases: needed only on the fallback path
@@ -402,19 +403,21 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   launch_pass(nLow + 1, keyOut, K, nullptr, nullptr, nullptr);
   {
     ProfScope prof(stream, 2);
-    const size_t llds = local_lds_bytes<U>();
-    auto lk = atomicRank ? thrs_local<KT, true> : thrs_local<KT, false>;
-    if (allow_lds(lk, llds) != hipSuccess) return THRS_ERROR_HIP;
-    int perCU = 0;  // persistent: as many workgroups as fit at once
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, lk, kLocThreads, llds) != hipSuccess || perCU < 1)
-      perCU = 1;
-    // never more workgroups than chunks can exist: <= 256 (one per top digit)
-    // + 2 per non-empty bucket, and <= the number of buckets
-    const uint64_t maxChunks = std::min<uint64_t>(kBuckets, 256 + 2 * (uint64_t)n);
-    const uint32_t lgrid = THRS_LOC_PERSIST ? (uint32_t)std::min<uint64_t>(maxChunks, (uint64_t)perCU * cu_count())
-                                            : (uint32_t)maxChunks;
-    hipLaunchKernelGGL(lk, dim3(lgrid), dim3(kLocThreads), llds, stream, K, orderMask, startBits, nLow, chunkOff,
-                       chunkB0, meta);
+    {
+      const size_t llds = local_lds_bytes<U>();
+      auto lk = atomicRank ? thrs_local<KT, true> : thrs_local<KT, false>;
+      if (allow_lds(lk, llds) != hipSuccess) return THRS_ERROR_HIP;
+      int perCU = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, lk, kLocThreads, llds) != hipSuccess || perCU < 1)
+        perCU = 1;
+      // never more workgroups than chunks can exist: <= 256 (one per top digit)
+      // + 2 per non-empty bucket, and <= the number of buckets
+      const uint64_t maxChunks = std::min<uint64_t>(kBuckets, 256 + 2 * (uint64_t)n);
+      const uint32_t lgrid = THRS_LOC_PERSIST ? (uint32_t)std::min<uint64_t>(maxChunks, (uint64_t)perCU * cu_count())
+                                              : (uint32_t)maxChunks;
+      hipLaunchKernelGGL(lk, dim3(lgrid), dim3(kLocThreads), llds, stream, K, orderMask, startBits, nLow, chunkOff,
+                         chunkB0, meta);
+    }
   }
   if (hipGetLastError() != hipSuccess) return THRS_ERROR_HIP;
   }
