@@ -132,6 +132,10 @@ int thrs_rank_mode(void);
  * sort kernel (4-byte keys), from the runtime's occupancy calculator. */
 int thrs_debug_local_occupancy(void);
 
+/* Diagnostic: in -DTHRS_STAMPS builds only, the local bucket sort writes 8
+ * s_memrealtime stamps per chunk to buf[chunk*8 .. +7] (NULL = off). */
+int thrs_debug_set_local_stamps(void* buf);
+
 /* == thrs::Buffer (tinyhipradixsort.hpp:501-528): hipMalloc(max(bytes,1)). */
 int thrs_malloc(void** ptr, int64_t bytes);
 int thrs_free(void* ptr);

@@ -160,7 +160,8 @@ struct ProfScope {  // records [a, b) around the launches issued in its lifetime
   }
 };
 
-uint64_t* g_stamps = nullptr;  // THRS_STAMPS diagnostic builds only (thrs_debug_set_stamps)
+uint64_t* g_stamps = nullptr;   // THRS_STAMPS diagnostic builds only (thrs_debug_set_stamps)
+uint64_t* g_lstamps = nullptr;  // same, local sort: [chunk][8] (thrs_debug_set_local_stamps)
 
 // Per-device result of thrs_probe_lds_order: 1 = lane-ordered LDS atomics
 // (fast rank), 0 = ballot-match rank.  -1 = not probed yet.  THRS_RANK=ballot
@@ -416,7 +417,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
       const uint32_t lgrid = THRS_LOC_PERSIST ? (uint32_t)std::min<uint64_t>(maxChunks, (uint64_t)perCU * cu_count())
                                               : (uint32_t)maxChunks;
       hipLaunchKernelGGL(lk, dim3(lgrid), dim3(kLocThreads), llds, stream, K, orderMask, startBits, nLow, chunkOff,
-                         chunkB0, meta);
+                         chunkB0, meta, g_lstamps);
     }
   }
   if (hipGetLastError() != hipSuccess) return THRS_ERROR_HIP;
@@ -607,6 +608,13 @@ THRS_API int thrs_profile_read(double* histMs, int* histLaunches, double* passMs
 // the pass kernel writes per-tile phase timestamps to buf[(pass*nTiles+tile)*16+i].
 THRS_API int thrs_debug_set_stamps(void* buf) {
   g_stamps = static_cast<uint64_t*>(buf);
+  return THRS_SUCCESS;
+}
+
+// Diagnostic hook: in -DTHRS_STAMPS builds the local sort kernel writes
+// per-chunk phase timestamps to buf[chunk*8+i] (thrs_hybrid.hpp loc_stamp).
+THRS_API int thrs_debug_set_local_stamps(void* buf) {
+  g_lstamps = static_cast<uint64_t*>(buf);
   return THRS_SUCCESS;
 }
 

@@ -347,11 +347,24 @@ __device__ __forceinline__ void loc_load(typename KeyTraits<KT>::U (&k)[kLocKpt]
   for (int j = 0; j < kLocKpt; ++j) k[j] = (j * 64 < lim) ? src[j * 64] : pad;
 }
 
+// THRS_STAMPS builds: per chunk, s_memrealtime (100 MHz) at 0 entry, 1 keys
+// loaded, 2 round 0 done, 3 round 1 done, 4 write-out issued, 5 stores
+// drained; slot 6 = HW_ID (CU / SE), 7 = XCC id (thread 0 of the workgroup).
+constexpr int kLocStampSlots = 8;
+__device__ __forceinline__ void loc_stamp(uint64_t* st, int i) {
+#ifdef THRS_STAMPS
+  if (st && threadIdx.x == 0) st[i] = __builtin_amdgcn_s_memrealtime();
+#else
+  (void)st;
+  (void)i;
+#endif
+}
+
 template <int KT, bool ATOMIC_RANK>
 __device__ __forceinline__ void loc_sort_chunk(typename KeyTraits<KT>::U (&k)[kLocKpt],
                                                typename KeyTraits<KT>::U* __restrict__ keys, const LocChunk& ch,
                                                typename KeyTraits<KT>::U orderMask, int startBits, int nLow,
-                                               unsigned char* smem) {
+                                               unsigned char* smem, uint64_t* st = nullptr) {
   using U = typename KeyTraits<KT>::U;
   constexpr int KPT = kLocKpt;
   constexpr uint32_t CHUNK = 64 * KPT;
@@ -361,6 +374,10 @@ __device__ __forceinline__ void loc_sort_chunk(typename KeyTraits<KT>::U (&k)[kL
   const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6);
   uint32_t* cnt = s_cnt + w * kBins;
   U* stw = stage + w * CHUNK + lane;
+  // items wholly past the chunk (j*64 >= limw: padding in every lane) take no
+  // part in any round: they rank after every real key, so skipping them
+  // changes no real key's slot (scalar test: limw is wave-uniform)
+  const int32_t limw = __builtin_amdgcn_readfirstlane((int32_t)ch.size - (int32_t)(w * CHUNK));
 #if defined(THRS_LOC_EXP) && THRS_LOC_EXP == 2
   const int roundsRun = ch.rounds > 0 ? 1 : 0;  // EXPERIMENT ONLY (wrong output): one round
 #elif defined(THRS_LOC_EXP) && THRS_LOC_EXP == 1
@@ -378,7 +395,8 @@ __device__ __forceinline__ void loc_sort_chunk(typename KeyTraits<KT>::U (&k)[kL
     for (int i = 0; i < kBins / 64; ++i) cnt[i * 64 + lane] = 0;
 #pragma unroll
     for (int j = 0; j < KPT; ++j)
-      __hip_atomic_fetch_add(&cnt[digit_of(k[j])], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (j * 64 < limw)
+        __hip_atomic_fetch_add(&cnt[digit_of(k[j])], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     lds_barrier();
     {  // threads d < 256: digit d's total over the waves -> block exclusive scan
        // (wave totals through stage words: the stage is free between the
@@ -406,30 +424,45 @@ __device__ __forceinline__ void loc_sort_chunk(typename KeyTraits<KT>::U (&k)[kL
       }
     }
     lds_barrier();
-    // rank + scatter (every lane of every item: the rank's wave is fully active)
-#pragma unroll
-    for (int j = 0; j < KPT; ++j) {
-      pin(k[j]);
-      const uint32_t dj = digit_of(k[j]);
-      uint32_t slot;
-      if constexpr (ATOMIC_RANK) {
-        slot = __hip_atomic_fetch_add(&cnt[dj], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      } else {
-        uint32_t mlo, mhi;
-        match_digit(dj, mlo, mhi);
-        const uint32_t cc = cnt[dj];
-        slot = __builtin_amdgcn_mbcnt_hi(mhi, __builtin_amdgcn_mbcnt_lo(mlo, cc));
-        cnt[dj] = __builtin_popcount(mhi) + __builtin_popcount(mlo) + cc;
-      }
-      stage[slot] = k[j];
-#ifndef THRS_LOC_NOSB
-      __builtin_amdgcn_sched_barrier(0);
+    // rank + scatter (every lane of every item: the rank's wave is fully
+    // active).  Ranks are taken in batches of RB items -- their atomics issue
+    // back to back and return together -- then the batch is scattered: a
+    // scatter write right after each rank would wait for that rank's round
+    // trip (the compiler cannot reorder LDS accesses that may alias).
+#ifndef THRS_LOC_RB
+#define THRS_LOC_RB 12
 #endif
+    constexpr int RB = THRS_LOC_RB;
+#pragma unroll
+    for (int j0 = 0; j0 < KPT; j0 += RB) {
+      uint32_t sl[RB];
+#pragma unroll
+      for (int jj = 0; jj < RB; ++jj) {
+        const int j = j0 + jj;
+        if (j < KPT && j * 64 < limw) {
+          const uint32_t dj = digit_of(k[j]);
+          if constexpr (ATOMIC_RANK) {
+            sl[jj] = __hip_atomic_fetch_add(&cnt[dj], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          } else {
+            uint32_t mlo, mhi;
+            match_digit(dj, mlo, mhi);
+            const uint32_t cc = cnt[dj];
+            sl[jj] = __builtin_amdgcn_mbcnt_hi(mhi, __builtin_amdgcn_mbcnt_lo(mlo, cc));
+            cnt[dj] = __builtin_popcount(mhi) + __builtin_popcount(mlo) + cc;
+          }
+        }
+      }
+#pragma unroll
+      for (int jj = 0; jj < RB; ++jj)
+        if (j0 + jj < KPT && (j0 + jj) * 64 < limw) stage[sl[jj]] = k[j0 + jj];
+      __builtin_amdgcn_sched_barrier(0);
     }
     lds_barrier();
+    loc_stamp(st, 2 + (r & 1));
     if (r + 1 < roundsRun) {
 #pragma unroll
-      for (int j = 0; j < KPT; ++j) k[j] = stw[j * 64];
+      for (int j = 0; j < KPT; ++j)
+        if (j * 64 < limw) k[j] = stw[j * 64];
     }
   }
   int32_t lim = (int32_t)ch.size - (int32_t)(w * CHUNK + lane);
@@ -444,6 +477,13 @@ __device__ __forceinline__ void loc_sort_chunk(typename KeyTraits<KT>::U (&k)[kL
 #pragma unroll
   for (int j = 0; j < KPT; ++j)
     if (j * 64 < lim) src[j * 64] = stw[j * 64];
+#ifdef THRS_STAMPS
+  loc_stamp(st, 4);
+  if (st) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    loc_stamp(st, 5);
+  }
+#endif
 }
 
 template <int KT, bool ATOMIC_RANK>
@@ -451,7 +491,7 @@ __global__ __launch_bounds__(kLocThreads) void thrs_local(typename KeyTraits<KT>
                                                           typename KeyTraits<KT>::U orderMask, int startBits,
                                                           int nLow, const uint32_t* __restrict__ chunkOff,
                                                           const uint32_t* __restrict__ chunkB0,
-                                                          uint32_t* __restrict__ meta) {
+                                                          uint32_t* __restrict__ meta, uint64_t* __restrict__ stamps) {
   using U = typename KeyTraits<KT>::U;
   static_assert(sizeof(U) == 4, "the local sort is for 4-byte keys");
   if (meta[kMetaFallback] != 0) return;  // the plain LSD passes sorted everything
@@ -461,11 +501,25 @@ __global__ __launch_bounds__(kLocThreads) void thrs_local(typename KeyTraits<KT>
   {
     const uint32_t c = blockIdx.x;
     if (c >= nChunks) return;
+    uint64_t* st = stamps ? stamps + (uint64_t)c * kLocStampSlots : nullptr;
+    loc_stamp(st, 0);
     const LocChunk ch = loc_chunk<KT>(c, nLow, chunkOff, chunkB0);
     if (ch.size == 0) return;
     U k[kLocKpt];
     loc_load<KT>(k, keys, ch, loc_pad<KT>(ch.b0, nLow, startBits, (uint32_t)orderMask));
-    loc_sort_chunk<KT, ATOMIC_RANK>(k, keys, ch, orderMask, startBits, nLow, smem);
+#ifdef THRS_STAMPS
+    if (st) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      loc_stamp(st, 1);
+      if (threadIdx.x == 0) {
+        uint32_t hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        st[6] = hw;
+        st[7] = xcc_id();
+      }
+    }
+#endif
+    loc_sort_chunk<KT, ATOMIC_RANK>(k, keys, ch, orderMask, startBits, nLow, smem, st);
     return;
   }
 #endif
