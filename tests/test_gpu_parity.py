@@ -197,6 +197,33 @@ def test_hybrid_paths_vs_oracle(gpu, kt, desc):
                 assert np.array_equal(k, ek), (name, n, s, e)
 
 
+@pytest.mark.parametrize("desc", [False, True])
+def test_hybrid_pairs_vs_oracle(gpu, desc):
+    """sortPairs with u32 keys + u32 values over the whole key takes the hybrid
+    path (single-bucket chunks, positions carried in the local sort's items);
+    stability on ties, the gated LSD fallback, and partial windows (plain LSD)."""
+    torch = gpu
+    rs = make_sorter(O.U32, 4, desc)
+    dists = {
+        "uniform": lambda k: k,
+        "low20": lambda k: k & np.array(0xFFFFF, k.dtype),
+        "ties": lambda k: k & np.array(0xFF00FF00, k.dtype),
+        "few": lambda k: k & np.array(0x00030007, k.dtype),
+        "const": lambda k: np.full_like(k, k[0]),
+    }
+    j = 0
+    for name, f in dists.items():
+        for n in [1, 100, 18432, 18433, 70001, 300007, 1 << 20]:
+            for (s, e) in [(0, 32), (8, 32)]:
+                j += 1
+                keys = f(O.randomize_np(O.U32, O.splitmix64_stream(9191 * j, n)))
+                vals = np.arange(n, dtype=np.uint32) * np.uint32(2654435761)
+                k, v = gpu_sort(torch, rs, {"keys": keys, "values": vals}, O.U32, 4, s, e)
+                ek, ev = O.lsd_sort(O.U32, keys, vals, s, e, desc)
+                assert np.array_equal(k, ek), (name, n, s, e)
+                assert np.array_equal(v, ev), (name, n, s, e)
+
+
 def test_concurrent_sorts_on_distinct_temps(gpu):
     """Per-call state lives in the caller's temp buffer: two sorts on two
     streams at once (the reference's module-global g_iterator would race)."""

@@ -274,8 +274,10 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
 
   const U orderMask = desc ? (U)~(U)0 : (U)0;
   const int hyEnv = hybrid_override();
-  constexpr bool kHybridType = sizeof(U) == 4 && VB == 0;  // 4-byte keys without values
-  const bool hybrid = kHybridType && !counts && nPass >= 3 && hyEnv != 0;
+  // 4-byte keys without values; u32 keys with 4-byte values over the whole key
+  constexpr bool kHybridType = sizeof(U) == 4 && (VB == 0 || (VB == 4 && KT == 0));
+  const bool fullWindow = startBits == 0 && nPass * 8 >= (int)(8 * sizeof(U));
+  const bool hybrid = kHybridType && !counts && nPass >= 3 && hyEnv != 0 && (VB == 0 || fullWindow);
   const int nLow = nPass - 2;
 
   // header (histograms, tile counters, error word) + first status table; the
@@ -297,7 +299,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                          static_cast<const U*>(keys), n, orderMask, startBits + 8 * nLow, vec, joint);
       // chunks: whole buckets; neighbouring buckets below kLocCap/2 keys share one
       hipLaunchKernelGGL(thrs_plan, dim3(1), dim3(kPlanThreads), 0, stream, joint, n, base + nLow * kBins, chunkOff,
-                         chunkB0, meta, kLocCap, kLocCap / 2);
+                         chunkB0, meta, kLocCap, VB ? -1 : kLocLogT);  // pairs: single-bucket chunks
       // the low digits' histograms + bases: needed only on the fallback path
       const size_t lds = (size_t)nLow * kBins * hist_copies<(int)sizeof(U)>() * 4;
       if (allow_lds(thrs_hist<KT>, lds) != hipSuccess) return THRS_ERROR_HIP;
@@ -388,39 +390,55 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
 
   // ---- hybrid: fallback-only low passes, then the two top digits, then local
   if constexpr (kHybridType) {
-  U* K = static_cast<U*>(keys);
-  {
-    U* kin = K;
-    U* kout = keyOut;
-    for (int p = 0; p < nLow; ++p) {
-      launch_pass(p, kin, kout, nullptr, nullptr, meta + kMetaFallback);
-      std::swap(kin, kout);
-    }
-    if (nLow & 1)  // fallback result is in keyOut: the top-digit passes read K
-      hipLaunchKernelGGL(thrs_copy_gated, dim3(2048), dim3(256), 0, stream, reinterpret_cast<const uint32_t*>(keyOut),
-                         reinterpret_cast<uint32_t*>(K), (uint64_t)n, meta + kMetaFallback, 1u);
-  }
-  launch_pass(nLow, K, keyOut, nullptr, nullptr, nullptr);
-  launch_pass(nLow + 1, keyOut, K, nullptr, nullptr, nullptr);
-  {
-    ProfScope prof(stream, 2);
+    U* K = static_cast<U*>(keys);
+    VW* V = static_cast<VW*>(vals);
     {
+      U* kin = K;
+      U* kout = keyOut;
+      VW* vin = V;
+      VW* vout = valOut;
+      for (int p = 0; p < nLow; ++p) {
+        launch_pass(p, kin, kout, vin, vout, meta + kMetaFallback);
+        std::swap(kin, kout);
+        std::swap(vin, vout);
+      }
+      if (nLow & 1) {  // fallback result is in keyOut: the top-digit passes read K
+        hipLaunchKernelGGL(thrs_copy_gated, dim3(2048), dim3(256), 0, stream,
+                           reinterpret_cast<const uint32_t*>(keyOut), reinterpret_cast<uint32_t*>(K), (uint64_t)n,
+                           meta + kMetaFallback, 1u);
+        if (VB)
+          hipLaunchKernelGGL(thrs_copy_gated, dim3(2048), dim3(256), 0, stream,
+                             reinterpret_cast<const uint32_t*>(valOut), reinterpret_cast<uint32_t*>(V),
+                             (uint64_t)n * VB / 4, meta + kMetaFallback, 1u);
+      }
+    }
+    launch_pass(nLow, K, keyOut, V, valOut, nullptr);
+    launch_pass(nLow + 1, keyOut, K, valOut, V, nullptr);
+    {
+      ProfScope prof(stream, 2);
       const size_t llds = local_lds_bytes<U>();
-      auto lk = atomicRank ? thrs_local<KT, true> : thrs_local<KT, false>;
-      if (allow_lds(lk, llds) != hipSuccess) return THRS_ERROR_HIP;
-      int perCU = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, lk, kLocThreads, llds) != hipSuccess || perCU < 1)
-        perCU = 1;
       // never more workgroups than chunks can exist: <= 256 (one per top digit)
       // + 2 per non-empty bucket, and <= the number of buckets
       const uint64_t maxChunks = std::min<uint64_t>(kBuckets, 256 + 2 * (uint64_t)n);
-      const uint32_t lgrid = THRS_LOC_PERSIST ? (uint32_t)std::min<uint64_t>(maxChunks, (uint64_t)perCU * cu_count())
-                                              : (uint32_t)maxChunks;
-      hipLaunchKernelGGL(lk, dim3(lgrid), dim3(kLocThreads), llds, stream, K, orderMask, startBits, nLow, chunkOff,
-                         chunkB0, meta, g_lstamps);
+      if constexpr (VB == 4) {
+        auto lk = atomicRank ? thrs_local_pairs<true> : thrs_local_pairs<false>;
+        if (allow_lds(lk, llds) != hipSuccess) return THRS_ERROR_HIP;
+        hipLaunchKernelGGL(lk, dim3((uint32_t)maxChunks), dim3(kLocThreads), llds, stream,
+                           reinterpret_cast<uint32_t*>(K), reinterpret_cast<uint32_t*>(V), (uint32_t)orderMask,
+                           chunkOff, chunkB0, meta);
+      } else {
+        auto lk = atomicRank ? thrs_local<KT, true> : thrs_local<KT, false>;
+        if (allow_lds(lk, llds) != hipSuccess) return THRS_ERROR_HIP;
+        int perCU = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, lk, kLocThreads, llds) != hipSuccess || perCU < 1)
+          perCU = 1;
+        const uint32_t lgrid = THRS_LOC_PERSIST ? (uint32_t)std::min<uint64_t>(maxChunks, (uint64_t)perCU * cu_count())
+                                                : (uint32_t)maxChunks;
+        hipLaunchKernelGGL(lk, dim3(lgrid), dim3(kLocThreads), llds, stream, K, orderMask, startBits, nLow, chunkOff,
+                           chunkB0, meta, g_lstamps);
+      }
     }
-  }
-  if (hipGetLastError() != hipSuccess) return THRS_ERROR_HIP;
+    if (hipGetLastError() != hipSuccess) return THRS_ERROR_HIP;
   }
   return THRS_SUCCESS;
 }

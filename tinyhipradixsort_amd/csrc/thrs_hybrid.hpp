@@ -137,7 +137,7 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
 // (floor(off/T) differs from the previous bucket's), or b or b-1 holds more
 // than T keys.  All buckets of a multi-bucket chunk start inside one T-window
 // and hold <= T keys, so a chunk holds < 2T <= cap keys unless it is a single
-// bucket; a single bucket above cap sets the fallback flag.
+// bucket; a single bucket above cap sets the fallback flag.  T = 2^logT.
 constexpr int kPlanThreads = 1024;
 __device__ __forceinline__ uint32_t block_excl_scan1024(uint32_t v, uint32_t* s_w, uint32_t* total) {
   const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -160,7 +160,7 @@ __global__ __launch_bounds__(kPlanThreads) void thrs_plan(const uint32_t* __rest
                                                           uint32_t* __restrict__ baseTop /* [2][256]: second, top */,
                                                           uint32_t* __restrict__ chunkOff,
                                                           uint32_t* __restrict__ chunkB0, uint32_t* __restrict__ meta,
-                                                          uint32_t cap, uint32_t T) {
+                                                          uint32_t cap, int logT) {
   constexpr int SLICE_ROWS = 32;  // column sums through an LDS transpose, 32 top-digit rows at a time
   __shared__ uint32_t s_tr[SLICE_ROWS][kBins + 1];
   __shared__ uint32_t s_last[kPlanThreads], s_w[kPlanThreads / 64], s_row[kBins], s_flag;
@@ -230,8 +230,14 @@ __global__ __launch_bounds__(kPlanThreads) void thrs_plan(const uint32_t* __rest
   }
 
   // chunk starts
+  // logT < 0: single-bucket chunks (every non-empty bucket, and every bucket
+  // after one, opens a chunk); else T = 2^logT (a shift, not a division)
+  const bool single = logT < 0;
+  const int lt = single ? 0 : logT;
+  const uint32_t T = 1u << lt;
   auto opens = [&](uint32_t b, uint32_t off, uint32_t sz, uint32_t prevSz) -> bool {
-    return (b & 255u) == 0 || (off / T) != ((off - prevSz) / T) || sz > T || prevSz > T;
+    if (single) return (b & 255u) == 0 || sz != 0 || prevSz != 0;
+    return (b & 255u) == 0 || (off >> lt) != ((off - prevSz) >> lt) || sz > T || prevSz > T;
   };
   uint32_t nOpen = 0;
   {
@@ -294,6 +300,7 @@ __global__ __launch_bounds__(kPlanThreads) void thrs_plan(const uint32_t* __rest
 constexpr int kLocCfg[2] = {THRS_LOC_CFG};
 constexpr int kLocWaves = kLocCfg[0], kLocThreads = 64 * kLocWaves, kLocKpt = kLocCfg[1];
 constexpr uint32_t kLocCap = (uint32_t)kLocThreads * kLocKpt;  // 18432 keys
+constexpr int kLocLogT = 31 - __builtin_clz(kLocCap / 2);      // chunking window T = 8192 <= cap / 2
 enum { kMetaClaim = 2 };
 #ifndef THRS_LOC_PERSIST
 #define THRS_LOC_PERSIST 0  // 1: persistent workgroups with next-chunk prefetch; 0: one workgroup per chunk
@@ -360,11 +367,12 @@ __device__ __forceinline__ void loc_stamp(uint64_t* st, int i) {
 #endif
 }
 
+// The LDS rounds of one chunk: on return (after a barrier) the stage holds
+// the chunk's items in sorted order; returns the number of rounds run.
 template <int KT, bool ATOMIC_RANK>
-__device__ __forceinline__ void loc_sort_chunk(typename KeyTraits<KT>::U (&k)[kLocKpt],
-                                               typename KeyTraits<KT>::U* __restrict__ keys, const LocChunk& ch,
-                                               typename KeyTraits<KT>::U orderMask, int startBits, int nLow,
-                                               unsigned char* smem, uint64_t* st = nullptr) {
+__device__ __forceinline__ int loc_rounds(typename KeyTraits<KT>::U (&k)[kLocKpt], const LocChunk& ch,
+                                          typename KeyTraits<KT>::U orderMask, int startBits, int nLow,
+                                          unsigned char* smem, uint64_t* st) {
   using U = typename KeyTraits<KT>::U;
   constexpr int KPT = kLocKpt;
   constexpr uint32_t CHUNK = 64 * KPT;
@@ -465,6 +473,22 @@ __device__ __forceinline__ void loc_sort_chunk(typename KeyTraits<KT>::U (&k)[kL
         if (j * 64 < limw) k[j] = stw[j * 64];
     }
   }
+  return roundsRun;
+}
+
+template <int KT, bool ATOMIC_RANK>
+__device__ __forceinline__ void loc_sort_chunk(typename KeyTraits<KT>::U (&k)[kLocKpt],
+                                               typename KeyTraits<KT>::U* __restrict__ keys, const LocChunk& ch,
+                                               typename KeyTraits<KT>::U orderMask, int startBits, int nLow,
+                                               unsigned char* smem, uint64_t* st = nullptr) {
+  using U = typename KeyTraits<KT>::U;
+  constexpr int KPT = kLocKpt;
+  constexpr uint32_t CHUNK = 64 * KPT;
+  const int roundsRun = loc_rounds<KT, ATOMIC_RANK>(k, ch, orderMask, startBits, nLow, smem, st);
+  const U* stage = reinterpret_cast<const U*>(smem);
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const U* stw = stage + w * CHUNK + lane;
   int32_t lim = (int32_t)ch.size - (int32_t)(w * CHUNK + lane);
   pin(reinterpret_cast<uint32_t&>(lim));
   U* src = keys + ch.start + w * CHUNK + lane;
@@ -552,6 +576,74 @@ __global__ __launch_bounds__(kLocThreads) void thrs_local(typename KeyTraits<KT>
     for (int j = 0; j < kLocKpt; ++j) k[j] = kn[j];
     ch = chn;
   }
+}
+
+// ------------------------------------------------------ local sort, pairs
+// sortPairs with u32 keys and 4-byte values over the whole key (startBits 0,
+// 32 bits): chunks are single buckets (thrs_plan single mode), so a key is
+// (bucket << 16 | low16) in image space and needs only its low 16 bits plus
+// its chunk position to be carried: item = low16 << 16 | position (positions
+// < 18432 < 2^16).  The rounds sort the items by their top 16 bits, exactly
+// as the keys-only rounds (stable, lane-ordered rank); then the keys are
+// rebuilt from the bucket and written, and the values are permuted through
+// the same LDS stage by the carried positions.  (f32 keys stay on the LSD
+// path: +0 and -0 share one image and could not be rebuilt bit-exactly.)
+template <bool ATOMIC_RANK>
+__global__ __launch_bounds__(kLocThreads) __attribute__((amdgpu_waves_per_eu(4))) void thrs_local_pairs(
+    uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, uint32_t orderMask,
+    const uint32_t* __restrict__ chunkOff, const uint32_t* __restrict__ chunkB0, const uint32_t* __restrict__ meta) {
+  constexpr int KPT = kLocKpt;
+  constexpr uint32_t CHUNK = 64 * KPT;
+  if (meta[kMetaFallback] != 0) return;  // the plain LSD passes sorted everything
+  const uint32_t c = blockIdx.x;
+  if (c >= meta[kMetaChunks]) return;
+  LocChunk ch;
+  ch.start = chunkOff[c];
+  ch.size = chunkOff[c + 1] - ch.start;
+  if (ch.size == 0) return;
+  ch.b0 = 0;
+  ch.rounds = 2;  // single-bucket chunk: the two low digits of the key = the item's top 16 bits
+  const uint32_t hiImg = chunkB0[c] << 16;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  int32_t lim = (int32_t)ch.size - (int32_t)(w * CHUNK + lane);
+  pin(reinterpret_cast<uint32_t&>(lim));
+  uint32_t* ksrc = keys + ch.start + w * CHUNK + lane;
+  uint32_t* vsrc = vals + ch.start + w * CHUNK + lane;
+  uint32_t it[KPT];
+#pragma unroll
+  for (int j = 0; j < KPT; ++j) {
+    const uint32_t pos = w * CHUNK + j * 64 + lane;
+    it[j] = (j * 64 < lim) ? (((ksrc[j * 64] ^ orderMask) << 16) | pos) : 0xFFFF0000u;  // padding: digits 255
+  }
+  loc_rounds<0, ATOMIC_RANK>(it, ch, 0u, 16, 2, smem, nullptr);
+  // values of this thread's positions (the item registers are free again)
+  pin(reinterpret_cast<uint32_t&>(lim));
+#pragma unroll
+  for (int j = 0; j < KPT; ++j)
+    if (j * 64 < lim) it[j] = vsrc[j * 64];
+  uint32_t* stage = reinterpret_cast<uint32_t*>(smem);
+  const uint32_t* stw = stage + w * CHUNK + lane;
+  uint32_t id[(KPT + 1) / 2];  // carried positions, two 16-bit halves per register
+#pragma unroll
+  for (int j = 0; j < (KPT + 1) / 2; ++j) id[j] = 0;
+#pragma unroll
+  for (int j = 0; j < KPT; ++j) {
+    if (j * 64 < lim) {
+      const uint32_t item = stw[j * 64];
+      ksrc[j * 64] = (hiImg | (item >> 16)) ^ orderMask;
+      id[j / 2] |= (item & 0xFFFFu) << (16 * (j & 1));
+    }
+  }
+  lds_barrier();  // every sorted item has been read: the stage takes the values
+#pragma unroll
+  for (int j = 0; j < KPT; ++j)
+    if (j * 64 < lim) stage[w * CHUNK + j * 64 + lane] = it[j];
+  lds_barrier();
+#pragma unroll
+  for (int j = 0; j < KPT; ++j)
+    if (j * 64 < lim) vsrc[j * 64] = stage[(id[j / 2] >> (16 * (j & 1))) & 0xFFFFu];
 }
 
 // Copy on the fallback path only (odd number of low passes: their result is
