@@ -158,8 +158,8 @@ def test_cpp_port_with_claim_mode_forced(gpu, xb):
 @pytest.mark.parametrize("hy", ["1", "0"])
 def test_cpp_port_with_hybrid_forced(gpu, hy):
     """The UTEST matrix with the 3-HBM-pass path (bucket passes + local LDS
-    sort, thrs_hybrid.hpp) on (THRS_HYBRID=1, also the default) and off (plain
-    LSD passes for every window)."""
+    sort, thrs_hybrid.hpp) forced on for every size (THRS_HYBRID=1; by default
+    it runs for n in [0.75 * 2^30, 2^30 + 2^26]) and off (plain LSD passes)."""
     exe = os.path.join(ROOT, "tests", "cpp", "unittest_thrs")
     env = dict(os.environ, THRS_HYBRID=hy)
     r = subprocess.run([exe], capture_output=True, text=True, timeout=900, env=env)
@@ -168,12 +168,14 @@ def test_cpp_port_with_hybrid_forced(gpu, hy):
 
 @pytest.mark.parametrize("kt", [O.U32, O.F32])
 @pytest.mark.parametrize("desc", [False, True])
-def test_hybrid_paths_vs_oracle(gpu, kt, desc):
-    """4-byte keys-only sorts with >= 3 digits take the hybrid path: chunked
+def test_hybrid_paths_vs_oracle(gpu, kt, desc, monkeypatch):
+    """4-byte keys-only sorts with >= 3 digits take the hybrid path (forced
+    here for every size; by default it runs for n in [0.75*2^30, 2^30 + 2^26]): chunked
     local sort (single- and multi-bucket chunks), and the gated fallback to
     plain LSD when one bucket exceeds the local capacity (18432 keys) --
     including an odd number of low passes (window of 3 digits: gated copy)."""
     torch = gpu
+    monkeypatch.setenv("THRS_HYBRID", "1")
     rs = make_sorter(kt, 0, desc)
     dists = {
         "uniform": lambda k: k,
@@ -198,11 +200,12 @@ def test_hybrid_paths_vs_oracle(gpu, kt, desc):
 
 
 @pytest.mark.parametrize("desc", [False, True])
-def test_hybrid_pairs_vs_oracle(gpu, desc):
+def test_hybrid_pairs_vs_oracle(gpu, desc, monkeypatch):
     """sortPairs with u32 keys + u32 values over the whole key takes the hybrid
     path (single-bucket chunks, positions carried in the local sort's items);
     stability on ties, the gated LSD fallback, and partial windows (plain LSD)."""
     torch = gpu
+    monkeypatch.setenv("THRS_HYBRID", "1")  # forced for every size
     rs = make_sorter(O.U32, 4, desc)
     dists = {
         "uniform": lambda k: k,

@@ -221,15 +221,13 @@ hipError_t allow_lds(F kernel, size_t bytes) {
 }
 
 // THRS_HYBRID=1 / THRS_HYBRID=0 in the environment: force the 3-HBM-pass path
-// (thrs_hybrid.hpp) on / off wherever it applies (-1 = default: on).
+// (thrs_hybrid.hpp) on / off wherever it applies (-1 = default: by size).
+// Read on every sort (tests switch it within one process).
 int hybrid_override() {
-  static const int v = [] {
-    const char* e = getenv("THRS_HYBRID");
-    if (e && !strcmp(e, "1")) return 1;
-    if (e && !strcmp(e, "0")) return 0;
-    return -1;
-  }();
-  return v;
+  const char* e = getenv("THRS_HYBRID");
+  if (e && !strcmp(e, "1")) return 1;
+  if (e && !strcmp(e, "0")) return 0;
+  return -1;
 }
 
 // One launch sequence.  Sort mode (counts == nullptr): the result lands in
@@ -277,7 +275,15 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   // 4-byte keys without values; u32 keys with 4-byte values over the whole key
   constexpr bool kHybridType = sizeof(U) == 4 && (VB == 0 || (VB == 4 && KT == 0));
   const bool fullWindow = startBits == 0 && nPass * 8 >= (int)(8 * sizeof(U));
-  const bool hybrid = kHybridType && !counts && nPass >= 3 && hyEnv != 0 && (VB == 0 || fullWindow);
+  // Size window (uniform keys: n / 65536 keys per bucket; docs/EXPERIMENTS.md
+  // row 29).  The local sort costs about the same per chunk whatever its size,
+  // so below ~0.75 * 2^30 the two passes it replaces are cheaper; above
+  // 2^30 + 2^26 the largest of 65536 uniform buckets (mean + ~4.5 sigma)
+  // outgrows kLocCap and the fallback would pay for the bucket histogram in
+  // vain.  THRS_HYBRID=1 forces the path for any n (tests), =0 turns it off.
+  const bool sizeOk = (uint64_t)n >= (3ull << 28) && (uint64_t)n <= (1ull << 30) + (1ull << 26);
+  const bool hybrid = kHybridType && !counts && nPass >= 3 && (hyEnv == 1 || (hyEnv < 0 && sizeOk)) &&
+                      (VB == 0 || fullWindow);
   const int nLow = nPass - 2;
 
   // header (histograms, tile counters, error word) + first status table; the

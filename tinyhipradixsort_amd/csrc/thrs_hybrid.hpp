@@ -161,57 +161,67 @@ __global__ __launch_bounds__(kPlanThreads) void thrs_plan(const uint32_t* __rest
                                                           uint32_t* __restrict__ chunkOff,
                                                           uint32_t* __restrict__ chunkB0, uint32_t* __restrict__ meta,
                                                           uint32_t cap, int logT) {
-  constexpr int SLICE_ROWS = 32;  // column sums through an LDS transpose, 32 top-digit rows at a time
-  __shared__ uint32_t s_tr[SLICE_ROWS][kBins + 1];
-  __shared__ uint32_t s_last[kPlanThreads], s_w[kPlanThreads / 64], s_row[kBins], s_flag;
-  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  // Wave w owns buckets [4096w, 4096w + 4096); in step i (0..63) lane l holds
+  // bucket 4096w + 64i + l, so every load and every chunk-table store is
+  // lane-consecutive; prefixes in bucket order come from wave scans.
+  constexpr int WAVES = kPlanThreads / 64, STEPS = (int)kBuckets / kPlanThreads;  // 16, 64
+  __shared__ uint32_t s_col[WAVES][kBins], s_row[kBins], s_wsum[WAVES], s_wopen[WAVES], s_wlast[WAVES], s_flag;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint32_t* src = joint + w * (64 * STEPS) + lane;
   if (tid == 0) s_flag = 0;
-  constexpr int PER = kBuckets / kPlanThreads;  // 64: thread t owns row t>>2, columns 64(t&3)..+63
-  const uint32_t b0 = tid * PER;
-  uint32_t v[PER];  // 16 x 16-B loads, all in flight at once
-  {
-    const uint4* q = reinterpret_cast<const uint4*>(joint + b0);
-#pragma unroll
-    for (int i = 0; i < PER / 4; ++i) {
-      const uint4 x = q[i];
-      v[4 * i] = x.x; v[4 * i + 1] = x.y; v[4 * i + 2] = x.z; v[4 * i + 3] = x.w;
-    }
-  }
-  uint32_t sum = 0;
+  // logT < 0: single-bucket chunks (every non-empty bucket, and every bucket
+  // after one, opens a chunk); else T = 2^logT (a shift, not a division)
+  const bool single = logT < 0;
+  const int lt = single ? 0 : logT;
+  const uint32_t T = 1u << lt;
+  auto opens = [&](uint32_t b, uint32_t off, uint32_t sz, uint32_t prevSz) -> bool {
+    if (single) return (b & 255u) == 0 || sz != 0 || prevSz != 0;
+    return (b & 255u) == 0 || (off >> lt) != ((off - prevSz) >> lt) || sz > T || prevSz > T;
+  };
+
+  // sweep 1: wave totals, the fallback test, row (top digit) and column
+  // (second digit) sums.  Bucket 4096w + 64i + l: row 16w + i/4, column 64(i%4) + l.
+  uint32_t tot = 0, col[4] = {0, 0, 0, 0};
   bool big = false;
-#pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    sum += v[i];
-    big |= v[i] > cap;
-  }
-  {  // row (top digit) sums: four consecutive threads
-    uint32_t r = sum + __shfl_xor(sum, 1, 64);
-    r += __shfl_xor(r, 2, 64);
-    if ((tid & 3u) == 0) s_row[tid >> 2] = r;
-  }
-  uint32_t colSum = 0;  // thread c < 256: column (second digit) c
-  for (int sl = 0; sl < kBins / SLICE_ROWS; ++sl) {
-    if ((tid >> 7) == (uint32_t)sl) {
-      const uint32_t row = (tid >> 2) - sl * SLICE_ROWS, col0 = (tid & 3u) * PER;
-#pragma unroll
-      for (int i = 0; i < PER; ++i) s_tr[row][col0 + i] = v[i];
-    }
-    __syncthreads();
-    if (tid < kBins) {
 #pragma unroll 8
-      for (int r = 0; r < SLICE_ROWS; ++r) colSum += s_tr[r][tid];
+  for (int q4 = 0; q4 < STEPS / 4; ++q4) {
+    uint32_t rs = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t x = src[64 * (4 * q4 + q)];
+      big |= x > cap;
+      col[q] += x;
+      rs += x;
     }
-    __syncthreads();
+    tot += rs;
+    // row 16w + q4: sum over the wave
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) rs += __shfl_xor(rs, off, 64);
+    if (lane == 0) s_row[16 * w + q4] = rs;
   }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) s_col[w][64 * q + lane] = col[q];
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) tot += __shfl_xor(tot, off, 64);
+  if (lane == 0) s_wsum[w] = tot;
+  if (lane == 63) s_wlast[w] = src[64 * (STEPS - 1)];
   if (big) s_flag = 1;
-  s_last[tid] = v[PER - 1];
-  uint32_t total;
-  const uint32_t excl = block_excl_scan1024(sum, s_w, &total);  // its barriers publish s_last, s_row, s_flag
-  (void)total;
-  {  // bases of the two top digits: [0] second digit (column sums), [1] top digit (row sums)
+  __syncthreads();
+  uint32_t wbase = 0;
+  for (uint32_t ww = 0; ww < w; ++ww) wbase += s_wsum[ww];
+  const uint32_t prevLast0 = w ? s_wlast[w - 1] : 0u;  // bucket before this wave's first
+
+  // digit bases of the two top digits: [0] second digit (column sums), [1] top digit (row sums)
+  if (tid < kBins) {
+    uint32_t cs = 0;
+#pragma unroll
+    for (int ww = 0; ww < WAVES; ++ww) cs += s_col[ww][tid];
+    s_col[0][tid] = cs;  // (each thread reads and rewrites its own column only)
+  }
+  __syncthreads();
+  {
     __shared__ uint32_t s_wt[2][4];
-    const uint32_t w = tid >> 6;
-    const uint32_t x0 = tid < kBins ? colSum : 0u, x1 = tid < kBins ? s_row[tid] : 0u;
+    const uint32_t x0 = tid < kBins ? s_col[0][tid] : 0u, x1 = tid < kBins ? s_row[tid] : 0u;
     const uint32_t i0 = wave_incl_scan(x0, lane), i1 = wave_incl_scan(x1, lane);
     if (tid < kBins && lane == 63) {
       s_wt[0][w] = i0;
@@ -229,47 +239,54 @@ __global__ __launch_bounds__(kPlanThreads) void thrs_plan(const uint32_t* __rest
     }
   }
 
-  // chunk starts
-  // logT < 0: single-bucket chunks (every non-empty bucket, and every bucket
-  // after one, opens a chunk); else T = 2^logT (a shift, not a division)
-  const bool single = logT < 0;
-  const int lt = single ? 0 : logT;
-  const uint32_t T = 1u << lt;
-  auto opens = [&](uint32_t b, uint32_t off, uint32_t sz, uint32_t prevSz) -> bool {
-    if (single) return (b & 255u) == 0 || sz != 0 || prevSz != 0;
-    return (b & 255u) == 0 || (off >> lt) != ((off - prevSz) >> lt) || sz > T || prevSz > T;
-  };
-  uint32_t nOpen = 0;
-  {
-    uint32_t off = excl, prev = tid ? s_last[tid - 1] : 0u;
+  // sweeps 2 and 3: absolute offsets in bucket order, chunk-opening flags;
+  // sweep 2 counts the wave's chunks, sweep 3 writes them
+  auto sweep = [&](bool write, uint32_t cbase) -> uint32_t {
+    uint32_t run = wbase, prevTop = prevLast0, nOpen = 0;
+    constexpr int BATCH = 16;  // loads of a batch in flight together (L2 hits, ~1 us each otherwise)
+    for (int i0 = 0; i0 < STEPS; i0 += BATCH) {
+    uint32_t xb[BATCH];
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      nOpen += opens(b0 + i, off, v[i], prev) ? 1u : 0u;
-      off += v[i];
-      prev = v[i];
-    }
-  }
-  uint32_t nChunks;
-  uint32_t c = block_excl_scan1024(nOpen, s_w, &nChunks);
-  {
-    uint32_t off = excl, prev = tid ? s_last[tid - 1] : 0u;
+    for (int q = 0; q < BATCH; ++q) xb[q] = src[64 * (i0 + q)];
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      if (opens(b0 + i, off, v[i], prev)) {
+    for (int q = 0; q < BATCH; ++q) {
+      const int i = i0 + q;
+      const uint32_t x = xb[q];
+      const uint32_t inc = wave_incl_scan(x, lane);
+      const uint32_t off = run + inc - x;
+      uint32_t prev = __shfl_up(x, 1, 64);
+      if (lane == 0) prev = prevTop;
+      const uint32_t b = w * (64 * STEPS) + 64 * i + lane;
+      const bool o = opens(b, off, x, prev);
+      const uint64_t m = __ballot(o);
+      if (write && o) {
+        const uint32_t c = cbase + nOpen + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
         chunkOff[c] = off;
-        chunkB0[c] = b0 + i;
-        ++c;
+        chunkB0[c] = b;
       }
-      off += v[i];
-      prev = v[i];
+      nOpen += (uint32_t)__builtin_popcountll(m);
+      run += __shfl(inc, 63, 64);
+      prevTop = __shfl(x, 63, 64);
     }
+    }
+    return nOpen;
+  };
+  const uint32_t myOpen = sweep(false, 0);
+  if (lane == 0) s_wopen[w] = myOpen;
+  __syncthreads();
+  uint32_t cbase = 0, nChunks = 0;
+  for (int ww = 0; ww < WAVES; ++ww) {
+    cbase += ((uint32_t)ww < w) ? s_wopen[ww] : 0u;
+    nChunks += s_wopen[ww];
   }
+  sweep(true, cbase);
   if (tid == kPlanThreads - 1) {
     chunkOff[nChunks] = n;
     chunkB0[nChunks] = kBuckets;
     meta[kMetaChunks] = nChunks;
     meta[kMetaFallback] = s_flag;
-    meta[2] = 0;  // kMetaClaim: the local sort's chunk counter
+    meta[2] = 0;  // kMetaClaim: the persistent local sort's chunk counter
   }
 }
 
@@ -300,7 +317,7 @@ __global__ __launch_bounds__(kPlanThreads) void thrs_plan(const uint32_t* __rest
 constexpr int kLocCfg[2] = {THRS_LOC_CFG};
 constexpr int kLocWaves = kLocCfg[0], kLocThreads = 64 * kLocWaves, kLocKpt = kLocCfg[1];
 constexpr uint32_t kLocCap = (uint32_t)kLocThreads * kLocKpt;  // 18432 keys
-constexpr int kLocLogT = 31 - __builtin_clz(kLocCap / 2);      // chunking window T = 8192 <= cap / 2
+constexpr int kLocLogT = 12;  // chunking window T = 4096: buckets of a 2^29+ uniform sort never merge
 enum { kMetaClaim = 2 };
 #ifndef THRS_LOC_PERSIST
 #define THRS_LOC_PERSIST 0  // 1: persistent workgroups with next-chunk prefetch; 0: one workgroup per chunk
@@ -588,6 +605,9 @@ __global__ __launch_bounds__(kLocThreads) void thrs_local(typename KeyTraits<KT>
 // rebuilt from the bucket and written, and the values are permuted through
 // the same LDS stage by the carried positions.  (f32 keys stay on the LSD
 // path: +0 and -0 share one image and could not be rebuilt bit-exactly.)
+#ifndef THRS_PAIRS_EARLY_VALUES
+#define THRS_PAIRS_EARLY_VALUES 0  // 1: load the values with the keys (spills 36 VGPRs at 8x36)
+#endif
 template <bool ATOMIC_RANK>
 __global__ __launch_bounds__(kLocThreads) __attribute__((amdgpu_waves_per_eu(4))) void thrs_local_pairs(
     uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, uint32_t orderMask,
@@ -617,12 +637,22 @@ __global__ __launch_bounds__(kLocThreads) __attribute__((amdgpu_waves_per_eu(4))
     const uint32_t pos = w * CHUNK + j * 64 + lane;
     it[j] = (j * 64 < lim) ? (((ksrc[j * 64] ^ orderMask) << 16) | pos) : 0xFFFF0000u;  // padding: digits 255
   }
+#if THRS_PAIRS_EARLY_VALUES
+  uint32_t vv[KPT];  // values in flight during the rounds
+#pragma unroll
+  for (int j = 0; j < KPT; ++j) vv[j] = (j * 64 < lim) ? vsrc[j * 64] : 0u;
+#endif
   loc_rounds<0, ATOMIC_RANK>(it, ch, 0u, 16, 2, smem, nullptr);
-  // values of this thread's positions (the item registers are free again)
   pin(reinterpret_cast<uint32_t&>(lim));
+#if THRS_PAIRS_EARLY_VALUES
+#pragma unroll
+  for (int j = 0; j < KPT; ++j) it[j] = vv[j];
+#else
+  // values of this thread's positions (the item registers are free again)
 #pragma unroll
   for (int j = 0; j < KPT; ++j)
     if (j * 64 < lim) it[j] = vsrc[j * 64];
+#endif
   uint32_t* stage = reinterpret_cast<uint32_t*>(smem);
   const uint32_t* stw = stage + w * CHUNK + lane;
   uint32_t id[(KPT + 1) / 2];  // carried positions, two 16-bit halves per register
