@@ -166,9 +166,10 @@ def test_cpp_port_with_hybrid_forced(gpu, hy):
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
 
 
+@pytest.mark.parametrize("seg", ["1", "0"])
 @pytest.mark.parametrize("kt", [O.U32, O.F32])
 @pytest.mark.parametrize("desc", [False, True])
-def test_hybrid_paths_vs_oracle(gpu, kt, desc, monkeypatch):
+def test_hybrid_paths_vs_oracle(gpu, kt, desc, seg, monkeypatch):
     """4-byte keys-only sorts with >= 3 digits take the hybrid path (forced
     here for every size; by default it runs for n in [0.75*2^30, 2^30 + 2^26]): chunked
     local sort (single- and multi-bucket chunks), and the gated fallback to
@@ -176,6 +177,7 @@ def test_hybrid_paths_vs_oracle(gpu, kt, desc, monkeypatch):
     including an odd number of low passes (window of 3 digits: gated copy)."""
     torch = gpu
     monkeypatch.setenv("THRS_HYBRID", "1")
+    monkeypatch.setenv("THRS_SEG", seg)  # top-digit pass XCD-segmented (default) or not
     rs = make_sorter(kt, 0, desc)
     dists = {
         "uniform": lambda k: k,

@@ -87,7 +87,12 @@ constexpr uint64_t kJointBytes = kBuckets * 4;
 constexpr uint64_t kChunkOffOff = kJointBytes;
 constexpr uint64_t kChunkB0Off = kChunkOffOff + round_up_c((kBuckets + 1) * 4, 256);
 constexpr uint64_t kMetaOff = kChunkB0Off + round_up_c((kBuckets + 1) * 4, 256);
-constexpr uint64_t kHybridBytes = kMetaOff + 256;
+constexpr uint64_t kSegInfoOff = kMetaOff + 256;      // segPos[9] | segTiles[9] ... tickets[8] at +256 B (thrs_pass_seg)
+constexpr uint64_t kSegBaseOff = kSegInfoOff + 512;   // u32 [8][256] per-segment top-digit bases
+constexpr uint64_t kHybridBytes = kSegBaseOff + kSegs * 256 * 4;
+// tile ids of the segmented pass: each of the 8 segments adds at most one
+// partial tile and rounds its id range up to a multiple of kGroup
+constexpr uint64_t kSegTilePad = kSegs * kGroup;
 
 Plan make_plan(int keyType, int valueBytesOrZero, uint32_t n) {
   Plan p{};
@@ -96,8 +101,9 @@ Plan make_plan(int keyType, int valueBytesOrZero, uint32_t n) {
   p.tileKeys = tile_keys(p.kb, p.vb);
   p.nTiles = std::max<uint64_t>(1, ((uint64_t)n + p.tileKeys - 1) / p.tileKeys);
   p.wideStatus = (uint64_t)n >= (1ull << 31);
-  p.statusBytes = round_up(p.nTiles * kBins * (p.wideStatus ? 8 : 4), kAlign);
-  const uint64_t nGroups = kGroup > 0 ? (p.nTiles + kGroup - 1) / kGroup : 0;
+  const uint64_t rows = p.nTiles + kSegTilePad;  // + the segmented pass's extra tile ids
+  p.statusBytes = round_up(rows * kBins * (p.wideStatus ? 8 : 4), kAlign);
+  const uint64_t nGroups = kGroup > 0 ? (rows + kGroup - 1) / kGroup : 0;
   p.gaBytes = round_up(nGroups * kBins * 4, kAlign);
   p.gpBytes = round_up(nGroups * kBins * (p.wideStatus ? 8 : 4), kAlign);
   p.setBytes = p.statusBytes + p.gaBytes + p.gpBytes;
@@ -230,6 +236,13 @@ int hybrid_override() {
   return -1;
 }
 
+// THRS_SEG=0 in the environment: the 3-pass path's top-digit pass runs
+// unsegmented (thrs_pass / thrs_pass_xb).  Read on every sort.
+bool seg_enabled() {
+  const char* e = getenv("THRS_SEG");
+  return !(e && !strcmp(e, "0"));
+}
+
 // One launch sequence.  Sort mode (counts == nullptr): the result lands in
 // keys/vals.  Partition mode (counts != nullptr, nPass == 1,
 // thrs_partition_pass): the pass writes keyOutBuf/valOutBuf, which are the
@@ -305,7 +318,9 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                          static_cast<const U*>(keys), n, orderMask, startBits + 8 * nLow, vec, joint);
       // chunks: whole buckets; neighbouring buckets below kLocCap/2 keys share one
       hipLaunchKernelGGL(thrs_plan, dim3(1), dim3(kPlanThreads), 0, stream, joint, n, base + nLow * kBins, chunkOff,
-                         chunkB0, meta, kLocCap, VB ? -1 : kLocLogT);  // pairs: single-bucket chunks
+                         chunkB0, meta, kLocCap, VB ? -1 : kLocLogT,  // pairs: single-bucket chunks
+                         reinterpret_cast<uint32_t*>(hyb + kSegInfoOff), reinterpret_cast<uint32_t*>(hyb + kSegBaseOff),
+                         (uint32_t)G::TILE);
       // the low digits' histograms + bases: needed only on the fallback path
       const size_t lds = (size_t)nLow * kBins * hist_copies<(int)sizeof(U)>() * 4;
       if (allow_lds(thrs_hist<KT>, lds) != hipSuccess) return THRS_ERROR_HIP;
@@ -419,7 +434,31 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
       }
     }
     launch_pass(nLow, K, keyOut, V, valOut, nullptr);
-    launch_pass(nLow + 1, keyOut, K, valOut, V, nullptr);
+    if (seg_enabled()) {
+      // top digit: XCD-segmented pass (thrs_kernels.hpp thrs_pass_seg).  Its
+      // tile ids reach past nTiles (per-segment rounding): clear those rows of
+      // its table set (pass nLow cleared rows [0, nTiles) for it).
+      const int p = nLow + 1, set = p & 1;
+      const uint64_t sw = plan.wideStatus ? 8 : 4;
+      const uint64_t nGroups0 = (plan.nTiles + kGroup - 1) / kGroup;
+      if (hipMemsetAsync(reinterpret_cast<char*>(status[set]) + plan.nTiles * kBins * sw, 0,
+                         kSegTilePad * kBins * sw, stream) != hipSuccess ||
+          hipMemsetAsync(grp[set].ga + nGroups0 * kBins, 0, (kSegs + 1) * kBins * 4, stream) != hipSuccess ||
+          hipMemsetAsync(reinterpret_cast<char*>(grp[set].gp) + nGroups0 * kBins * sw, 0, (kSegs + 1) * kBins * sw,
+                         stream) != hipSuccess)
+        return THRS_ERROR_HIP;
+      auto sk = atomicRank ? thrs_pass_seg<KT, VB, ST, true> : thrs_pass_seg<KT, VB, ST, false>;
+      if (allow_lds(sk, lds) != hipSuccess) return THRS_ERROR_HIP;
+      int perCU = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, sk, G::THREADS, lds) != hipSuccess || perCU < 1)
+        perCU = 1;
+      ProfScope prof(stream, 1);
+      hipLaunchKernelGGL(sk, dim3((uint32_t)perCU * cu_count()), dim3(G::THREADS), lds, stream, keyOut, K, valOut, V,
+                         orderMask, startBits + 8 * p, reinterpret_cast<uint32_t*>(hyb + kSegInfoOff),
+                         reinterpret_cast<const uint32_t*>(hyb + kSegBaseOff), status[set], err, grp[set]);
+    } else {
+      launch_pass(nLow + 1, keyOut, K, valOut, V, nullptr);
+    }
     {
       ProfScope prof(stream, 2);
       const size_t llds = local_lds_bytes<U>();

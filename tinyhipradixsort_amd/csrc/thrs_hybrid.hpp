@@ -160,12 +160,16 @@ __global__ __launch_bounds__(kPlanThreads) void thrs_plan(const uint32_t* __rest
                                                           uint32_t* __restrict__ baseTop /* [2][256]: second, top */,
                                                           uint32_t* __restrict__ chunkOff,
                                                           uint32_t* __restrict__ chunkB0, uint32_t* __restrict__ meta,
-                                                          uint32_t cap, int logT) {
+                                                          uint32_t cap, int logT, uint32_t* __restrict__ segInfo,
+                                                          uint32_t* __restrict__ segBase, uint32_t tileKeys) {
   // Wave w owns buckets [4096w, 4096w + 4096); in step i (0..63) lane l holds
   // bucket 4096w + 64i + l, so every load and every chunk-table store is
   // lane-consecutive; prefixes in bucket order come from wave scans.
   constexpr int WAVES = kPlanThreads / 64, STEPS = (int)kBuckets / kPlanThreads;  // 16, 64
   __shared__ uint32_t s_col[WAVES][kBins], s_row[kBins], s_wsum[WAVES], s_wopen[WAVES], s_wlast[WAVES], s_flag;
+  // top-digit histogram of every second-digit segment [32s, 32s+32) (the
+  // segmented top-digit pass, thrs_pass_seg) and the second digit's bases
+  __shared__ uint32_t s_seg[kSegs][kBins], s_b2[kBins];
   const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const uint32_t* src = joint + w * (64 * STEPS) + lane;
   if (tid == 0) s_flag = 0;
@@ -192,6 +196,11 @@ __global__ __launch_bounds__(kPlanThreads) void thrs_plan(const uint32_t* __rest
       big |= x > cap;
       col[q] += x;
       rs += x;
+      // bucket (top 16w + q4, second 64q + l): segment 2q + l/32, one half-wave each
+      uint32_t hs = x;
+#pragma unroll
+      for (int off = 16; off >= 1; off >>= 1) hs += __shfl_xor(hs, off, 64);
+      if ((lane & 31u) == 0) s_seg[2 * q + (lane >> 5)][16 * w + q4] = hs;
     }
     tot += rs;
     // row 16w + q4: sum over the wave
@@ -236,6 +245,28 @@ __global__ __launch_bounds__(kPlanThreads) void thrs_plan(const uint32_t* __rest
       }
       baseTop[tid] = p0 + i0 - x0;
       baseTop[kBins + tid] = p1 + i1 - x1;
+      s_b2[tid] = p0 + i0 - x0;
+      // segment bases of the top digit: base + the top digit's keys in earlier segments
+      uint32_t sb = p1 + i1 - x1;
+      for (int sg = 0; sg < kSegs; ++sg) {
+        segBase[sg * kBins + tid] = sb;
+        sb += s_seg[sg][tid];
+      }
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {  // segment positions, first tile ids (multiples of kGroup), tickets
+    uint32_t tiles = 0;
+    for (int sg = 0; sg <= kSegs; ++sg) {
+      const uint32_t pos = sg < kSegs ? s_b2[32 * sg] : n;
+      segInfo[sg] = pos;
+      segInfo[kSegs + 1 + sg] = tiles;
+      if (sg < kSegs) {
+        const uint32_t len = (sg + 1 < kSegs ? s_b2[32 * (sg + 1)] : n) - pos;
+        const uint32_t nT = (len + tileKeys - 1) / tileKeys;
+        tiles += (nT + kGroup - 1) / kGroup * kGroup;
+        segInfo[64 + sg] = 0;  // ticket (own cache line)
+      }
     }
   }
 

@@ -291,7 +291,8 @@ template <typename ST> struct GroupTables {
   ST* gp;            // [nGroups][256] Status<ST>::pre(inclusive prefix)
   uint32_t* gaNext;  // next pass's tables, cleared by each group's last tile
   ST* gpNext;
-  uint32_t nTiles;
+  uint32_t nTiles;    // end of this tile's chain (tile ids)
+  uint32_t gmin = 0;  // first group of this tile's chain (segmented passes)
 };
 
 #ifndef THRS_RELOAD_KEYS
@@ -415,14 +416,14 @@ struct GroupWalk {
     jt = gstart;
     jg = (int32_t)g - 1;
   }
-  __device__ __forceinline__ bool walking() const { return jt < tile || jg >= 0; }
+  __device__ __forceinline__ bool walking() const { return jt < tile || jg >= (int32_t)grp->gmin; }
   __device__ __forceinline__ void issue() {
 #pragma unroll
     for (int q = 0; q < kTileWindow; ++q)
       wt[q] = (jt + q < tile) ? load_agent(status + (uint64_t)(jt + q) * kBins + d) : (ST)0;
 #pragma unroll
     for (int q = 0; q < kGroupWindow; ++q) {
-      const bool in = jg - q >= 0;
+      const bool in = jg - q >= (int32_t)grp->gmin;
       wp[q] = in ? load_agent(grp->gp + (uint64_t)(jg - q) * kBins + d) : (ST)0;
       wa[q] = in ? load_agent(grp->ga + (uint64_t)(jg - q) * kBins + d) : 0u;
     }
@@ -444,11 +445,11 @@ struct GroupWalk {
     bool gstop = false;
 #pragma unroll
     for (int q = 0; q < kGroupWindow; ++q) {
-      if (!gstop && jg >= 0) {
+      if (!gstop && jg >= (int32_t)grp->gmin) {
         if (wp[q] != 0) {  // inclusive prefix of group jg: done
           excl += Status<ST>::val(wp[q]);
           found = jg;
-          jg = -1;
+          jg = (int32_t)grp->gmin - 1;
         } else {
           const uint32_t members = min((uint32_t)kGroup, grp->nTiles - (uint32_t)jg * kGroup);
           if ((wa[q] >> 20) == members) {
@@ -531,10 +532,12 @@ struct GroupWalk {
 // Load one tile's keys (and values) into registers: item j of lane l of wave
 // w is key w*64*KPT + j*64 + l of the tile (blocked by wave, striped by lane),
 // which is the order the stable rank walks.  Keys past n read as 0.
+// keyStart / valid: the tile's first key and key count (tile * TILE and
+// min(TILE, n - tile * TILE) except in segmented passes).
 template <int KT, int VB>
 __device__ __forceinline__ void load_tile(const typename KeyTraits<KT>::U* __restrict__ keysIn,
-                                          const typename ValueWord<VB>::T* __restrict__ valsIn, uint32_t n,
-                                          uint32_t tile,
+                                          const typename ValueWord<VB>::T* __restrict__ valsIn, uint64_t keyStart,
+                                          uint32_t valid,
                                           typename KeyTraits<KT>::U (&k)[PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::KPT],
                                           typename ValueWord<VB>::T (&v)[VB ? PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::KPT : 1]) {
   using U = typename KeyTraits<KT>::U;
@@ -543,9 +546,7 @@ __device__ __forceinline__ void load_tile(const typename KeyTraits<KT>::U* __res
   constexpr int KPT = G::KPT;
   constexpr uint32_t T = G::TILE, CHUNK = 64 * KPT;
   const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const uint64_t tileBase = (uint64_t)tile * T;
-  const uint32_t valid = (uint32_t)min((uint64_t)T, (uint64_t)n - tileBase);
-  const uint64_t chunkBase = tileBase + w * CHUNK;
+  const uint64_t chunkBase = keyStart + w * CHUNK;
   int32_t lim = (int32_t)valid - (int32_t)(w * CHUNK + lane);  // item j is real iff j*64 < lim
   pin(reinterpret_cast<uint32_t&>(lim));
   if (valid == T) {
@@ -561,6 +562,11 @@ __device__ __forceinline__ void load_tile(const typename KeyTraits<KT>::U* __res
   }
 }
 
+// keys in tile `tile` of an unsegmented pass over n keys
+template <uint32_t T> __device__ __forceinline__ uint32_t tile_valid(uint32_t n, uint32_t tile) {
+  return (uint32_t)min((uint64_t)T, (uint64_t)n - (uint64_t)tile * T);
+}
+
 struct NoMid {
   __device__ __forceinline__ void operator()() const {}
 };
@@ -569,9 +575,9 @@ template <int KT, int VB, typename ST, bool ATOMIC_RANK, typename Mid>
 __device__ __forceinline__ void pass_tile(
     const typename KeyTraits<KT>::U* __restrict__ keysIn, typename KeyTraits<KT>::U* __restrict__ keysOut,
     const typename ValueWord<VB>::T* __restrict__ valsIn, typename ValueWord<VB>::T* __restrict__ valsOut,
-    uint32_t n, typename KeyTraits<KT>::U orderMask, int shift, uint32_t myBase, ST* __restrict__ status,
-    ST* __restrict__ statusNext, uint32_t* __restrict__ errFlag, uint32_t tile, uint32_t chainStart,
-    const GroupTables<ST>& grp, unsigned char* smem, uint64_t* __restrict__ stamps,
+    uint64_t keyStart, uint32_t valid, typename KeyTraits<KT>::U orderMask, int shift, uint32_t myBase,
+    ST* __restrict__ status, ST* __restrict__ statusNext, uint32_t* __restrict__ errFlag, uint32_t tile,
+    uint32_t chainStart, const GroupTables<ST>& grp, unsigned char* smem, uint64_t* __restrict__ stamps,
     typename KeyTraits<KT>::U (&k)[PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::KPT],
     typename ValueWord<VB>::T (&v)[VB ? PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::KPT : 1], Mid mid) {
   using U = typename KeyTraits<KT>::U;
@@ -607,8 +613,6 @@ __device__ __forceinline__ void pass_tile(
 #endif
 
   THRS_STAMP(1);
-  const uint64_t tileBase = (uint64_t)tile * T;
-  const uint32_t valid = (uint32_t)min((uint64_t)T, (uint64_t)n - tileBase);
   const bool full = valid == T;
   const uint32_t d = tid & 255u;
 
@@ -828,7 +832,7 @@ __device__ __forceinline__ void pass_tile(
 #if THRS_RELOAD_KEYS
       // re-read this round's keys from the tile's input (L2 / Infinity Cache
       // hits) rather than holding KPT keys in registers across the walk
-      const uint64_t chunkBase = (uint64_t)tile * T + w * CHUNK;
+      const uint64_t chunkBase = keyStart + w * CHUNK;
 #endif
 #pragma unroll
       for (int j = 0; j < KPT; ++j) {
@@ -855,7 +859,7 @@ __device__ __forceinline__ void pass_tile(
         const U key = stage_k[i];
         const uint32_t dd = (uint32_t)((KeyTraits<KT>::bits(key) ^ orderMask) >> shift) & 0xFFu;
 #ifdef THRS_FAKE_WALK
-        const uint32_t dst = min(s_gofs[dd] + slot, n - 1);  // stay in bounds
+        const uint32_t dst = min(s_gofs[dd] + slot, (uint32_t)(keyStart + valid - 1));  // stay in bounds
 #else
         const uint32_t dst = s_gofs[dd] + slot;
 #endif
@@ -941,8 +945,9 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
 #endif
   typename KeyTraits<KT>::U k[G::KPT];
   typename ValueWord<VB>::T v[VB ? G::KPT : 1];
-  load_tile<KT, VB>(keysIn, valsIn, n, tile, k, v);
-  pass_tile<KT, VB, ST, ATOMIC_RANK>(keysIn, keysOut, valsIn, valsOut, n, orderMask, shift, myBase, status,
+  load_tile<KT, VB>(keysIn, valsIn, (uint64_t)tile * G::TILE, tile_valid<G::TILE>(n, tile), k, v);
+  pass_tile<KT, VB, ST, ATOMIC_RANK>(keysIn, keysOut, valsIn, valsOut, (uint64_t)tile * G::TILE,
+                                     tile_valid<G::TILE>(n, tile), orderMask, shift, myBase, status,
                                      statusNext, errFlag, tile, 0, grp, smem, stamps, k, v, NoMid{});
 }
 
@@ -980,7 +985,7 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
   if (tile >= nTiles) return;
   U k[G::KPT];
   VW v[VB ? G::KPT : 1];
-  load_tile<KT, VB>(keysIn, valsIn, n, tile, k, v);
+  load_tile<KT, VB>(keysIn, valsIn, (uint64_t)tile * G::TILE, tile_valid<G::TILE>(n, tile), k, v);
   for (;;) {
 #ifdef THRS_STAMPS
     if (stamps && tid == 0) {
@@ -996,9 +1001,10 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
       if (tid == 0) s_misc[8] = atomicAdd(tileCounter, 1u);
       lds_barrier();
       next = s_misc[8];
-      if (next < nTiles) load_tile<KT, VB>(keysIn, valsIn, n, next, k, v);
+      if (next < nTiles) load_tile<KT, VB>(keysIn, valsIn, (uint64_t)next * G::TILE, tile_valid<G::TILE>(n, next), k, v);
     };
-    pass_tile<KT, VB, ST, ATOMIC_RANK>(keysIn, keysOut, valsIn, valsOut, n, orderMask, shift, myBase, status,
+    pass_tile<KT, VB, ST, ATOMIC_RANK>(keysIn, keysOut, valsIn, valsOut, (uint64_t)tile * G::TILE,
+                                       tile_valid<G::TILE>(n, tile), orderMask, shift, myBase, status,
                                        statusNext, errFlag, tile, 0, grp, smem, stamps, k, v, mid);
     // every wave is past its write-out: the stage, s_gofs and s_cnt are free
     for (uint32_t i = tid; i < (uint32_t)(G::WAVES * kBins); i += G::THREADS) s_cnt[i] = 0;
@@ -1114,10 +1120,95 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
     lds_barrier();
     const uint32_t tile = s_misc[0];
     if (tile == kXbDone) break;
-    load_tile<KT, VB>(keysIn, valsIn, n, tile, k, v);
-    pass_tile<KT, VB, ST, ATOMIC_RANK>(keysIn, keysOut, valsIn, valsOut, n, orderMask, shift, myBase, status,
+    load_tile<KT, VB>(keysIn, valsIn, (uint64_t)tile * G::TILE, tile_valid<G::TILE>(n, tile), k, v);
+    pass_tile<KT, VB, ST, ATOMIC_RANK>(keysIn, keysOut, valsIn, valsOut, (uint64_t)tile * G::TILE,
+                                       tile_valid<G::TILE>(n, tile), orderMask, shift, myBase, status,
                                        statusNext, errFlag, tile, 0, grp, smem, stamps, k, v, NoMid{});
     lds_barrier();  // stage, s_gofs and s_misc[0] are reused by the next tile
+  }
+}
+
+// ============================================================ XCD segments
+// Segmented pass (the 3-pass path's TOP-digit pass, thrs_hybrid.hpp): its
+// input is sorted by the second digit, so it splits into 8 segments of
+// second-digit ranges [32s, 32s+32) whose top-digit histograms -- column
+// blocks of the bucket histogram -- give every segment its own digit bases.
+// Segment s is tiled on its own (tile ids from segTiles[s], a multiple of
+// kGroup, so groups never span segments) and its look-back chain starts at
+// its first tile: segments never wait on each other.  The workgroups of XCD
+// x claim segment x's tiles in order (one ticket counter per segment), so
+// neighbouring tiles -- whose digit runs share 128-B lines -- are written
+// through one L2 and the whole segment is one contiguous range per XCD
+// (docs/EXPERIMENTS.md: abut probe 1.88 ms vs 2.08 for 8-tile blocks); a
+// workgroup whose segment is exhausted steals from the next ones.
+// Deadlock-free: a walk waits only on earlier tiles of its segment, which
+// were claimed earlier (tickets are monotone) by running workgroups.
+// segInfo: segPos[9] (key positions), segTiles[9] (first tile id); tickets[8] at word 64
+constexpr int kSegs = 8;
+template <int KT, int VB, typename ST, bool ATOMIC_RANK>
+__global__ __launch_bounds__((PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::THREADS))
+__attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::WPE))) void thrs_pass_seg(
+    const typename KeyTraits<KT>::U* __restrict__ keysIn, typename KeyTraits<KT>::U* __restrict__ keysOut,
+    const typename ValueWord<VB>::T* __restrict__ valsIn, typename ValueWord<VB>::T* __restrict__ valsOut,
+    typename KeyTraits<KT>::U orderMask, int shift, uint32_t* __restrict__ segInfo,
+    const uint32_t* __restrict__ segBase, ST* __restrict__ status, uint32_t* __restrict__ errFlag,
+    GroupTables<ST> grp) {
+  using U = typename KeyTraits<KT>::U;
+  using VW = typename ValueWord<VB>::T;
+  using G = PassGeom<sizeof(U), VB>;
+  constexpr uint32_t T = G::TILE;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint32_t* s_cnt = reinterpret_cast<uint32_t*>(smem + G::STAGE * (sizeof(U) + VB));
+  uint32_t* s_misc = s_cnt + (G::WAVES + 1) * kBins;
+  __shared__ uint32_t segPos[kSegs + 1], segTiles[kSegs + 1];  // read once per workgroup
+  uint32_t* tickets = segInfo + 64;                            // a cache line of their own
+  const uint32_t tid = threadIdx.x;
+  if (tid < 2 * (kSegs + 1)) (tid <= (uint32_t)kSegs ? segPos[tid] : segTiles[tid - kSegs - 1]) = segInfo[tid];
+  __syncthreads();
+#ifdef THRS_SEG_HOME0
+  const uint32_t home = 0;  // EXPERIMENT: every workgroup takes the segments in order (no XCD affinity)
+#else
+  const uint32_t home = xcc_id() & (kSegs - 1);
+#endif
+  uint32_t done = 0;  // thread 0: segments found exhausted
+  U k[G::KPT];
+  VW v[VB ? G::KPT : 1];
+  for (;;) {
+    if (tid == 0) {
+      uint32_t seg = kSegs, t = 0;
+      for (int q = 0; q < kSegs; ++q) {
+        const uint32_t s = (home + q) & (kSegs - 1);
+        if (done & (1u << s)) continue;
+        const uint32_t nT = (segPos[s + 1] - segPos[s] + T - 1) / T;
+        const uint32_t x = nT ? atomicAdd(&tickets[s], 1u) : nT;
+        if (x < nT) {
+          seg = s;
+          t = x;
+          break;
+        }
+        done |= 1u << s;
+      }
+      s_misc[8] = seg;
+      s_misc[9] = t;
+    }
+    for (uint32_t i = tid; i < (uint32_t)(G::WAVES * kBins); i += G::THREADS) s_cnt[i] = 0;
+    lds_barrier();
+    const uint32_t seg = s_misc[8], t = s_misc[9];
+    if (seg >= (uint32_t)kSegs) break;
+    const uint32_t segStart = segPos[seg], segEnd = segPos[seg + 1];
+    const uint64_t keyStart = (uint64_t)segStart + (uint64_t)t * T;
+    const uint32_t valid = (uint32_t)min((uint64_t)T, (uint64_t)segEnd - keyStart);
+    const uint32_t chain = segTiles[seg];
+    GroupTables<ST> g = grp;
+    g.nTiles = chain + (segEnd - segStart + T - 1) / T;  // end of this segment's tile ids
+    g.gmin = chain / kGroup;
+    g.gaNext = nullptr;
+    g.gpNext = nullptr;
+    const uint32_t myBase = segBase[seg * kBins + (tid & 255u)];
+    load_tile<KT, VB>(keysIn, valsIn, keyStart, valid, k, v);
+    pass_tile<KT, VB, ST, ATOMIC_RANK>(keysIn, keysOut, valsIn, valsOut, keyStart, valid, orderMask, shift, myBase,
+                                       status, nullptr, errFlag, chain + t, chain, g, smem, nullptr, k, v, NoMid{});
+    lds_barrier();  // stage, s_gofs and s_misc are reused by the next tile
   }
 }
 
