@@ -75,9 +75,11 @@ def test_temporary_buffer_layout(kt, vt, n):
     assert d.getOutputKeyBuffer(1000) == 1000 + d.pSumBuffer
     assert d.getOutputValueBuffer(1000) == 1000 + d.pSumBuffer + d.keyOutBuffer
     # scratch (look-back status words) stays a modest fraction of the payload
-    # (the reference's pSum region is 4*256*ceil(n/2048) = n/2 bytes, hpp:839)
+    # (the reference's pSum region is 4*256*ceil(n/2048) = n/2 bytes, hpp:839),
+    # plus a fixed ~1.1 MiB: the 3-pass path's bucket histogram and chunk table
+    # and the segmented pass's extra look-back rows
     if n >= (1 << 20):
-        assert d.pSumBuffer < 0.3 * d.keyOutBuffer
+        assert d.pSumBuffer < 0.3 * d.keyOutBuffer + (3 << 20) // 2
 
 
 def test_argument_validation_needs_no_device():

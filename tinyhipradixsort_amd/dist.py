@@ -36,6 +36,7 @@ over libthrs.so, which raises if the library is missing.
 """
 from __future__ import annotations
 
+import os
 import time
 from dataclasses import dataclass, field
 
@@ -102,6 +103,7 @@ class HipLocalOps:
     def __init__(self, config: RadixSort.Config):
         self.rs = RadixSort([], config)
         self._tmp = None
+        self.lsd_finish = False  # set by DistributedRadixSort for world > 1 (see sort)
 
     def temp(self, n: int, like):
         import torch
@@ -124,10 +126,23 @@ class HipLocalOps:
         if n == 0:
             return
         tmp = self.temp(n, keys)
-        if vals is None:
-            self.rs.sortKeys(keys, n, tmp, start_bits, end_bits)
-        else:
-            self.rs.sortPairs(keys, vals, n, tmp, start_bits, end_bits)
+        # A rank's keys share 256/world top digits, so the 3-HBM-pass path's
+        # 16-bit buckets would hold ~world * 2^14 keys each: always over the
+        # local sort's capacity, i.e. its fallback plus a wasted bucket
+        # histogram.  The finish runs the plain LSD path unless THRS_HYBRID is
+        # set by the caller.
+        forced = os.environ.get("THRS_HYBRID")
+        off = self.lsd_finish and forced is None
+        if off:
+            os.environ["THRS_HYBRID"] = "0"
+        try:
+            if vals is None:
+                self.rs.sortKeys(keys, n, tmp, start_bits, end_bits)
+            else:
+                self.rs.sortPairs(keys, vals, n, tmp, start_bits, end_bits)
+        finally:
+            if off:
+                os.environ.pop("THRS_HYBRID", None)
 
 
 # ----------------------------------------------------------------- the sorter
@@ -149,6 +164,8 @@ class DistributedRadixSort:
         cfg = RadixSort.Config(keyType=self.key_type, valueType=self.value_type or ValueType.U32,
                                sortOrder=SortOrder(sort_order))
         self.ops = ops if ops is not None else HipLocalOps(cfg)
+        if hasattr(self.ops, "lsd_finish"):
+            self.ops.lsd_finish = self.world > 1
         self.backend = dist.get_backend(group)
         self.last_plan: ExchangePlan | None = None
 
