@@ -166,10 +166,10 @@ def test_cpp_port_with_hybrid_forced(gpu, hy):
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
 
 
-@pytest.mark.parametrize("seg", ["1", "0"])
+@pytest.mark.parametrize("geom,seg", [("big", "1"), ("small", "1"), ("big", "0")])
 @pytest.mark.parametrize("kt", [O.U32, O.F32])
 @pytest.mark.parametrize("desc", [False, True])
-def test_hybrid_paths_vs_oracle(gpu, kt, desc, seg, monkeypatch):
+def test_hybrid_paths_vs_oracle(gpu, kt, desc, geom, seg, monkeypatch):
     """4-byte keys-only sorts with >= 3 digits take the hybrid path (forced
     here for every size; by default it runs for n in [0.75*2^30, 2^30 + 2^26]): chunked
     local sort (single- and multi-bucket chunks), and the gated fallback to
@@ -178,6 +178,7 @@ def test_hybrid_paths_vs_oracle(gpu, kt, desc, seg, monkeypatch):
     torch = gpu
     monkeypatch.setenv("THRS_HYBRID", "1")
     monkeypatch.setenv("THRS_SEG", seg)  # top-digit pass XCD-segmented (default) or not
+    monkeypatch.setenv("THRS_LOCAL", geom)  # local-sort geometry: 18432- or 9216-key chunks
     rs = make_sorter(kt, 0, desc)
     dists = {
         "uniform": lambda k: k,
@@ -202,12 +203,14 @@ def test_hybrid_paths_vs_oracle(gpu, kt, desc, seg, monkeypatch):
 
 
 @pytest.mark.parametrize("desc", [False, True])
-def test_hybrid_pairs_vs_oracle(gpu, desc, monkeypatch):
+@pytest.mark.parametrize("geom", ["big", "small"])
+def test_hybrid_pairs_vs_oracle(gpu, desc, geom, monkeypatch):
     """sortPairs with u32 keys + u32 values over the whole key takes the hybrid
     path (single-bucket chunks, positions carried in the local sort's items);
     stability on ties, the gated LSD fallback, and partial windows (plain LSD)."""
     torch = gpu
     monkeypatch.setenv("THRS_HYBRID", "1")  # forced for every size
+    monkeypatch.setenv("THRS_LOCAL", geom)
     rs = make_sorter(O.U32, 4, desc)
     dists = {
         "uniform": lambda k: k,

@@ -294,7 +294,15 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   // 2^30 + 2^26 the largest of 65536 uniform buckets (mean + ~4.5 sigma)
   // outgrows kLocCap and the fallback would pay for the bucket histogram in
   // vain.  THRS_HYBRID=1 forces the path for any n (tests), =0 turns it off.
-  const bool sizeOk = (uint64_t)n >= (3ull << 28) && (uint64_t)n <= (1ull << 30) + (1ull << 26);
+  // Two local-sort geometries (thrs_hybrid.hpp LocG): LocSmall (9216-key
+  // chunks, uniform buckets of 4-8K keys) for n in [2^28, 2^29], LocBig
+  // (18432) above, up to 2^30 + 2^26 (docs/EXPERIMENTS.md rows 29, 33).
+  const uint64_t nn = n;
+  const bool sizeOk = nn >= (1ull << 28) && nn <= (1ull << 30) + (1ull << 26);
+  const char* locEnv = getenv("THRS_LOCAL");  // big / small: force the geometry (tests)
+  const bool smallLocal = locEnv && !strcmp(locEnv, "small") ? true
+                          : locEnv && !strcmp(locEnv, "big") ? false
+                                                              : nn <= (1ull << 29);
   const bool hybrid = kHybridType && !counts && nPass >= 3 && (hyEnv == 1 || (hyEnv < 0 && sizeOk)) &&
                       (VB == 0 || fullWindow);
   const int nLow = nPass - 2;
@@ -318,7 +326,8 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                          static_cast<const U*>(keys), n, orderMask, startBits + 8 * nLow, vec, joint);
       // chunks: whole buckets; neighbouring buckets below kLocCap/2 keys share one
       hipLaunchKernelGGL(thrs_plan, dim3(1), dim3(kPlanThreads), 0, stream, joint, n, base + nLow * kBins, chunkOff,
-                         chunkB0, meta, kLocCap, VB ? -1 : kLocLogT,  // pairs: single-bucket chunks
+                         chunkB0, meta, smallLocal ? LocSmall::CAP : LocBig::CAP,
+                         VB ? -1 : (smallLocal ? kLocSmallLogT : kLocLogT),  // pairs: single-bucket chunks
                          reinterpret_cast<uint32_t*>(hyb + kSegInfoOff), reinterpret_cast<uint32_t*>(hyb + kSegBaseOff),
                          (uint32_t)G::TILE);
       // the low digits' histograms + bases: needed only on the fallback path
@@ -461,27 +470,33 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     }
     {
       ProfScope prof(stream, 2);
-      const size_t llds = local_lds_bytes<U>();
       // never more workgroups than chunks can exist: <= 256 (one per top digit)
       // + 2 per non-empty bucket, and <= the number of buckets
       const uint64_t maxChunks = std::min<uint64_t>(kBuckets, 256 + 2 * (uint64_t)n);
-      if constexpr (VB == 4) {
-        auto lk = atomicRank ? thrs_local_pairs<true> : thrs_local_pairs<false>;
-        if (allow_lds(lk, llds) != hipSuccess) return THRS_ERROR_HIP;
-        hipLaunchKernelGGL(lk, dim3((uint32_t)maxChunks), dim3(kLocThreads), llds, stream,
-                           reinterpret_cast<uint32_t*>(K), reinterpret_cast<uint32_t*>(V), (uint32_t)orderMask,
-                           chunkOff, chunkB0, meta);
-      } else {
-        auto lk = atomicRank ? thrs_local<KT, true> : thrs_local<KT, false>;
-        if (allow_lds(lk, llds) != hipSuccess) return THRS_ERROR_HIP;
-        int perCU = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, lk, kLocThreads, llds) != hipSuccess || perCU < 1)
-          perCU = 1;
-        const uint32_t lgrid = THRS_LOC_PERSIST ? (uint32_t)std::min<uint64_t>(maxChunks, (uint64_t)perCU * cu_count())
-                                                : (uint32_t)maxChunks;
-        hipLaunchKernelGGL(lk, dim3(lgrid), dim3(kLocThreads), llds, stream, K, orderMask, startBits, nLow, chunkOff,
-                           chunkB0, meta, g_lstamps);
-      }
+      auto launch_local = [&](auto geom) -> int {
+        using LG = decltype(geom);
+        const size_t llds = LG::template lds<U>();
+        if constexpr (VB == 4) {
+          auto lk = atomicRank ? thrs_local_pairs<true, LG> : thrs_local_pairs<false, LG>;
+          if (allow_lds(lk, llds) != hipSuccess) return THRS_ERROR_HIP;
+          hipLaunchKernelGGL(lk, dim3((uint32_t)maxChunks), dim3(LG::THREADS), llds, stream,
+                             reinterpret_cast<uint32_t*>(K), reinterpret_cast<uint32_t*>(V), (uint32_t)orderMask,
+                             chunkOff, chunkB0, meta);
+        } else {
+          auto lk = atomicRank ? thrs_local<KT, true, LG> : thrs_local<KT, false, LG>;
+          if (allow_lds(lk, llds) != hipSuccess) return THRS_ERROR_HIP;
+          int perCU = 0;
+          if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, lk, LG::THREADS, llds) != hipSuccess || perCU < 1)
+            perCU = 1;
+          const uint32_t lgrid = THRS_LOC_PERSIST ? (uint32_t)std::min<uint64_t>(maxChunks, (uint64_t)perCU * cu_count())
+                                                  : (uint32_t)maxChunks;
+          hipLaunchKernelGGL(lk, dim3(lgrid), dim3(LG::THREADS), llds, stream, K, orderMask, startBits, nLow,
+                             chunkOff, chunkB0, meta, g_lstamps);
+        }
+        return THRS_SUCCESS;
+      };
+      const int rc = smallLocal ? launch_local(LocSmall{}) : launch_local(LocBig{});
+      if (rc) return rc;
     }
     if (hipGetLastError() != hipSuccess) return THRS_ERROR_HIP;
   }
@@ -690,9 +705,9 @@ THRS_API uint64_t thrs_debug_tile_keys(int keyType, int valueBytes) {
 // kernel for 4-byte keys, as the runtime computes it from its LDS and VGPRs.
 THRS_API int thrs_debug_local_occupancy(void) {
   const size_t lds = local_lds_bytes<uint32_t>();
-  if (allow_lds(thrs_local<0, true>, lds) != hipSuccess) return -1;
+  if (allow_lds(thrs_local<0, true, LocBig>, lds) != hipSuccess) return -1;
   int perCU = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, thrs_local<0, true>, kLocThreads, lds) != hipSuccess)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, thrs_local<0, true, LocBig>, kLocThreads, lds) != hipSuccess)
     return -1;
   return perCU;
 }

@@ -343,19 +343,32 @@ __global__ __launch_bounds__(kPlanThreads) void thrs_plan(const uint32_t* __rest
 // real keys take slots [0, size) and no per-item predicate is needed between
 // the load and the final store.
 #ifndef THRS_LOC_CFG
-#define THRS_LOC_CFG 8, 36  // waves, keys per lane: 2 workgroups per CU
+#define THRS_LOC_CFG 8, 36  // waves, keys per lane of the large geometry: 2 workgroups per CU
 #endif
 constexpr int kLocCfg[2] = {THRS_LOC_CFG};
-constexpr int kLocWaves = kLocCfg[0], kLocThreads = 64 * kLocWaves, kLocKpt = kLocCfg[1];
-constexpr uint32_t kLocCap = (uint32_t)kLocThreads * kLocKpt;  // 18432 keys
-constexpr int kLocLogT = 12;  // chunking window T = 4096: buckets of a 2^29+ uniform sort never merge
-enum { kMetaClaim = 2 };
 #ifndef THRS_LOC_PERSIST
 #define THRS_LOC_PERSIST 0  // 1: persistent workgroups with next-chunk prefetch; 0: one workgroup per chunk
 #endif
-template <typename U> constexpr size_t local_lds_bytes() {
-  return (size_t)kLocCap * sizeof(U) + (size_t)kLocWaves * kBins * 4;
-}
+// Local-sort geometry: WAVES waves x KPT keys per lane = CAP slots per chunk.
+//   LocBig   8 x 36 = 18432 keys, 2 WGs / CU (72 KiB stage + 8 KiB counters):
+//            buckets of 2^30-key sorts (~16K keys)
+//   LocSmall 4 x 36 = 9216 keys, 4 WGs / CU (36 KiB + 4 KiB): buckets of
+//            2^27..2^29-key sorts, where a large chunk's fixed cost dominates
+template <int W, int K> struct LocG {
+  static constexpr int WAVES = W, KPT = K, THREADS = 64 * W;
+  static constexpr uint32_t CAP = (uint32_t)THREADS * K;
+  template <typename U> static constexpr size_t lds() { return (size_t)CAP * sizeof(U) + (size_t)W * kBins * 4; }
+};
+using LocBig = LocG<kLocCfg[0], kLocCfg[1]>;
+using LocSmall = LocG<4, 36>;
+constexpr int kLocWaves = LocBig::WAVES, kLocThreads = LocBig::THREADS, kLocKpt = LocBig::KPT;
+constexpr uint32_t kLocCap = LocBig::CAP;  // 18432 keys
+// chunking windows T = 2^logT (<= CAP/2): uniform buckets of the size range a
+// geometry serves never merge (a merged chunk's bucket round has few distinct
+// digits, i.e. same-address atomics)
+constexpr int kLocLogT = 12, kLocSmallLogT = 11;
+enum { kMetaClaim = 2 };
+template <typename U> constexpr size_t local_lds_bytes() { return LocBig::lds<U>(); }
 
 // raw 4-byte key whose getKeyBits image is y (inverse of KeyTraits::bits, for
 // images that do not come from -0)
@@ -390,16 +403,16 @@ __device__ __forceinline__ uint32_t loc_pad(uint32_t b0, int nLow, int startBits
   return unbits32<KT>(padT ^ orderMask);
 }
 
-template <int KT>
-__device__ __forceinline__ void loc_load(typename KeyTraits<KT>::U (&k)[kLocKpt],
+template <int KT, typename LG>
+__device__ __forceinline__ void loc_load(typename KeyTraits<KT>::U (&k)[LG::KPT],
                                          const typename KeyTraits<KT>::U* __restrict__ keys, const LocChunk& ch,
                                          uint32_t pad) {
   const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  int32_t lim = (int32_t)ch.size - (int32_t)(w * 64 * kLocKpt + lane);
+  int32_t lim = (int32_t)ch.size - (int32_t)(w * 64 * LG::KPT + lane);
   pin(reinterpret_cast<uint32_t&>(lim));
-  const typename KeyTraits<KT>::U* src = keys + ch.start + w * 64 * kLocKpt + lane;
+  const typename KeyTraits<KT>::U* src = keys + ch.start + w * 64 * LG::KPT + lane;
 #pragma unroll
-  for (int j = 0; j < kLocKpt; ++j) k[j] = (j * 64 < lim) ? src[j * 64] : pad;
+  for (int j = 0; j < LG::KPT; ++j) k[j] = (j * 64 < lim) ? src[j * 64] : pad;
 }
 
 // THRS_STAMPS builds: per chunk, s_memrealtime (100 MHz) at 0 entry, 1 keys
@@ -417,15 +430,15 @@ __device__ __forceinline__ void loc_stamp(uint64_t* st, int i) {
 
 // The LDS rounds of one chunk: on return (after a barrier) the stage holds
 // the chunk's items in sorted order; returns the number of rounds run.
-template <int KT, bool ATOMIC_RANK>
-__device__ __forceinline__ int loc_rounds(typename KeyTraits<KT>::U (&k)[kLocKpt], const LocChunk& ch,
+template <int KT, bool ATOMIC_RANK, typename LG>
+__device__ __forceinline__ int loc_rounds(typename KeyTraits<KT>::U (&k)[LG::KPT], const LocChunk& ch,
                                           typename KeyTraits<KT>::U orderMask, int startBits, int nLow,
                                           unsigned char* smem, uint64_t* st) {
   using U = typename KeyTraits<KT>::U;
-  constexpr int KPT = kLocKpt;
+  constexpr int KPT = LG::KPT;
   constexpr uint32_t CHUNK = 64 * KPT;
   U* stage = reinterpret_cast<U*>(smem);
-  uint32_t* s_cnt = reinterpret_cast<uint32_t*>(smem + (size_t)kLocCap * sizeof(U));  // [waves][256]
+  uint32_t* s_cnt = reinterpret_cast<uint32_t*>(smem + (size_t)LG::CAP * sizeof(U));  // [waves][256]
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6);
   uint32_t* cnt = s_cnt + w * kBins;
@@ -458,10 +471,10 @@ __device__ __forceinline__ int loc_rounds(typename KeyTraits<KT>::U (&k)[kLocKpt
        // (wave totals through stage words: the stage is free between the
        // reload and the scatter) -> per-wave running offsets
       uint32_t* s_wt = reinterpret_cast<uint32_t*>(stage);
-      uint32_t c[kLocWaves], tot = 0, inc = 0;
+      uint32_t c[LG::WAVES], tot = 0, inc = 0;
       if (tid < kBins) {
 #pragma unroll
-        for (int ww = 0; ww < kLocWaves; ++ww) {
+        for (int ww = 0; ww < LG::WAVES; ++ww) {
           c[ww] = s_cnt[ww * kBins + tid];
           tot += c[ww];
         }
@@ -473,7 +486,7 @@ __device__ __forceinline__ int loc_rounds(typename KeyTraits<KT>::U (&k)[kLocKpt
         const uint32_t w0 = s_wt[0], w1 = s_wt[1], w2 = s_wt[2];
         uint32_t run = inc - tot + (w > 0 ? w0 : 0u) + (w > 1 ? w1 : 0u) + (w > 2 ? w2 : 0u);
 #pragma unroll
-        for (int ww = 0; ww < kLocWaves; ++ww) {
+        for (int ww = 0; ww < LG::WAVES; ++ww) {
           s_cnt[ww * kBins + tid] = run;
           run += c[ww];
         }
@@ -524,15 +537,15 @@ __device__ __forceinline__ int loc_rounds(typename KeyTraits<KT>::U (&k)[kLocKpt
   return roundsRun;
 }
 
-template <int KT, bool ATOMIC_RANK>
-__device__ __forceinline__ void loc_sort_chunk(typename KeyTraits<KT>::U (&k)[kLocKpt],
+template <int KT, bool ATOMIC_RANK, typename LG>
+__device__ __forceinline__ void loc_sort_chunk(typename KeyTraits<KT>::U (&k)[LG::KPT],
                                                typename KeyTraits<KT>::U* __restrict__ keys, const LocChunk& ch,
                                                typename KeyTraits<KT>::U orderMask, int startBits, int nLow,
                                                unsigned char* smem, uint64_t* st = nullptr) {
   using U = typename KeyTraits<KT>::U;
-  constexpr int KPT = kLocKpt;
+  constexpr int KPT = LG::KPT;
   constexpr uint32_t CHUNK = 64 * KPT;
-  const int roundsRun = loc_rounds<KT, ATOMIC_RANK>(k, ch, orderMask, startBits, nLow, smem, st);
+  const int roundsRun = loc_rounds<KT, ATOMIC_RANK, LG>(k, ch, orderMask, startBits, nLow, smem, st);
   const U* stage = reinterpret_cast<const U*>(smem);
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -558,8 +571,8 @@ __device__ __forceinline__ void loc_sort_chunk(typename KeyTraits<KT>::U (&k)[kL
 #endif
 }
 
-template <int KT, bool ATOMIC_RANK>
-__global__ __launch_bounds__(kLocThreads) void thrs_local(typename KeyTraits<KT>::U* __restrict__ keys,
+template <int KT, bool ATOMIC_RANK, typename LG>
+__global__ __launch_bounds__(LG::THREADS) void thrs_local(typename KeyTraits<KT>::U* __restrict__ keys,
                                                           typename KeyTraits<KT>::U orderMask, int startBits,
                                                           int nLow, const uint32_t* __restrict__ chunkOff,
                                                           const uint32_t* __restrict__ chunkB0,
@@ -577,8 +590,8 @@ __global__ __launch_bounds__(kLocThreads) void thrs_local(typename KeyTraits<KT>
     loc_stamp(st, 0);
     const LocChunk ch = loc_chunk<KT>(c, nLow, chunkOff, chunkB0);
     if (ch.size == 0) return;
-    U k[kLocKpt];
-    loc_load<KT>(k, keys, ch, loc_pad<KT>(ch.b0, nLow, startBits, (uint32_t)orderMask));
+    U k[LG::KPT];
+    loc_load<KT, LG>(k, keys, ch, loc_pad<KT>(ch.b0, nLow, startBits, (uint32_t)orderMask));
 #ifdef THRS_STAMPS
     if (st) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -591,7 +604,7 @@ __global__ __launch_bounds__(kLocThreads) void thrs_local(typename KeyTraits<KT>
       }
     }
 #endif
-    loc_sort_chunk<KT, ATOMIC_RANK>(k, keys, ch, orderMask, startBits, nLow, smem, st);
+    loc_sort_chunk<KT, ATOMIC_RANK, LG>(k, keys, ch, orderMask, startBits, nLow, smem, st);
     return;
   }
 #endif
@@ -607,21 +620,21 @@ __global__ __launch_bounds__(kLocThreads) void thrs_local(typename KeyTraits<KT>
   uint32_t c = claim();
   if (c >= nChunks) return;
   LocChunk ch = loc_chunk<KT>(c, nLow, chunkOff, chunkB0);
-  U k[kLocKpt];
-  loc_load<KT>(k, keys, ch, loc_pad<KT>(ch.b0, nLow, startBits, (uint32_t)orderMask));
+  U k[LG::KPT];
+  loc_load<KT, LG>(k, keys, ch, loc_pad<KT>(ch.b0, nLow, startBits, (uint32_t)orderMask));
   for (;;) {
     const uint32_t cn = claim();
-    U kn[kLocKpt];
+    U kn[LG::KPT];
     LocChunk chn{};
     if (cn < nChunks) {  // next chunk's loads in flight during this chunk's LDS rounds
       chn = loc_chunk<KT>(cn, nLow, chunkOff, chunkB0);
-      loc_load<KT>(kn, keys, chn, loc_pad<KT>(chn.b0, nLow, startBits, (uint32_t)orderMask));
+      loc_load<KT, LG>(kn, keys, chn, loc_pad<KT>(chn.b0, nLow, startBits, (uint32_t)orderMask));
     }
-    if (ch.size) loc_sort_chunk<KT, ATOMIC_RANK>(k, keys, ch, orderMask, startBits, nLow, smem);
+    if (ch.size) loc_sort_chunk<KT, ATOMIC_RANK, LG>(k, keys, ch, orderMask, startBits, nLow, smem);
     if (cn >= nChunks) break;
     lds_barrier();  // every wave is past the write-out's stage reads
 #pragma unroll
-    for (int j = 0; j < kLocKpt; ++j) k[j] = kn[j];
+    for (int j = 0; j < LG::KPT; ++j) k[j] = kn[j];
     ch = chn;
   }
 }
@@ -639,11 +652,11 @@ __global__ __launch_bounds__(kLocThreads) void thrs_local(typename KeyTraits<KT>
 #ifndef THRS_PAIRS_EARLY_VALUES
 #define THRS_PAIRS_EARLY_VALUES 0  // 1: load the values with the keys (spills 36 VGPRs at 8x36)
 #endif
-template <bool ATOMIC_RANK>
-__global__ __launch_bounds__(kLocThreads) __attribute__((amdgpu_waves_per_eu(4))) void thrs_local_pairs(
+template <bool ATOMIC_RANK, typename LG>
+__global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(4))) void thrs_local_pairs(
     uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, uint32_t orderMask,
     const uint32_t* __restrict__ chunkOff, const uint32_t* __restrict__ chunkB0, const uint32_t* __restrict__ meta) {
-  constexpr int KPT = kLocKpt;
+  constexpr int KPT = LG::KPT;
   constexpr uint32_t CHUNK = 64 * KPT;
   if (meta[kMetaFallback] != 0) return;  // the plain LSD passes sorted everything
   const uint32_t c = blockIdx.x;
@@ -673,7 +686,7 @@ __global__ __launch_bounds__(kLocThreads) __attribute__((amdgpu_waves_per_eu(4))
 #pragma unroll
   for (int j = 0; j < KPT; ++j) vv[j] = (j * 64 < lim) ? vsrc[j * 64] : 0u;
 #endif
-  loc_rounds<0, ATOMIC_RANK>(it, ch, 0u, 16, 2, smem, nullptr);
+  loc_rounds<0, ATOMIC_RANK, LG>(it, ch, 0u, 16, 2, smem, nullptr);
   pin(reinterpret_cast<uint32_t&>(lim));
 #if THRS_PAIRS_EARLY_VALUES
 #pragma unroll
