@@ -197,21 +197,21 @@ __global__ __launch_bounds__(kPlanThreads) void thrs_plan(const uint32_t* __rest
       col[q] += x;
       rs += x;
       // bucket (top 16w + q4, second 64q + l): segment 2q + l/32, one half-wave each
-      uint32_t hs = x;
-#pragma unroll
-      for (int off = 16; off >= 1; off >>= 1) hs += __shfl_xor(hs, off, 64);
-      if ((lane & 31u) == 0) s_seg[2 * q + (lane >> 5)][16 * w + q4] = hs;
+      const uint32_t sc = wave_incl_scan(x, lane);
+      const uint32_t h0 = (uint32_t)__builtin_amdgcn_readlane((int)sc, 31), h1 = lane63(sc) - h0;
+      if (lane == 0) {
+        s_seg[2 * q][16 * w + q4] = h0;
+        s_seg[2 * q + 1][16 * w + q4] = h1;
+      }
     }
     tot += rs;
     // row 16w + q4: sum over the wave
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) rs += __shfl_xor(rs, off, 64);
+    rs = lane63(wave_incl_scan(rs, lane));
     if (lane == 0) s_row[16 * w + q4] = rs;
   }
 #pragma unroll
   for (int q = 0; q < 4; ++q) s_col[w][64 * q + lane] = col[q];
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) tot += __shfl_xor(tot, off, 64);
+  tot = lane63(wave_incl_scan(tot, lane));
   if (lane == 0) s_wsum[w] = tot;
   if (lane == 63) s_wlast[w] = src[64 * (STEPS - 1)];
   if (big) s_flag = 1;
@@ -285,8 +285,7 @@ __global__ __launch_bounds__(kPlanThreads) void thrs_plan(const uint32_t* __rest
       const uint32_t x = xb[q];
       const uint32_t inc = wave_incl_scan(x, lane);
       const uint32_t off = run + inc - x;
-      uint32_t prev = __shfl_up(x, 1, 64);
-      if (lane == 0) prev = prevTop;
+      const uint32_t prev = wave_prev_lane(x, prevTop);
       const uint32_t b = w * (64 * STEPS) + 64 * i + lane;
       const bool o = opens(b, off, x, prev);
       const uint64_t m = __ballot(o);
@@ -297,8 +296,8 @@ __global__ __launch_bounds__(kPlanThreads) void thrs_plan(const uint32_t* __rest
         chunkB0[c] = b;
       }
       nOpen += (uint32_t)__builtin_popcountll(m);
-      run += __shfl(inc, 63, 64);
-      prevTop = __shfl(x, 63, 64);
+      run += lane63(inc);
+      prevTop = lane63(x);
     }
     }
     return nOpen;

@@ -116,15 +116,26 @@ __device__ __forceinline__ void match_digit(uint32_t d, uint32_t& mlo, uint32_t&
   }
 }
 
-// Inclusive scan over the 64 lanes of a wave.
+// Inclusive scan over the 64 lanes of a wave, in DPP (no LDS round trips:
+// __shfl_up compiles to ds_bpermute, ~100+ cycles each): row_shr 1, 2, 4, 8
+// scan each row of 16 lanes, then row_bcast:15 / row_bcast:31 carry rows
+// 0 -> 1, 2 -> 3 and {0,1} -> {2,3}.  Lanes outside a DPP source keep 0.
+constexpr int kDppRowShr = 0x110, kDppRowBcast15 = 0x142, kDppRowBcast31 = 0x143, kDppWaveShr1 = 0x138;
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, uint32_t lane) {
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    uint32_t y = __shfl_up(x, off, 64);
-    if (lane >= (uint32_t)off) x += y;
-  }
+  (void)lane;
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, kDppRowShr | 1, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, kDppRowShr | 2, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, kDppRowShr | 4, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, kDppRowShr | 8, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, kDppRowBcast15, 0xa, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, kDppRowBcast31, 0xc, 0xf, false);
   return x;
 }
+// value of the previous lane (lane 0: `first`), in DPP
+__device__ __forceinline__ uint32_t wave_prev_lane(uint32_t x, uint32_t first) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)first, (int)x, kDppWaveShr1, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t lane63(uint32_t x) { return (uint32_t)__builtin_amdgcn_readlane((int)x, 63); }
 
 // Exclusive scan of one value per thread over a 256-thread block.
 // s_w: 4 words of LDS scratch.  Leaves *total = block sum.  Two barriers.
