@@ -159,25 +159,27 @@ def test_cpp_port_with_claim_mode_forced(gpu, xb):
 def test_cpp_port_with_hybrid_forced(gpu, hy):
     """The UTEST matrix with the 3-HBM-pass path (bucket passes + local LDS
     sort, thrs_hybrid.hpp) forced on for every size (THRS_HYBRID=1; by default
-    it runs for n in [0.75 * 2^30, 2^30 + 2^26]) and off (plain LSD passes)."""
+    it runs for n in [2^28, 2^30 + 2^26]) and off (plain LSD passes)."""
     exe = os.path.join(ROOT, "tests", "cpp", "unittest_thrs")
     env = dict(os.environ, THRS_HYBRID=hy)
     r = subprocess.run([exe], capture_output=True, text=True, timeout=900, env=env)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
 
 
-@pytest.mark.parametrize("geom,seg", [("big", "1"), ("small", "1"), ("big", "0")])
+@pytest.mark.parametrize("geom,seg", [("big", "1"), ("small", "1"), ("big", "0"), ("big", "top")])
 @pytest.mark.parametrize("kt", [O.U32, O.F32])
 @pytest.mark.parametrize("desc", [False, True])
 def test_hybrid_paths_vs_oracle(gpu, kt, desc, geom, seg, monkeypatch):
     """4-byte keys-only sorts with >= 3 digits take the hybrid path (forced
-    here for every size; by default it runs for n in [0.75*2^30, 2^30 + 2^26]): chunked
+    here for every size; by default it runs for n in [2^28, 2^30 + 2^26]): chunked
     local sort (single- and multi-bucket chunks), and the gated fallback to
     plain LSD when one bucket exceeds the local capacity (18432 keys) --
     including an odd number of low passes (window of 3 digits: gated copy)."""
     torch = gpu
     monkeypatch.setenv("THRS_HYBRID", "1")
-    monkeypatch.setenv("THRS_SEG", seg)  # top-digit pass XCD-segmented (default) or not
+    # the two top-digit passes XCD-segmented (default), neither, or the top one only
+    monkeypatch.setenv("THRS_SEG", "0" if seg == "0" else "1")
+    monkeypatch.setenv("THRS_SEGA", "1" if seg == "1" else "0")
     monkeypatch.setenv("THRS_LOCAL", geom)  # local-sort geometry: 18432- or 9216-key chunks
     rs = make_sorter(kt, 0, desc)
     dists = {

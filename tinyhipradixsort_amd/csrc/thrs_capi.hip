@@ -82,14 +82,19 @@ struct Plan {
   uint64_t scratchBytes;  // header + 2 sets (ping-pong between passes) + 8 claim areas + hybrid area
 };
 
-// hybrid area: u32 joint[65536] | chunkOff[65537] | chunkB0[65537] | meta[4]
+// hybrid area: u32 joint[65536] | segHistA[8][256] | chunkOff[65537] |
+// chunkB0[65537] | meta[4] | segment tables of the two top-digit passes
 constexpr uint64_t kJointBytes = kBuckets * 4;
-constexpr uint64_t kChunkOffOff = kJointBytes;
+constexpr uint64_t kSegHistAOff = kJointBytes;         // zeroed with joint
+constexpr uint64_t kJointZero = kJointBytes + kSegs * 256 * 4;
+constexpr uint64_t kChunkOffOff = kJointZero;
 constexpr uint64_t kChunkB0Off = kChunkOffOff + round_up_c((kBuckets + 1) * 4, 256);
 constexpr uint64_t kMetaOff = kChunkB0Off + round_up_c((kBuckets + 1) * 4, 256);
 constexpr uint64_t kSegInfoOff = kMetaOff + 256;      // segPos[9] | segTiles[9] ... tickets[8] at +256 B (thrs_pass_seg)
 constexpr uint64_t kSegBaseOff = kSegInfoOff + 512;   // u32 [8][256] per-segment top-digit bases
-constexpr uint64_t kHybridBytes = kSegBaseOff + kSegs * 256 * 4;
+constexpr uint64_t kSegInfoAOff = kSegBaseOff + kSegs * 256 * 4;  // the same two for the second-digit pass
+constexpr uint64_t kSegBaseAOff = kSegInfoAOff + 512;
+constexpr uint64_t kHybridBytes = kSegBaseAOff + kSegs * 256 * 4;
 // tile ids of the segmented pass: each of the 8 segments adds at most one
 // partial tile and rounds its id range up to a multiple of kGroup
 constexpr uint64_t kSegTilePad = kSegs * kGroup;
@@ -242,6 +247,10 @@ bool seg_enabled() {
   const char* e = getenv("THRS_SEG");
   return !(e && !strcmp(e, "0"));
 }
+bool seg_a_enabled() {  // THRS_SEGA=0: the second-digit pass unsegmented (tests, A/B)
+  const char* e = getenv("THRS_SEGA");
+  return !(e && !strcmp(e, "0"));
+}
 
 // One launch sequence.  Sort mode (counts == nullptr): the result lands in
 // keys/vals.  Partition mode (counts != nullptr, nPass == 1,
@@ -312,7 +321,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   // too, and zeroes its bucket histogram
   const uint64_t sets = (hybrid && (nLow & 1)) ? 2 : 1;
   if (hipMemsetAsync(scratch, 0, kHeaderBytes + sets * plan.setBytes, stream) != hipSuccess) return THRS_ERROR_HIP;
-  if (hybrid && hipMemsetAsync(joint, 0, kJointBytes, stream) != hipSuccess) return THRS_ERROR_HIP;
+  if (hybrid && hipMemsetAsync(joint, 0, kJointZero, stream) != hipSuccess) return THRS_ERROR_HIP;
   char* claim = scratch + kHeaderBytes + 2 * plan.setBytes;  // 8 per-pass claim areas
 
   {  // histograms of every pass in one read of the keys
@@ -323,13 +332,15 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     if (hybrid) {
       if (allow_lds(thrs_hist_joint<KT>, kJointLds) != hipSuccess) return THRS_ERROR_HIP;
       hipLaunchKernelGGL(thrs_hist_joint<KT>, dim3(grid), dim3(kHistThreads), kJointLds, stream,
-                         static_cast<const U*>(keys), n, orderMask, startBits + 8 * nLow, vec, joint);
+                         static_cast<const U*>(keys), n, orderMask, startBits + 8 * nLow, vec, joint,
+                         reinterpret_cast<uint32_t*>(hyb + kSegHistAOff));
       // chunks: whole buckets; neighbouring buckets below kLocCap/2 keys share one
       hipLaunchKernelGGL(thrs_plan, dim3(1), dim3(kPlanThreads), 0, stream, joint, n, base + nLow * kBins, chunkOff,
                          chunkB0, meta, smallLocal ? LocSmall::CAP : LocBig::CAP,
                          VB ? -1 : (smallLocal ? kLocSmallLogT : kLocLogT),  // pairs: single-bucket chunks
                          reinterpret_cast<uint32_t*>(hyb + kSegInfoOff), reinterpret_cast<uint32_t*>(hyb + kSegBaseOff),
-                         (uint32_t)G::TILE);
+                         (uint32_t)G::TILE, reinterpret_cast<const uint32_t*>(hyb + kSegHistAOff), (uint32_t)grid,
+                         reinterpret_cast<uint32_t*>(hyb + kSegInfoAOff), reinterpret_cast<uint32_t*>(hyb + kSegBaseAOff));
       // the low digits' histograms + bases: needed only on the fallback path
       const size_t lds = (size_t)nLow * kBins * hist_copies<(int)sizeof(U)>() * 4;
       if (allow_lds(thrs_hist<KT>, lds) != hipSuccess) return THRS_ERROR_HIP;
@@ -442,32 +453,48 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                              (uint64_t)n * VB / 4, meta + kMetaFallback, 1u);
       }
     }
-    launch_pass(nLow, K, keyOut, V, valOut, nullptr);
-    if (seg_enabled()) {
-      // top digit: XCD-segmented pass (thrs_kernels.hpp thrs_pass_seg).  Its
-      // tile ids reach past nTiles (per-segment rounding): clear those rows of
-      // its table set (pass nLow cleared rows [0, nTiles) for it).
-      const int p = nLow + 1, set = p & 1;
-      const uint64_t sw = plan.wideStatus ? 8 : 4;
+    // the two top digits: XCD-segmented passes (thrs_kernels.hpp
+    // thrs_pass_seg) -- the second digit over position segments (the bucket
+    // histogram's workgroup ranges), the top digit over second-digit ranges
+    auto sk = atomicRank ? thrs_pass_seg<KT, VB, ST, true> : thrs_pass_seg<KT, VB, ST, false>;
+    if (allow_lds(sk, lds) != hipSuccess) return THRS_ERROR_HIP;
+    int segPerCU = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&segPerCU, sk, G::THREADS, lds) != hipSuccess || segPerCU < 1)
+      segPerCU = 1;
+    auto launch_seg = [&](int p, U* kin, U* kout, VW* vin, VW* vout, uint64_t infoOff, uint64_t baseOff,
+                          const uint32_t* gate, uint32_t want) {
+      ProfScope prof(stream, 1);
+      hipLaunchKernelGGL(sk, dim3((uint32_t)segPerCU * cu_count()), dim3(G::THREADS), lds, stream, kin, kout, vin,
+                         vout, orderMask, startBits + 8 * p, reinterpret_cast<uint32_t*>(hyb + infoOff),
+                         reinterpret_cast<const uint32_t*>(hyb + baseOff), status[p & 1], err, grp[p & 1], gate, want);
+    };
+    const uint64_t sw = plan.wideStatus ? 8 : 4;
+    const int setB = (nLow + 1) & 1;
+    if (seg_a_enabled()) {
+      // The position segments' digit counts are those of the INPUT order:
+      // after the fallback's low passes the plain pass runs instead (both
+      // gated on the flag).  The table set is clean either way: zeroed up
+      // front, or rows [0, nTiles) cleared by the last fallback pass.  Neither
+      // clears rows for the top-digit pass: zero that set.
+      launch_seg(nLow, K, keyOut, V, valOut, kSegInfoAOff, kSegBaseAOff, meta + kMetaFallback, 0u);
+      launch_pass(nLow, K, keyOut, V, valOut, meta + kMetaFallback);
+      if (hipMemsetAsync(status[setB], 0, plan.setBytes, stream) != hipSuccess) return THRS_ERROR_HIP;
+    } else {
+      launch_pass(nLow, K, keyOut, V, valOut, nullptr);
+      // the segmented pass's tile ids reach past nTiles (per-segment
+      // rounding): clear those rows (pass nLow cleared rows [0, nTiles))
       const uint64_t nGroups0 = (plan.nTiles + kGroup - 1) / kGroup;
-      if (hipMemsetAsync(reinterpret_cast<char*>(status[set]) + plan.nTiles * kBins * sw, 0,
+      if (hipMemsetAsync(reinterpret_cast<char*>(status[setB]) + plan.nTiles * kBins * sw, 0,
                          kSegTilePad * kBins * sw, stream) != hipSuccess ||
-          hipMemsetAsync(grp[set].ga + nGroups0 * kBins, 0, (kSegs + 1) * kBins * 4, stream) != hipSuccess ||
-          hipMemsetAsync(reinterpret_cast<char*>(grp[set].gp) + nGroups0 * kBins * sw, 0, (kSegs + 1) * kBins * sw,
+          hipMemsetAsync(grp[setB].ga + nGroups0 * kBins, 0, (kSegs + 1) * kBins * 4, stream) != hipSuccess ||
+          hipMemsetAsync(reinterpret_cast<char*>(grp[setB].gp) + nGroups0 * kBins * sw, 0, (kSegs + 1) * kBins * sw,
                          stream) != hipSuccess)
         return THRS_ERROR_HIP;
-      auto sk = atomicRank ? thrs_pass_seg<KT, VB, ST, true> : thrs_pass_seg<KT, VB, ST, false>;
-      if (allow_lds(sk, lds) != hipSuccess) return THRS_ERROR_HIP;
-      int perCU = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, sk, G::THREADS, lds) != hipSuccess || perCU < 1)
-        perCU = 1;
-      ProfScope prof(stream, 1);
-      hipLaunchKernelGGL(sk, dim3((uint32_t)perCU * cu_count()), dim3(G::THREADS), lds, stream, keyOut, K, valOut, V,
-                         orderMask, startBits + 8 * p, reinterpret_cast<uint32_t*>(hyb + kSegInfoOff),
-                         reinterpret_cast<const uint32_t*>(hyb + kSegBaseOff), status[set], err, grp[set]);
-    } else {
-      launch_pass(nLow + 1, keyOut, K, valOut, V, nullptr);
     }
+    if (seg_enabled())
+      launch_seg(nLow + 1, keyOut, K, valOut, V, kSegInfoOff, kSegBaseOff, nullptr, 0u);
+    else
+      launch_pass(nLow + 1, keyOut, K, valOut, V, nullptr);
     {
       ProfScope prof(stream, 2);
       // never more workgroups than chunks can exist: <= 256 (one per top digit)

@@ -45,18 +45,35 @@ enum { kMetaChunks = 0, kMetaFallback = 1 };
 // any skew is counted exactly.  (The two top digits' histograms are the row
 // and column sums of this one: thrs_plan.)
 constexpr uint32_t kJointWords = kBuckets / 2;
-constexpr size_t kJointLds = (size_t)kJointWords * 4;
+constexpr size_t kJointLds = (size_t)kJointWords * 4 + kBins * 4;  // + the range's second-digit counts
+
+// Workgroup i of the bucket histogram reads the contiguous key range
+// [i*len, (i+1)*len) (len a multiple of 4: 16-byte loads stay aligned), and
+// workgroups [ceil(sG/8), ceil((s+1)G/8)) make up position segment s of the
+// segmented second-digit pass: their second-digit counts are segment s's.
+__device__ __forceinline__ uint64_t hj_len(uint32_t n, uint32_t G) {
+  return (((uint64_t)n + G - 1) / G + 3) & ~3ull;
+}
+__device__ __forceinline__ uint32_t hj_seg_pos(uint32_t n, uint32_t G, uint32_t s) {
+  const uint64_t first = ((uint64_t)s * G + kSegs - 1) / kSegs;
+  return (uint32_t)min((uint64_t)n, first * hj_len(n, G));
+}
 
 template <int KT>
 __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename KeyTraits<KT>::U* __restrict__ keys,
                                                                 uint32_t n, typename KeyTraits<KT>::U orderMask,
                                                                 int bucketShift, int vec,
-                                                                uint32_t* __restrict__ joint) {
+                                                                uint32_t* __restrict__ joint,
+                                                                uint32_t* __restrict__ segHist /* [8][256] */) {
   using U = typename KeyTraits<KT>::U;
   extern __shared__ __attribute__((aligned(16))) uint32_t s_joint[];
+  uint32_t* s_d2 = s_joint + kJointWords;
   const uint32_t tid = threadIdx.x;
-  for (uint32_t i = tid; i < kJointWords; i += kHistThreads) s_joint[i] = 0;
+  for (uint32_t i = tid; i < kJointWords + kBins; i += kHistThreads) s_joint[i] = 0;
   __syncthreads();
+  const uint64_t len = hj_len(n, gridDim.x);
+  const uint64_t lo = min((uint64_t)n, (uint64_t)blockIdx.x * len), hi = min((uint64_t)n, lo + len);
+  uint32_t* segH = segHist + (blockIdx.x * kSegs / gridDim.x) * kBins;
 
   auto bucket_of = [&](U k) -> uint32_t {
     return (uint32_t)((KeyTraits<KT>::bits(k) ^ orderMask) >> bucketShift) & 0xFFFFu;
@@ -70,18 +87,18 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
     if (((old >> sh) & 0x7FFFu) == 0x7FFFu) {  // this add set the guard bit
       __hip_atomic_fetch_sub(&s_joint[b >> 1], 0x8000u << sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       atomicAdd(&joint[b], 0x8000u);
+      atomicAdd(&segH[b & 255u], 0x8000u);
     }
   };
 
-  const uint64_t gstride = (uint64_t)gridDim.x * kHistThreads;
-  const uint64_t gtid = (uint64_t)blockIdx.x * kHistThreads + tid;
-  uint64_t tailStart = 0;
+  constexpr uint64_t gstride = kHistThreads;  // the workgroup's own range
+  uint64_t tailStart = lo;
   if (vec) {  // 16-byte loads, 4 in flight per lane (keys base 16-B aligned, checked on host)
     constexpr int PER = 16 / sizeof(U);
     constexpr int UN = 4;
-    const uint64_t nv = n / PER;
+    const uint64_t nv = hi / PER;
     const uint4* kv = reinterpret_cast<const uint4*>(keys);
-    uint64_t i = gtid;
+    uint64_t i = lo / PER + tid;
     for (; i + (UN - 1) * gstride < nv; i += UN * gstride) {
       uint4 q[UN];
 #pragma unroll
@@ -116,9 +133,9 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
 #pragma unroll
       for (int e = 0; e < PER; ++e) check(b[e], add(b[e]));
     }
-    tailStart = nv * PER;
+    tailStart = max(lo, nv * PER);
   }
-  for (uint64_t i = tailStart + gtid; i < n; i += gstride) {
+  for (uint64_t i = tailStart + tid; i < hi; i += gstride) {
     const uint32_t b = bucket_of(keys[i]);
     check(b, add(b));
   }
@@ -127,6 +144,20 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
     const uint32_t c = (s_joint[i >> 1] >> ((i & 1u) << 4)) & 0xFFFFu;
     if (c) atomicAdd(&joint[i], c);
   }
+  // the range's second-digit counts (column sums; lanes d, d+1 share a word)
+  static_assert(kHistThreads == 4 * kBins, "four top-digit quarters per second digit");
+  {
+    const uint32_t d = tid & (kBins - 1), top0 = (tid >> 8) * 64;
+    uint32_t c = 0;
+#pragma unroll 8
+    for (uint32_t t = top0; t < top0 + 64; ++t) {
+      const uint32_t b = t * kBins + d;
+      c += (s_joint[b >> 1] >> ((b & 1u) << 4)) & 0xFFFFu;
+    }
+    __hip_atomic_fetch_add(&s_d2[d], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  __syncthreads();
+  if (tid < kBins && s_d2[tid]) atomicAdd(&segH[tid], s_d2[tid]);
 }
 
 // ------------------------------------------------------------------- plan
@@ -161,7 +192,10 @@ __global__ __launch_bounds__(kPlanThreads) void thrs_plan(const uint32_t* __rest
                                                           uint32_t* __restrict__ chunkOff,
                                                           uint32_t* __restrict__ chunkB0, uint32_t* __restrict__ meta,
                                                           uint32_t cap, int logT, uint32_t* __restrict__ segInfo,
-                                                          uint32_t* __restrict__ segBase, uint32_t tileKeys) {
+                                                          uint32_t* __restrict__ segBase, uint32_t tileKeys,
+                                                          const uint32_t* __restrict__ segHistA, uint32_t histGrid,
+                                                          uint32_t* __restrict__ segInfoA,
+                                                          uint32_t* __restrict__ segBaseA) {
   // Wave w owns buckets [4096w, 4096w + 4096); in step i (0..63) lane l holds
   // bucket 4096w + 64i + l, so every load and every chunk-table store is
   // lane-consecutive; prefixes in bucket order come from wave scans.
@@ -246,6 +280,12 @@ __global__ __launch_bounds__(kPlanThreads) void thrs_plan(const uint32_t* __rest
       baseTop[tid] = p0 + i0 - x0;
       baseTop[kBins + tid] = p1 + i1 - x1;
       s_b2[tid] = p0 + i0 - x0;
+      // segment bases of the second digit (position segments: thrs_hist_joint's ranges)
+      uint32_t sa = p0 + i0 - x0;
+      for (int sg = 0; sg < kSegs; ++sg) {
+        segBaseA[sg * kBins + tid] = sa;
+        sa += segHistA[sg * kBins + tid];
+      }
       // segment bases of the top digit: base + the top digit's keys in earlier segments
       uint32_t sb = p1 + i1 - x1;
       for (int sg = 0; sg < kSegs; ++sg) {
@@ -255,17 +295,26 @@ __global__ __launch_bounds__(kPlanThreads) void thrs_plan(const uint32_t* __rest
     }
   }
   __syncthreads();
-  if (tid == 0) {  // segment positions, first tile ids (multiples of kGroup), tickets
+  // segment positions, first tile ids (multiples of kGroup), tickets: thread 0
+  // for the top-digit pass (second-digit ranges), thread 64 for the
+  // second-digit pass (position ranges)
+  if (tid == 0 || tid == 64) {
+    const bool top = tid == 0;
+    uint32_t* info = top ? segInfo : segInfoA;
+    auto pos_of = [&](int sg) -> uint32_t {
+      if (sg >= kSegs) return n;
+      return top ? s_b2[32 * sg] : hj_seg_pos(n, histGrid, (uint32_t)sg);
+    };
     uint32_t tiles = 0;
     for (int sg = 0; sg <= kSegs; ++sg) {
-      const uint32_t pos = sg < kSegs ? s_b2[32 * sg] : n;
-      segInfo[sg] = pos;
-      segInfo[kSegs + 1 + sg] = tiles;
+      const uint32_t pos = pos_of(sg);
+      info[sg] = pos;
+      info[kSegs + 1 + sg] = tiles;
       if (sg < kSegs) {
-        const uint32_t len = (sg + 1 < kSegs ? s_b2[32 * (sg + 1)] : n) - pos;
+        const uint32_t len = pos_of(sg + 1) - pos;
         const uint32_t nT = (len + tileKeys - 1) / tileKeys;
         tiles += (nT + kGroup - 1) / kGroup * kGroup;
-        segInfo[64 + sg] = 0;  // ticket (own cache line)
+        info[64 + sg] = 0;  // ticket (own cache line)
       }
     }
   }

@@ -1163,11 +1163,12 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
     const typename ValueWord<VB>::T* __restrict__ valsIn, typename ValueWord<VB>::T* __restrict__ valsOut,
     typename KeyTraits<KT>::U orderMask, int shift, uint32_t* __restrict__ segInfo,
     const uint32_t* __restrict__ segBase, ST* __restrict__ status, uint32_t* __restrict__ errFlag,
-    GroupTables<ST> grp) {
+    GroupTables<ST> grp, const uint32_t* __restrict__ gate, uint32_t gateWant) {
   using U = typename KeyTraits<KT>::U;
   using VW = typename ValueWord<VB>::T;
   using G = PassGeom<sizeof(U), VB>;
   constexpr uint32_t T = G::TILE;
+  if (gate && *gate != gateWant) return;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint32_t* s_cnt = reinterpret_cast<uint32_t*>(smem + G::STAGE * (sizeof(U) + VB));
   uint32_t* s_misc = s_cnt + (G::WAVES + 1) * kBins;
