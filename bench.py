@@ -275,7 +275,9 @@ def main():
         achieved = alg_bytes / (avg_pass_ms / 1e3) / 1e9
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": load_pmc_traffic(wl),
-                "kernel": "thrs_pass", "avg_launch_ms": round(avg_pass_ms, 4),
+                # 3-HBM-pass path: the two top-digit passes are thrs_pass_seg
+                "kernel": "thrs_pass_seg" if prof.get("local_launches") else "thrs_pass",
+                "avg_launch_ms": round(avg_pass_ms, 4),
                 "alg_bytes_per_launch": alg_bytes,
                 "hist_avg_ms": round(prof["hist_ms"] / max(1, prof["hist_launches"]), 4)}
         # whole-sort algorithmic rate (B_alg = P*2*N*(K+V) for P 8-bit digits,

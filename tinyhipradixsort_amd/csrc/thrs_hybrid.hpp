@@ -44,6 +44,12 @@ enum { kMetaChunks = 0, kMetaFallback = 1 };
 // to the global count, so no carry ever reaches the neighbouring field and
 // any skew is counted exactly.  (The two top digits' histograms are the row
 // and column sums of this one: thrs_plan.)
+#ifndef THRS_HJ_UN
+#define THRS_HJ_UN 4  // 16-byte loads in flight per lane
+#endif
+#ifndef THRS_HJ_NORTN
+#define THRS_HJ_NORTN 0
+#endif
 constexpr uint32_t kJointWords = kBuckets / 2;
 constexpr size_t kJointLds = (size_t)kJointWords * 4 + kBins * 4;  // + the range's second-digit counts
 
@@ -79,6 +85,10 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
     return (uint32_t)((KeyTraits<KT>::bits(k) ^ orderMask) >> bucketShift) & 0xFFFFu;
   };
   auto add = [&](uint32_t b) -> uint32_t {
+#if THRS_HJ_NORTN  // EXPERIMENT: no-return LDS atomics, no overflow check (exact only below 32768 per bin and WG)
+    __hip_atomic_fetch_add(&s_joint[b >> 1], 1u << ((b & 1u) << 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return 0u;
+#endif
     return __hip_atomic_fetch_add(&s_joint[b >> 1], 1u << ((b & 1u) << 4), __ATOMIC_RELAXED,
                                   __HIP_MEMORY_SCOPE_WORKGROUP);
   };
@@ -95,7 +105,7 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
   uint64_t tailStart = lo;
   if (vec) {  // 16-byte loads, 4 in flight per lane (keys base 16-B aligned, checked on host)
     constexpr int PER = 16 / sizeof(U);
-    constexpr int UN = 4;
+    constexpr int UN = THRS_HJ_UN;
     const uint64_t nv = hi / PER;
     const uint4* kv = reinterpret_cast<const uint4*>(keys);
     uint64_t i = lo / PER + tid;
@@ -143,6 +153,12 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
   for (uint32_t i = tid; i < kBuckets; i += kHistThreads) {
     const uint32_t c = (s_joint[i >> 1] >> ((i & 1u) << 4)) & 0xFFFFu;
     if (c) atomicAdd(&joint[i], c);
+#ifdef THRS_HJ_FLUSH3  // EXPERIMENT: two more flushes (net zero) to price the flush
+    if (c) {
+      atomicAdd(&joint[i], c);
+      atomicSub(&joint[i], c);
+    }
+#endif
   }
   // the range's second-digit counts (column sums; lanes d, d+1 share a word)
   static_assert(kHistThreads == 4 * kBins, "four top-digit quarters per second digit");
