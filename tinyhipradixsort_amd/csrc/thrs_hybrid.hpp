@@ -44,6 +44,9 @@ enum { kMetaChunks = 0, kMetaFallback = 1 };
 // to the global count, so no carry ever reaches the neighbouring field and
 // any skew is counted exactly.  (The two top digits' histograms are the row
 // and column sums of this one: thrs_plan.)
+#ifndef THRS_LOC_RANKFIRST
+#define THRS_LOC_RANKFIRST 0  // EXPERIMENT: rank into zeroed counters, no counting pass (slower: EXPERIMENTS.md row 38)
+#endif
 #ifndef THRS_HJ_UN
 #define THRS_HJ_UN 4  // 16-byte loads in flight per lane
 #endif
@@ -526,10 +529,39 @@ __device__ __forceinline__ int loc_rounds(typename KeyTraits<KT>::U (&k)[LG::KPT
     };
 #pragma unroll
     for (int i = 0; i < kBins / 64; ++i) cnt[i * 64 + lane] = 0;
+#if THRS_LOC_RANKFIRST
+    // rank first, into the wave's zeroed counters (lane-ordered atomics:
+    // items in (j, lane) order = chunk order); the counters then hold the
+    // wave's digit counts, the scan turns them into the wave's digit offsets,
+    // and the scatter adds offset and rank -- a broadcast-friendly read per
+    // key instead of a separate counting atomic
+    constexpr int NP = (KPT + 1) / 2;
+    uint32_t rk[NP];  // two 16-bit ranks per register (ranks < 64 * KPT)
+#pragma unroll
+    for (int q = 0; q < NP; ++q) rk[q] = 0;
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) {
+      if (j * 64 < limw) {
+        const uint32_t dj = digit_of(k[j]);
+        uint32_t x;
+        if constexpr (ATOMIC_RANK) {
+          x = __hip_atomic_fetch_add(&cnt[dj], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else {
+          uint32_t mlo, mhi;
+          match_digit(dj, mlo, mhi);
+          const uint32_t cc = cnt[dj];
+          x = __builtin_amdgcn_mbcnt_hi(mhi, __builtin_amdgcn_mbcnt_lo(mlo, cc));
+          cnt[dj] = __builtin_popcount(mhi) + __builtin_popcount(mlo) + cc;
+        }
+        rk[j >> 1] |= x << ((j & 1) * 16);
+      }
+    }
+#else
 #pragma unroll
     for (int j = 0; j < KPT; ++j)
       if (j * 64 < limw)
         __hip_atomic_fetch_add(&cnt[digit_of(k[j])], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
     lds_barrier();
     {  // threads d < 256: digit d's total over the waves -> block exclusive scan
        // (wave totals through stage words: the stage is free between the
@@ -566,6 +598,21 @@ __device__ __forceinline__ int loc_rounds(typename KeyTraits<KT>::U (&k)[LG::KPT
 #define THRS_LOC_RB 12
 #endif
     constexpr int RB = THRS_LOC_RB;
+#if THRS_LOC_RANKFIRST
+#pragma unroll
+    for (int j0 = 0; j0 < KPT; j0 += RB) {
+      uint32_t sl[RB];
+#pragma unroll
+      for (int jj = 0; jj < RB; ++jj) {
+        const int j = j0 + jj;
+        if (j < KPT && j * 64 < limw) sl[jj] = cnt[digit_of(k[j])] + ((rk[j >> 1] >> ((j & 1) * 16)) & 0xFFFFu);
+      }
+#pragma unroll
+      for (int jj = 0; jj < RB; ++jj)
+        if (j0 + jj < KPT && (j0 + jj) * 64 < limw) stage[sl[jj]] = k[j0 + jj];
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#else
 #pragma unroll
     for (int j0 = 0; j0 < KPT; j0 += RB) {
       uint32_t sl[RB];
@@ -590,6 +637,7 @@ __device__ __forceinline__ int loc_rounds(typename KeyTraits<KT>::U (&k)[LG::KPT
         if (j0 + jj < KPT && (j0 + jj) * 64 < limw) stage[sl[jj]] = k[j0 + jj];
       __builtin_amdgcn_sched_barrier(0);
     }
+#endif
     lds_barrier();
     loc_stamp(st, 2 + (r & 1));
     if (r + 1 < roundsRun) {
