@@ -3,7 +3,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
-OUT=gpurun_out/pmc_lds_${1:-c2}
+OUT=gpurun_out/pmc_lds_${1:-c2}${TAG:-}
 mkdir -p $OUT
 timeout -s KILL 120 rocprofv3 --pmc ${PMC:-SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_LDS} --kernel-trace --output-format csv -d $OUT -o run -- python3 scripts/profile_run.py --workload ${1:-c2} --steps 2 > $OUT/log.txt 2>&1 || { tail -5 $OUT/log.txt; exit 1; }
 python3 - $OUT <<'PY'

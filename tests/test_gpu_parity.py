@@ -166,7 +166,7 @@ def test_cpp_port_with_hybrid_forced(gpu, hy):
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
 
 
-@pytest.mark.parametrize("geom,seg", [("big", "1"), ("small", "1"), ("big", "0"), ("big", "top")])
+@pytest.mark.parametrize("geom,seg", [("big", "1"), ("small", "1"), ("big", "0"), ("big", "top"), ("big32", "1")])
 @pytest.mark.parametrize("kt", [O.U32, O.F32])
 @pytest.mark.parametrize("desc", [False, True])
 def test_hybrid_paths_vs_oracle(gpu, kt, desc, geom, seg, monkeypatch):
@@ -180,7 +180,10 @@ def test_hybrid_paths_vs_oracle(gpu, kt, desc, geom, seg, monkeypatch):
     # the two top-digit passes XCD-segmented (default), neither, or the top one only
     monkeypatch.setenv("THRS_SEG", "0" if seg == "0" else "1")
     monkeypatch.setenv("THRS_SEGA", "1" if seg == "1" else "0")
-    monkeypatch.setenv("THRS_LOCAL", geom)  # local-sort geometry: 18432- or 9216-key chunks
+    # local-sort geometry: 18432- or 9216-key chunks; u32 keys over the whole
+    # key sort 16-bit items in the big geometry unless THRS_LOC16=0 ("big32")
+    monkeypatch.setenv("THRS_LOCAL", "small" if geom == "small" else "big")
+    monkeypatch.setenv("THRS_LOC16", "0" if geom == "big32" else "1")
     rs = make_sorter(kt, 0, desc)
     dists = {
         "uniform": lambda k: k,

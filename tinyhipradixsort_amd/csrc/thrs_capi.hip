@@ -247,6 +247,10 @@ bool seg_enabled() {
   const char* e = getenv("THRS_SEG");
   return !(e && !strcmp(e, "0"));
 }
+bool loc16_enabled() {  // THRS_LOC16=0: u32 keys keep the 32-bit local sort (tests, A/B)
+  const char* e = getenv("THRS_LOC16");
+  return !(e && !strcmp(e, "0"));
+}
 bool seg_a_enabled() {  // THRS_SEGA=0: the second-digit pass unsegmented (tests, A/B)
   const char* e = getenv("THRS_SEGA");
   return !(e && !strcmp(e, "0"));
@@ -315,6 +319,9 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   const bool hybrid = kHybridType && !counts && nPass >= 3 && (hyEnv == 1 || (hyEnv < 0 && sizeOk)) &&
                       (VB == 0 || fullWindow);
   const int nLow = nPass - 2;
+  // u32 keys over the whole key, large chunks: the local sort on 16-bit items
+  // (thrs_hybrid.hpp thrs_local16) over single-bucket chunks
+  const bool local16 = hybrid && KT == 0 && VB == 0 && fullWindow && !smallLocal && loc16_enabled();
 
   // header (histograms, tile counters, error word) + first status table; the
   // hybrid path with an odd number of (skippable) low passes starts on set 1
@@ -337,7 +344,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
       // chunks: whole buckets; neighbouring buckets below kLocCap/2 keys share one
       hipLaunchKernelGGL(thrs_plan, dim3(1), dim3(kPlanThreads), 0, stream, joint, n, base + nLow * kBins, chunkOff,
                          chunkB0, meta, smallLocal ? LocSmall::CAP : LocBig::CAP,
-                         VB ? -1 : (smallLocal ? kLocSmallLogT : kLocLogT),  // pairs: single-bucket chunks
+                         (VB || local16) ? -1 : (smallLocal ? kLocSmallLogT : kLocLogT),  // -1: single-bucket chunks
                          reinterpret_cast<uint32_t*>(hyb + kSegInfoOff), reinterpret_cast<uint32_t*>(hyb + kSegBaseOff),
                          (uint32_t)G::TILE, reinterpret_cast<const uint32_t*>(hyb + kSegHistAOff), (uint32_t)grid,
                          reinterpret_cast<uint32_t*>(hyb + kSegInfoAOff), reinterpret_cast<uint32_t*>(hyb + kSegBaseAOff));
@@ -522,8 +529,19 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
         }
         return THRS_SUCCESS;
       };
-      const int rc = smallLocal ? launch_local(LocSmall{}) : launch_local(LocBig{});
-      if (rc) return rc;
+      if (local16) {
+        if constexpr (KT == 0 && VB == 0) {
+          auto lk = atomicRank ? thrs_local16<true, Loc16> : thrs_local16<false, Loc16>;
+          const char* padEnv = getenv("THRS_LOC16_LDS");  // EXPERIMENT: more LDS per workgroup (fewer per CU)
+          const size_t l16 = padEnv ? std::max<size_t>(Loc16::LDS, (size_t)atol(padEnv)) : Loc16::LDS;
+          if (allow_lds(lk, l16) != hipSuccess) return THRS_ERROR_HIP;
+          hipLaunchKernelGGL(lk, dim3((uint32_t)maxChunks), dim3(Loc16::THREADS), l16, stream,
+                             reinterpret_cast<uint32_t*>(K), (uint32_t)orderMask, chunkOff, chunkB0, meta);
+        }
+      } else {
+        const int rc = smallLocal ? launch_local(LocSmall{}) : launch_local(LocBig{});
+        if (rc) return rc;
+      }
     }
     if (hipGetLastError() != hipSuccess) return THRS_ERROR_HIP;
   }

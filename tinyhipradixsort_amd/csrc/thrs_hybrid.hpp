@@ -44,6 +44,9 @@ enum { kMetaChunks = 0, kMetaFallback = 1 };
 // to the global count, so no carry ever reaches the neighbouring field and
 // any skew is counted exactly.  (The two top digits' histograms are the row
 // and column sums of this one: thrs_plan.)
+#ifndef THRS_LOC_STORE_HOIST
+#define THRS_LOC_STORE_HOIST 1  // local sort write-out: all stage reads before the stores
+#endif
 #ifndef THRS_LOC_RANKFIRST
 #define THRS_LOC_RANKFIRST 0  // EXPERIMENT: rank into zeroed counters, no counting pass (slower: EXPERIMENTS.md row 38)
 #endif
@@ -470,16 +473,43 @@ __device__ __forceinline__ uint32_t loc_pad(uint32_t b0, int nLow, int startBits
   return unbits32<KT>(padT ^ orderMask);
 }
 
+// A wave's KPT coalesced loads of its run of a chunk, all issued before any
+// is waited for.  A load under a lane condition is waited for before the next
+// one issues, so there is none: when the wave's whole run lies inside the
+// array (`whole`, wave-uniform: past the chunk's end is harmless) the loads
+// are plain (one base address, immediate offsets); otherwise (the array's
+// last run) every index is clamped into the chunk.  Callers select per lane.
+template <int KPT, typename T>
+__device__ __forceinline__ void load_run(T (&r)[KPT], const T* __restrict__ chunk, uint32_t myOff, uint32_t size,
+                                         bool whole) {
+  if (whole) {
+    const T* p = chunk + myOff;
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) r[j] = p[j * 64];
+  } else {
+    const uint32_t last = size - 1;
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) r[j] = chunk[min(myOff + (uint32_t)(j * 64), last)];
+  }
+}
+
 template <int KT, typename LG>
 __device__ __forceinline__ void loc_load(typename KeyTraits<KT>::U (&k)[LG::KPT],
                                          const typename KeyTraits<KT>::U* __restrict__ keys, const LocChunk& ch,
-                                         uint32_t pad) {
+                                         uint32_t pad, uint32_t nTotal) {
   const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   int32_t lim = (int32_t)ch.size - (int32_t)(w * 64 * LG::KPT + lane);
   pin(reinterpret_cast<uint32_t&>(lim));
-  const typename KeyTraits<KT>::U* src = keys + ch.start + w * 64 * LG::KPT + lane;
+  if (ch.size == 0) {
 #pragma unroll
-  for (int j = 0; j < LG::KPT; ++j) k[j] = (j * 64 < lim) ? src[j * 64] : pad;
+    for (int j = 0; j < LG::KPT; ++j) k[j] = pad;
+    return;
+  }
+  const uint32_t wEnd = ch.start + (w + 1) * 64 * LG::KPT;
+  load_run<LG::KPT>(k, keys + ch.start, w * 64 * LG::KPT + lane, ch.size,
+                    __builtin_amdgcn_readfirstlane(wEnd <= nTotal && wEnd >= ch.start));
+#pragma unroll
+  for (int j = 0; j < LG::KPT; ++j) k[j] = (j * 64 < lim) ? k[j] : pad;
 }
 
 // THRS_STAMPS builds: per chunk, s_memrealtime (100 MHz) at 0 entry, 1 keys
@@ -671,9 +701,18 @@ __device__ __forceinline__ void loc_sort_chunk(typename KeyTraits<KT>::U (&k)[LG
       if (j * 64 < lim) src[j * 64] = k[j];
     return;
   }
+#if THRS_LOC_STORE_HOIST
+  U o[KPT];  // stage reads first, then the lane-conditional stores (see thrs_local16)
+#pragma unroll
+  for (int j = 0; j < KPT; ++j) o[j] = stw[j * 64];
+#pragma unroll
+  for (int j = 0; j < KPT; ++j)
+    if (j * 64 < lim) src[j * 64] = o[j];
+#else
 #pragma unroll
   for (int j = 0; j < KPT; ++j)
     if (j * 64 < lim) src[j * 64] = stw[j * 64];
+#endif
 #ifdef THRS_STAMPS
   loc_stamp(st, 4);
   if (st) {
@@ -693,6 +732,7 @@ __global__ __launch_bounds__(LG::THREADS) void thrs_local(typename KeyTraits<KT>
   static_assert(sizeof(U) == 4, "the local sort is for 4-byte keys");
   if (meta[kMetaFallback] != 0) return;  // the plain LSD passes sorted everything
   const uint32_t nChunks = meta[kMetaChunks];
+  const uint32_t nTotal = chunkOff[nChunks];  // = n
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 #if !THRS_LOC_PERSIST
   {
@@ -703,7 +743,7 @@ __global__ __launch_bounds__(LG::THREADS) void thrs_local(typename KeyTraits<KT>
     const LocChunk ch = loc_chunk<KT>(c, nLow, chunkOff, chunkB0);
     if (ch.size == 0) return;
     U k[LG::KPT];
-    loc_load<KT, LG>(k, keys, ch, loc_pad<KT>(ch.b0, nLow, startBits, (uint32_t)orderMask));
+    loc_load<KT, LG>(k, keys, ch, loc_pad<KT>(ch.b0, nLow, startBits, (uint32_t)orderMask), nTotal);
 #ifdef THRS_STAMPS
     if (st) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -733,14 +773,14 @@ __global__ __launch_bounds__(LG::THREADS) void thrs_local(typename KeyTraits<KT>
   if (c >= nChunks) return;
   LocChunk ch = loc_chunk<KT>(c, nLow, chunkOff, chunkB0);
   U k[LG::KPT];
-  loc_load<KT, LG>(k, keys, ch, loc_pad<KT>(ch.b0, nLow, startBits, (uint32_t)orderMask));
+  loc_load<KT, LG>(k, keys, ch, loc_pad<KT>(ch.b0, nLow, startBits, (uint32_t)orderMask), nTotal);
   for (;;) {
     const uint32_t cn = claim();
     U kn[LG::KPT];
     LocChunk chn{};
     if (cn < nChunks) {  // next chunk's loads in flight during this chunk's LDS rounds
       chn = loc_chunk<KT>(cn, nLow, chunkOff, chunkB0);
-      loc_load<KT, LG>(kn, keys, chn, loc_pad<KT>(chn.b0, nLow, startBits, (uint32_t)orderMask));
+      loc_load<KT, LG>(kn, keys, chn, loc_pad<KT>(chn.b0, nLow, startBits, (uint32_t)orderMask), nTotal);
     }
     if (ch.size) loc_sort_chunk<KT, ATOMIC_RANK, LG>(k, keys, ch, orderMask, startBits, nLow, smem);
     if (cn >= nChunks) break;
@@ -749,6 +789,145 @@ __global__ __launch_bounds__(LG::THREADS) void thrs_local(typename KeyTraits<KT>
     for (int j = 0; j < LG::KPT; ++j) k[j] = kn[j];
     ch = chn;
   }
+}
+
+// ------------------------------------------------- local sort, 16-bit items
+// u32 keys without values over the whole key (startBits 0, 32 bits), single-
+// bucket chunks (thrs_plan single mode): every key of a chunk is
+// (bucket << 16 | low16) in image space, so only its low 16 bits take part:
+// the LDS stage holds 2-byte items (36 KiB for 18432 keys instead of 72) and
+// registers hold two items each -- three workgroups per CU instead of two.
+// The rounds are those of loc_rounds (count, scan, lane-ordered rank,
+// scatter, reload) on 16-bit items; the keys are rebuilt on the way out.
+// u32 only: f32 keys' +0 and -0 share one image.
+template <int W, int K> struct Loc16G {
+  static constexpr int WAVES = W, KPT = K, THREADS = 64 * W, NP = (K + 1) / 2;
+  static constexpr uint32_t CAP = (uint32_t)THREADS * K;
+  static constexpr size_t LDS = (size_t)CAP * 2 + (size_t)W * kBins * 4;
+};
+using Loc16 = Loc16G<8, 36>;
+static_assert(Loc16::CAP == LocBig::CAP, "same chunk capacity as the 32-bit geometry (thrs_plan's cap)");
+
+template <bool ATOMIC_RANK, typename LG>
+__global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(6))) void thrs_local16(uint32_t* __restrict__ keys, uint32_t orderMask,
+                                                            const uint32_t* __restrict__ chunkOff,
+                                                            const uint32_t* __restrict__ chunkB0,
+                                                            const uint32_t* __restrict__ meta) {
+  constexpr int KPT = LG::KPT, NP = LG::NP;
+  constexpr uint32_t CHUNK = 64 * KPT;
+  if (meta[kMetaFallback] != 0) return;
+  const uint32_t c = blockIdx.x;
+  if (c >= meta[kMetaChunks]) return;
+  const uint32_t start = chunkOff[c], size = chunkOff[c + 1] - start;
+  if (size == 0) return;
+  const uint32_t hiBits = chunkB0[c] << 16;  // the bucket: the image's top 16 bits
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint16_t* stage = reinterpret_cast<uint16_t*>(smem);
+  uint32_t* s_cnt = reinterpret_cast<uint32_t*>(smem + (size_t)LG::CAP * 2);  // [waves][256]
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  uint32_t* cnt = s_cnt + w * kBins;
+  const uint16_t* stw = stage + w * CHUNK + lane;
+  int32_t lim = (int32_t)size - (int32_t)(w * CHUNK + lane);
+  pin(reinterpret_cast<uint32_t&>(lim));
+  const int32_t limw = __builtin_amdgcn_readfirstlane((int32_t)size - (int32_t)(w * CHUNK));
+  uint32_t* src = keys + start + w * CHUNK + lane;
+
+  // items: low 16 bits of the image, two per register; padding 0xFFFF ranks
+  // after every real item (stable: it sits at the chunk's end)
+  // (loads: load_run)
+  uint32_t it[NP];
+  {
+    const uint32_t wEnd = start + (w + 1) * CHUNK;
+    uint32_t raw[KPT];
+    load_run<KPT>(raw, keys + start, w * CHUNK + lane, size,
+                  __builtin_amdgcn_readfirstlane(wEnd <= chunkOff[meta[kMetaChunks]] && wEnd >= start));
+#pragma unroll
+    for (int j = 0; j < KPT; j += 2) {
+      const uint32_t a = (j * 64 < lim) ? ((raw[j] ^ orderMask) & 0xFFFFu) : 0xFFFFu;
+      const uint32_t b = (j + 1 < KPT && (j + 1) * 64 < lim) ? ((raw[j + 1] ^ orderMask) & 0xFFFFu) : 0xFFFFu;
+      it[j >> 1] = a | (b << 16);
+    }
+  }
+  auto item = [&](int j) -> uint32_t { return (it[j >> 1] >> ((j & 1) * 16)) & 0xFFFFu; };
+
+  for (int r = 0; r < 2; ++r) {
+    const int shift = 8 * r;
+    auto digit_of = [&](int j) -> uint32_t { return (it[j >> 1] >> ((j & 1) * 16 + shift)) & 0xFFu; };
+#pragma unroll
+    for (int i = 0; i < kBins / 64; ++i) cnt[i * 64 + lane] = 0;
+#pragma unroll
+    for (int j = 0; j < KPT; ++j)
+      if (j * 64 < limw)
+        __hip_atomic_fetch_add(&cnt[digit_of(j)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    lds_barrier();
+    {  // digit totals over the waves -> block exclusive scan -> per-wave running offsets
+      uint32_t* s_wt = reinterpret_cast<uint32_t*>(smem);  // stage words: free until the scatter
+      uint32_t cw[LG::WAVES], tot = 0, inc = 0;
+      if (tid < kBins) {
+#pragma unroll
+        for (int ww = 0; ww < LG::WAVES; ++ww) {
+          cw[ww] = s_cnt[ww * kBins + tid];
+          tot += cw[ww];
+        }
+        inc = wave_incl_scan(tot, lane);
+        if (lane == 63) s_wt[w] = inc;
+      }
+      lds_barrier();
+      if (tid < kBins) {
+        const uint32_t w0 = s_wt[0], w1 = s_wt[1], w2 = s_wt[2];
+        uint32_t run = inc - tot + (w > 0 ? w0 : 0u) + (w > 1 ? w1 : 0u) + (w > 2 ? w2 : 0u);
+#pragma unroll
+        for (int ww = 0; ww < LG::WAVES; ++ww) {
+          s_cnt[ww * kBins + tid] = run;
+          run += cw[ww];
+        }
+      }
+    }
+    lds_barrier();
+    constexpr int RB = THRS_LOC_RB;
+#pragma unroll
+    for (int j0 = 0; j0 < KPT; j0 += RB) {
+      uint32_t sl[RB];
+#pragma unroll
+      for (int jj = 0; jj < RB; ++jj) {
+        const int j = j0 + jj;
+        if (j < KPT && j * 64 < limw) {
+          const uint32_t dj = digit_of(j);
+          if constexpr (ATOMIC_RANK) {
+            sl[jj] = __hip_atomic_fetch_add(&cnt[dj], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          } else {
+            uint32_t mlo, mhi;
+            match_digit(dj, mlo, mhi);
+            const uint32_t cc = cnt[dj];
+            sl[jj] = __builtin_amdgcn_mbcnt_hi(mhi, __builtin_amdgcn_mbcnt_lo(mlo, cc));
+            cnt[dj] = __builtin_popcount(mhi) + __builtin_popcount(mlo) + cc;
+          }
+        }
+      }
+#pragma unroll
+      for (int jj = 0; jj < RB; ++jj)
+        if (j0 + jj < KPT && (j0 + jj) * 64 < limw) stage[sl[jj]] = (uint16_t)item(j0 + jj);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    lds_barrier();
+    if (r == 0) {
+#pragma unroll
+      for (int j = 0; j < KPT; j += 2) {
+        const uint32_t a = (j * 64 < limw) ? (uint32_t)stw[j * 64] : 0xFFFFu;
+        const uint32_t b = (j + 1 < KPT && (j + 1) * 64 < limw) ? (uint32_t)stw[(j + 1) * 64] : 0xFFFFu;
+        it[j >> 1] = a | (b << 16);
+      }
+    }
+  }
+  // every stage read first (in bounds for all lanes), then the lane-conditional
+  // stores: a read inside the condition would be waited for one at a time
+  uint32_t o[KPT];
+#pragma unroll
+  for (int j = 0; j < KPT; ++j) o[j] = stw[j * 64];
+#pragma unroll
+  for (int j = 0; j < KPT; ++j)
+    if (j * 64 < lim) src[j * 64] = (hiBits | o[j]) ^ orderMask;
 }
 
 // ------------------------------------------------------ local sort, pairs
@@ -772,7 +951,8 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(4))
   constexpr uint32_t CHUNK = 64 * KPT;
   if (meta[kMetaFallback] != 0) return;  // the plain LSD passes sorted everything
   const uint32_t c = blockIdx.x;
-  if (c >= meta[kMetaChunks]) return;
+  const uint32_t nChunks = meta[kMetaChunks];
+  if (c >= nChunks) return;
   LocChunk ch;
   ch.start = chunkOff[c];
   ch.size = chunkOff[c + 1] - ch.start;
@@ -787,11 +967,16 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(4))
   pin(reinterpret_cast<uint32_t&>(lim));
   uint32_t* ksrc = keys + ch.start + w * CHUNK + lane;
   uint32_t* vsrc = vals + ch.start + w * CHUNK + lane;
+  // loads unconditional and clamped into the chunk (see loc_load)
+  const uint32_t myOff = w * CHUNK + lane;
+  const uint32_t wEnd = ch.start + (w + 1) * CHUNK;
+  const bool whole = __builtin_amdgcn_readfirstlane(wEnd <= chunkOff[nChunks] && wEnd >= ch.start);
   uint32_t it[KPT];
+  load_run<KPT>(it, keys + ch.start, myOff, ch.size, whole);
 #pragma unroll
   for (int j = 0; j < KPT; ++j) {
-    const uint32_t pos = w * CHUNK + j * 64 + lane;
-    it[j] = (j * 64 < lim) ? (((ksrc[j * 64] ^ orderMask) << 16) | pos) : 0xFFFF0000u;  // padding: digits 255
+    const uint32_t pos = myOff + j * 64;
+    it[j] = (j * 64 < lim) ? (((it[j] ^ orderMask) << 16) | pos) : 0xFFFF0000u;  // padding: digits 255
   }
 #if THRS_PAIRS_EARLY_VALUES
   uint32_t vv[KPT];  // values in flight during the rounds
@@ -805,21 +990,28 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(4))
   for (int j = 0; j < KPT; ++j) it[j] = vv[j];
 #else
   // values of this thread's positions (the item registers are free again)
-#pragma unroll
-  for (int j = 0; j < KPT; ++j)
-    if (j * 64 < lim) it[j] = vsrc[j * 64];
+  load_run<KPT>(it, vals + ch.start, myOff, ch.size, whole);
 #endif
   uint32_t* stage = reinterpret_cast<uint32_t*>(smem);
   const uint32_t* stw = stage + w * CHUNK + lane;
   uint32_t id[(KPT + 1) / 2];  // carried positions, two 16-bit halves per register
 #pragma unroll
   for (int j = 0; j < (KPT + 1) / 2; ++j) id[j] = 0;
+  // sorted items read in batches (reads unconditional, stores lane-conditional)
+  constexpr int BR = 12;
 #pragma unroll
-  for (int j = 0; j < KPT; ++j) {
-    if (j * 64 < lim) {
-      const uint32_t item = stw[j * 64];
-      ksrc[j * 64] = (hiImg | (item >> 16)) ^ orderMask;
-      id[j / 2] |= (item & 0xFFFFu) << (16 * (j & 1));
+  for (int j0 = 0; j0 < KPT; j0 += BR) {
+    uint32_t o[BR];
+#pragma unroll
+    for (int jj = 0; jj < BR; ++jj)
+      if (j0 + jj < KPT) o[jj] = stw[(j0 + jj) * 64];
+#pragma unroll
+    for (int jj = 0; jj < BR; ++jj) {
+      const int j = j0 + jj;
+      if (j < KPT) {
+        id[j / 2] |= (j * 64 < lim ? (o[jj] & 0xFFFFu) : 0u) << (16 * (j & 1));
+        if (j * 64 < lim) ksrc[j * 64] = (hiImg | (o[jj] >> 16)) ^ orderMask;
+      }
     }
   }
   lds_barrier();  // every sorted item has been read: the stage takes the values
@@ -828,8 +1020,15 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(4))
     if (j * 64 < lim) stage[w * CHUNK + j * 64 + lane] = it[j];
   lds_barrier();
 #pragma unroll
-  for (int j = 0; j < KPT; ++j)
-    if (j * 64 < lim) vsrc[j * 64] = stage[(id[j / 2] >> (16 * (j & 1))) & 0xFFFFu];
+  for (int j0 = 0; j0 < KPT; j0 += BR) {
+    uint32_t o[BR];
+#pragma unroll
+    for (int jj = 0; jj < BR; ++jj)
+      if (j0 + jj < KPT) o[jj] = stage[(id[(j0 + jj) / 2] >> (16 * ((j0 + jj) & 1))) & 0xFFFFu];
+#pragma unroll
+    for (int jj = 0; jj < BR; ++jj)
+      if (j0 + jj < KPT && (j0 + jj) * 64 < lim) vsrc[(j0 + jj) * 64] = o[jj];
+  }
 }
 
 // Copy on the fallback path only (odd number of low passes: their result is
