@@ -290,7 +290,11 @@ def main():
             # the 3-HBM-pass path's local bucket sort: reads and writes every key once
             lm = prof["local_ms"] / prof["local_launches"]
             la = alg_bytes / (lm / 1e3) / 1e9
-            roof["local"] = {"kernel": "thrs_local", "avg_launch_ms": round(lm, 4), "achieved": round(la, 1),
+            # (u32 keys over the whole key above 2^29: 16-bit items; u32 pairs: items carry positions)
+            lk = ("thrs_local_pairs" if vb else
+                  "thrs_local16" if (kt == 0 and n > (1 << 29))
+                  else "thrs_local")
+            roof["local"] = {"kernel": lk, "avg_launch_ms": round(lm, 4), "achieved": round(la, 1),
                              "frac": round(la / PEAK_HBM_GBS, 4), "alg_bytes_per_launch": alg_bytes}
 
     cpu = None

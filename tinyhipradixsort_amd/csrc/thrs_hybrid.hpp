@@ -475,14 +475,17 @@ __device__ __forceinline__ uint32_t loc_pad(uint32_t b0, int nLow, int startBits
 
 // A wave's KPT coalesced loads of its run of a chunk, all issued before any
 // is waited for.  A load under a lane condition is waited for before the next
-// one issues, so there is none: when the wave's whole run lies inside the
-// array (`whole`, wave-uniform: past the chunk's end is harmless) the loads
-// are plain (one base address, immediate offsets); otherwise (the array's
-// last run) every index is clamped into the chunk.  Callers select per lane.
+// one issues, so there is none.  The wave-uniform `avail` = the chunk's keys
+// from the wave's first slot on: a whole run loads plainly (one base address,
+// immediate offsets); the chunk's partial run clamps every index into the
+// chunk (repeats of its last key: no extra HBM traffic); a wave past the
+// chunk's end loads nothing.  Callers select per lane (r[j] is garbage for
+// slots past the chunk).
 template <int KPT, typename T>
 __device__ __forceinline__ void load_run(T (&r)[KPT], const T* __restrict__ chunk, uint32_t myOff, uint32_t size,
-                                         bool whole) {
-  if (whole) {
+                                         int32_t avail) {
+  if (avail <= 0) return;
+  if (avail >= 64 * KPT) {
     const T* p = chunk + myOff;
 #pragma unroll
     for (int j = 0; j < KPT; ++j) r[j] = p[j * 64];
@@ -496,7 +499,7 @@ __device__ __forceinline__ void load_run(T (&r)[KPT], const T* __restrict__ chun
 template <int KT, typename LG>
 __device__ __forceinline__ void loc_load(typename KeyTraits<KT>::U (&k)[LG::KPT],
                                          const typename KeyTraits<KT>::U* __restrict__ keys, const LocChunk& ch,
-                                         uint32_t pad, uint32_t nTotal) {
+                                         uint32_t pad) {
   const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   int32_t lim = (int32_t)ch.size - (int32_t)(w * 64 * LG::KPT + lane);
   pin(reinterpret_cast<uint32_t&>(lim));
@@ -505,9 +508,8 @@ __device__ __forceinline__ void loc_load(typename KeyTraits<KT>::U (&k)[LG::KPT]
     for (int j = 0; j < LG::KPT; ++j) k[j] = pad;
     return;
   }
-  const uint32_t wEnd = ch.start + (w + 1) * 64 * LG::KPT;
   load_run<LG::KPT>(k, keys + ch.start, w * 64 * LG::KPT + lane, ch.size,
-                    __builtin_amdgcn_readfirstlane(wEnd <= nTotal && wEnd >= ch.start));
+                    __builtin_amdgcn_readfirstlane((int32_t)ch.size - (int32_t)(w * 64 * LG::KPT)));
 #pragma unroll
   for (int j = 0; j < LG::KPT; ++j) k[j] = (j * 64 < lim) ? k[j] : pad;
 }
@@ -732,7 +734,6 @@ __global__ __launch_bounds__(LG::THREADS) void thrs_local(typename KeyTraits<KT>
   static_assert(sizeof(U) == 4, "the local sort is for 4-byte keys");
   if (meta[kMetaFallback] != 0) return;  // the plain LSD passes sorted everything
   const uint32_t nChunks = meta[kMetaChunks];
-  const uint32_t nTotal = chunkOff[nChunks];  // = n
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 #if !THRS_LOC_PERSIST
   {
@@ -743,7 +744,7 @@ __global__ __launch_bounds__(LG::THREADS) void thrs_local(typename KeyTraits<KT>
     const LocChunk ch = loc_chunk<KT>(c, nLow, chunkOff, chunkB0);
     if (ch.size == 0) return;
     U k[LG::KPT];
-    loc_load<KT, LG>(k, keys, ch, loc_pad<KT>(ch.b0, nLow, startBits, (uint32_t)orderMask), nTotal);
+    loc_load<KT, LG>(k, keys, ch, loc_pad<KT>(ch.b0, nLow, startBits, (uint32_t)orderMask));
 #ifdef THRS_STAMPS
     if (st) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -773,14 +774,14 @@ __global__ __launch_bounds__(LG::THREADS) void thrs_local(typename KeyTraits<KT>
   if (c >= nChunks) return;
   LocChunk ch = loc_chunk<KT>(c, nLow, chunkOff, chunkB0);
   U k[LG::KPT];
-  loc_load<KT, LG>(k, keys, ch, loc_pad<KT>(ch.b0, nLow, startBits, (uint32_t)orderMask), nTotal);
+  loc_load<KT, LG>(k, keys, ch, loc_pad<KT>(ch.b0, nLow, startBits, (uint32_t)orderMask));
   for (;;) {
     const uint32_t cn = claim();
     U kn[LG::KPT];
     LocChunk chn{};
     if (cn < nChunks) {  // next chunk's loads in flight during this chunk's LDS rounds
       chn = loc_chunk<KT>(cn, nLow, chunkOff, chunkB0);
-      loc_load<KT, LG>(kn, keys, chn, loc_pad<KT>(chn.b0, nLow, startBits, (uint32_t)orderMask), nTotal);
+      loc_load<KT, LG>(kn, keys, chn, loc_pad<KT>(chn.b0, nLow, startBits, (uint32_t)orderMask));
     }
     if (ch.size) loc_sort_chunk<KT, ATOMIC_RANK, LG>(k, keys, ch, orderMask, startBits, nLow, smem);
     if (cn >= nChunks) break;
@@ -838,10 +839,8 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(6))
   // (loads: load_run)
   uint32_t it[NP];
   {
-    const uint32_t wEnd = start + (w + 1) * CHUNK;
     uint32_t raw[KPT];
-    load_run<KPT>(raw, keys + start, w * CHUNK + lane, size,
-                  __builtin_amdgcn_readfirstlane(wEnd <= chunkOff[meta[kMetaChunks]] && wEnd >= start));
+    load_run<KPT>(raw, keys + start, w * CHUNK + lane, size, limw);
 #pragma unroll
     for (int j = 0; j < KPT; j += 2) {
       const uint32_t a = (j * 64 < lim) ? ((raw[j] ^ orderMask) & 0xFFFFu) : 0xFFFFu;
@@ -969,10 +968,9 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(4))
   uint32_t* vsrc = vals + ch.start + w * CHUNK + lane;
   // loads unconditional and clamped into the chunk (see loc_load)
   const uint32_t myOff = w * CHUNK + lane;
-  const uint32_t wEnd = ch.start + (w + 1) * CHUNK;
-  const bool whole = __builtin_amdgcn_readfirstlane(wEnd <= chunkOff[nChunks] && wEnd >= ch.start);
+  const int32_t avail = __builtin_amdgcn_readfirstlane((int32_t)ch.size - (int32_t)(w * CHUNK));
   uint32_t it[KPT];
-  load_run<KPT>(it, keys + ch.start, myOff, ch.size, whole);
+  load_run<KPT>(it, keys + ch.start, myOff, ch.size, avail);
 #pragma unroll
   for (int j = 0; j < KPT; ++j) {
     const uint32_t pos = myOff + j * 64;
@@ -990,7 +988,7 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(4))
   for (int j = 0; j < KPT; ++j) it[j] = vv[j];
 #else
   // values of this thread's positions (the item registers are free again)
-  load_run<KPT>(it, vals + ch.start, myOff, ch.size, whole);
+  load_run<KPT>(it, vals + ch.start, myOff, ch.size, avail);
 #endif
   uint32_t* stage = reinterpret_cast<uint32_t*>(smem);
   const uint32_t* stw = stage + w * CHUNK + lane;
