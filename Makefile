@@ -6,10 +6,16 @@ HIPFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -fvisibility=hidden -Iin
 PKG := tinyhipradixsort_amd
 KSRC := $(PKG)/csrc/thrs_capi.hip $(PKG)/csrc/thrs_kernels.hpp $(PKG)/csrc/thrs_hybrid.hpp include/thrs/thrs_capi.h
 
-all: $(PKG)/libthrs.so $(PKG)/libthrs_testutil.so $(PKG)/libthrs_vendor.so tests/cpp/unittest_thrs examples/helloworld oracle
+all: $(PKG)/libthrs.so $(PKG)/libthrs_testutil.so $(PKG)/libthrs_vendor.so $(PKG)/libthrs_spin0.so \
+     tests/cpp/unittest_thrs examples/helloworld oracle
 
 $(PKG)/libthrs.so: $(KSRC)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(PKG)/csrc/thrs_capi.hip
+
+# fault-injection build for the error-path tests only: every look-back /
+# claim wait gives up at its first unpublished predecessor (THRS_SPIN_MAX=0)
+$(PKG)/libthrs_spin0.so: $(KSRC)
+	$(HIPCC) $(HIPFLAGS) -DTHRS_SPIN_MAX=0 -shared -o $@ $(PKG)/csrc/thrs_capi.hip
 
 $(PKG)/libthrs_testutil.so: $(PKG)/csrc/thrs_testutil.hip $(PKG)/csrc/thrs_kernels.hpp
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(PKG)/csrc/thrs_testutil.hip

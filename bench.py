@@ -7,7 +7,7 @@ metric: "Gkeys/s and achieved HBM GB/s (% of peak), u32 keys N=2^30, 1/2/4/8 GPU
   reference bench's input distribution (splitmix64 from state 0,
   unittest.cpp:544-548), generated on the GPU and resident in HBM before the
   timed region.  One step = one full sort of a FRESH input buffer (the sort is
-  in place, so every step gets its own pre-generated buffer; see --pool).  For
+  in place, so every timed step gets its own pre-generated buffer).  For
   4-byte keys-only sorts the library takes its 3-HBM-pass path: bucket
   histogram + plan, two device-wide passes for the top two digits, and one
   in-LDS local sort of every 16-bit bucket; other workloads run
@@ -39,11 +39,16 @@ PEAK_HBM_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level par
 METRIC = "Gkeys/s and achieved HBM GB/s (% of peak), u32 keys N=2^30, 1/2/4/8 GPU"
 
 WORKLOADS = {
-    # name: (key type, value bytes, n per GPU, description)
-    "c2": (0, 0, 1 << 30, "C2: sortKeys u32, N=2^30 uniform (splitmix64), bits [0,32), 1xMI355X"),
-    "c3": (0, 4, 1 << 30, "C3: sortPairs u32 key + u32 index payload (stable), N=2^30"),
-    "c4": (2, 0, 1 << 28, "C4: sortKeys f32 via fpKey transform, N=2^28 (bits & 0xFF7FFFFF)"),
-    "c5": (1, 8, 1 << 30, "C5: sortPairs u64 key + u64 index payload, 2^30 per GPU"),
+    # name: (key type, value bytes, n per GPU, key distribution, description)
+    "c2": (0, 0, 1 << 30, "uniform", "C2: sortKeys u32, N=2^30 uniform (splitmix64), bits [0,32), 1xMI355X"),
+    "c3": (0, 4, 1 << 30, "uniform", "C3: sortPairs u32 key + u32 index payload (stable), N=2^30"),
+    "c4": (2, 0, 1 << 28, "uniform", "C4: sortKeys f32 via fpKey transform, N=2^28 (bits & 0xFF7FFFFF)"),
+    "c5": (1, 8, 1 << 30, "uniform", "C5: sortPairs u64 key + u64 index payload, 2^30 per GPU"),
+    # low-entropy inputs of C2's shape (not bench lines of BASELINE.json: robustness)
+    "c2_sorted": (0, 0, 1 << 30, "sorted", "C2 shape, already-sorted input (stratified sorted uniform sample)"),
+    "c2_reverse": (0, 0, 1 << 30, "reverse", "C2 shape, reverse-sorted input"),
+    "c2_extreme": (0, 0, 1 << 30, "extreme", "C2 shape, extremeCase input: all zero but two keys (unittest.cpp:191-225)"),
+    "c2_fewuniq": (0, 0, 1 << 30, "fewuniq", "C2 shape, 16 distinct uniform keys"),
 }
 KEY_BYTES = {0: 4, 1: 8, 2: 4, 3: 8}
 DTYPE = {0: "u32", 1: "u64", 2: "f32", 3: "f64"}
@@ -56,7 +61,8 @@ def parse():
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--workload", default=None, choices=sorted(WORKLOADS))
     p.add_argument("--n", type=int, default=None, help="keys per GPU (default: the workload's)")
-    p.add_argument("--pool", type=int, default=12, help="max distinct pre-generated input buffers")
+    p.add_argument("--vendor", default="auto", choices=["auto", "off"],
+                   help="time hipcub::DeviceRadixSort on the same inputs (N=1 only)")
     p.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--quiet", action="store_true")
@@ -69,30 +75,117 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(n_target_s: float) -> dict:
-    """std::sort of u32 keys (unittest.cpp:156), 1 thread, on a bounded sample
-    of the same splitmix64 stream; the oracle library is the timer's subject."""
-    import numpy as np
-    from oracle import oracle as O
-    n = 1 << 24
-    keys = O.randomize_np(O.U32, O.splitmix64_stream(0, n))
-    t0 = time.perf_counter()
-    O.std_sort_keys(O.U32, keys)
-    t1 = time.perf_counter() - t0
-    # scale the sample so one sort takes ~ n_target_s / 4
-    scale = max(1, min(8, int((n_target_s / 4) / max(t1, 1e-3))))
-    n = n * (1 << (scale.bit_length() - 1))
-    keys = O.randomize_np(O.U32, O.splitmix64_stream(0, n))
+def _time_leg(fn, make, n_target_s: float, min_runs: int = 2, max_runs: int = 5):
+    """median seconds of fn(make()) over a few runs within ~n_target_s"""
     times = []
     t_start = time.perf_counter()
-    while len(times) < 3 or (time.perf_counter() - t_start < n_target_s and len(times) < 8):
+    while len(times) < min_runs or (time.perf_counter() - t_start < n_target_s and len(times) < max_runs):
+        a = make()
         t0 = time.perf_counter()
-        O.std_sort_keys(O.U32, keys)
+        fn(a)
         times.append(time.perf_counter() - t0)
-    med = statistics.median(times)
-    return {"value": round(n / med / 1e9, 5), "unit": "Gkeys/s", "cores": 1, "kind": "port",
-            "sample": f"std::sort (unittest.cpp:156) of {n} splitmix64 u32 keys, 1 thread, median of {len(times)} "
-                      f"runs on {os.cpu_count()} visible host CPUs ({cpu_model()})"}
+    return statistics.median(times), len(times)
+
+
+def cpu_baseline(kt: int, vb: int, n_target_s: float) -> dict:
+    """The reference's CPU paths on this host, on bounded samples of the same
+    splitmix64 stream (the oracle library is the timer's subject, never the
+    GPU result's source):
+      * std::sort, 1 thread (unittest.cpp:156) -- or std::stable_sort of pairs
+        (stableSortPairs, unittest.cpp:358-377) for sortPairs workloads;
+      * __gnu_parallel::sort / stable_sort on all of this process's CPU share,
+        standing in for concurrency::parallel_radixsort / parallel_sort
+        (unittest.cpp:563, 711; MSVC PPL is not on Linux).
+    `value` is the all-core leg (the stronger baseline); `legs` lists both."""
+    import numpy as np
+    from oracle import oracle as O
+    threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or (os.cpu_count() or 1)
+    os.environ["OMP_NUM_THREADS"] = str(threads)
+    kdt = O.KEY_DTYPE[kt]
+
+    def keys_of(n):
+        return O.randomize_np(kt, O.splitmix64_stream(0, n)).astype(kdt)
+
+    legs = []
+    per = n_target_s / 2
+    # 1 thread: 2^24 keys (std::sort) / 2^22 pairs (stable_sort of pairs)
+    if vb:
+        n1 = 1 << 22
+        ks = keys_of(n1)
+        vs = np.arange(n1, dtype={4: np.uint32, 8: np.uint64}.get(vb, np.uint64))
+        med, runs = _time_leg(lambda a: O.std_stable_sort_pairs(kt, a, vs), lambda: ks, per)
+        legs.append({"name": "std::stable_sort pairs (unittest.cpp:369)", "threads": 1, "n": n1,
+                     "value": round(n1 / med / 1e9, 5), "runs": runs})
+    else:
+        n1 = 1 << 24
+        ks = keys_of(n1)
+        med, runs = _time_leg(lambda a: O.std_sort_keys(kt, a), lambda: ks, per)
+        legs.append({"name": "std::sort (unittest.cpp:156)", "threads": 1, "n": n1,
+                     "value": round(n1 / med / 1e9, 5), "runs": runs})
+    # all cores: 2^26 keys / 2^24 pairs
+    nP = (1 << 24) if vb else (1 << 26)
+    ks = keys_of(nP)
+    if vb:
+        vs = np.arange(nP, dtype={4: np.uint32, 8: np.uint64}.get(vb, np.uint64))
+        med, runs = _time_leg(lambda a: O.parallel_stable_sort_pairs(kt, a, vs), lambda: ks, per)
+        name = "__gnu_parallel::stable_sort pairs (stand-in for PPL parallel sort)"
+    else:
+        med, runs = _time_leg(lambda a: O.parallel_sort(a, kt), lambda: ks, per)
+        name = "__gnu_parallel::sort (stand-in for PPL parallel_radixsort, unittest.cpp:563)"
+    legs.append({"name": name, "threads": threads, "n": nP, "value": round(nP / med / 1e9, 5), "runs": runs})
+    best = legs[-1]
+    return {"value": best["value"], "unit": "Gkeys/s", "cores": threads, "kind": "port",
+            "sample": f"{best['name']} of {best['n']} splitmix64 {DTYPE[kt]} keys, median of {best['runs']} runs, "
+                      f"{threads} threads ({cpu_model()}); 1-thread leg in `legs`",
+            "legs": legs}
+
+
+def vendor_bench(T, TU, kt, kb, vb, n, keys, vals, gen, stream, runs: int = 3):
+    """hipcub::DeviceRadixSort (rocPRIM) on the same inputs -- the MI355X
+    analogue of the reference's CUB comparator (cudaEnv.cu:95-116) and of
+    Oro::RadixSort (unittest.cpp:490-531).  Event-timed per run on fresh input
+    (regenerated outside the timing)."""
+    import ctypes
+    import torch
+    path = os.path.join(ROOT, "tinyhipradixsort_amd", "libthrs_vendor.so")
+    if not os.path.exists(path) or vb not in (0, kb):
+        return None
+    L = ctypes.CDLL(path)
+    L.thrsv_temp_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64)]
+    L.thrsv_sort.argtypes = [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 4 + [
+        ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_int), ctypes.c_void_p]
+    tb = ctypes.c_uint64()
+    if L.thrsv_temp_bytes(kb, vb, n, ctypes.byref(tb)) != 0:
+        return None
+    vtmp = torch.empty(max(1, tb.value), dtype=torch.uint8, device="cuda")
+    kalt = torch.empty(n * kb, dtype=torch.uint8, device="cuda")
+    valt = torch.empty(n * vb, dtype=torch.uint8, device="cuda") if vb else None
+    sel = ctypes.c_int()
+    times = []
+    for r in range(runs + 1):               # run 0 is a warm-up
+        j = r % len(keys)
+        gen(keys[j], j)
+        if vb:
+            TU.iota(vb, vals[j], n)
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        rc = L.thrsv_sort(kb, vb, keys[j].data_ptr(), kalt.data_ptr(), vals[j].data_ptr() if vb else None,
+                          valt.data_ptr() if vb else None, n, vtmp.data_ptr(), tb.value, ctypes.byref(sel),
+                          stream.cuda_stream)
+        b.record(stream)
+        torch.cuda.synchronize()
+        if rc != 0:
+            return None
+        if r:
+            times.append(a.elapsed_time(b))
+    ms = statistics.median(times)
+    out = keys[j] if sel.value == 0 else kalt
+    if TU.count_unsorted(kt, out, n, 0, kb * 8):
+        return None
+    return {"name": "hipcub::DeviceRadixSort::" + ("SortPairs" if vb else "SortKeys") + " (rocPRIM)",
+            "value": round(n / (ms / 1e3) / 1e9, 3), "unit": "Gkeys/s", "ms_per_sort": round(ms, 4),
+            "runs": runs, "inputs": "same generator, fresh per run"}
 
 
 def cpu_model() -> str:
@@ -106,12 +199,20 @@ def cpu_model() -> str:
 
 
 def load_pmc_traffic(workload: str):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3
+    --pmc run (profiles/pmc_traffic.json: which run, counters and gfx950
+    corrections are recorded there).  Not measured by this process: returned
+    with its source so the line says so."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         d = json.load(open(path))
-        return d.get(workload, {}).get("thrs_pass_bytes_per_launch")
+        e = d.get(workload, {})
+        v = e.get("thrs_pass_bytes_per_launch")
+        if v is None:
+            return None, None
+        return v, f"profiles/pmc_traffic.json[{workload}] from {e.get('source', '?')} (rocprofv3 --pmc, not this run)"
     except (OSError, ValueError):
-        return None
+        return None, None
 
 
 def main():
@@ -137,7 +238,8 @@ def main():
     from tinyhipradixsort_amd import testutil as TU
 
     wl = args.workload or "c2"
-    kt, vb, n_default, desc = WORKLOADS[wl]
+    kt, vb, n_default, dist_name, desc = WORKLOADS[wl]
+    dist_kind = dist_name
     n = args.n or n_default
     kb = KEY_BYTES[kt]
     steps, warmup = args.steps, args.warmup
@@ -154,52 +256,79 @@ def main():
         tdef = rs.getTemporaryBufferBytes(n)
         tmp_bytes = tdef.getTemporaryBufferBytesForSortPairs() if vb else tdef.getTemporaryBufferBytesForSortKeys()
         tmp = torch.empty(tmp_bytes, dtype=torch.uint8, device="cuda")
-        # distinct fresh inputs for every step (bounded by --pool and memory)
+        # Every TIMED step sorts its own fresh buffer (the reference draws a new
+        # stream per run, unittest.cpp:544-549): `steps` distinct buffers must
+        # fit in HBM, else fail loudly -- inputs are never recycled.
         free, _total = torch.cuda.mem_get_info()
         per = n * (kb + vb)
-        pool = max(1, min(args.pool, steps + warmup, int((free - tmp_bytes - (4 << 30)) // max(per, 1))))
+        fit = int((free - tmp_bytes - (6 << 30)) // max(per, 1))
+        if fit < steps:
+            raise SystemExit(f"bench: {steps} fresh inputs of {per / 2**30:.1f} GiB do not fit in HBM "
+                             f"(room for {fit}); use fewer --steps")
+        pool = steps
+
+        def gen(buf, i):        # run r consumes stream draws r*N+1 .. (r+1)*N
+            if dist_kind == "uniform":
+                TU.fill_keys(kt, buf, n, start=i * n)
+            else:
+                TU.fill_dist(kt, buf, n, dist_kind, start=i * n)
+
         keys, vals = [], []
         for i in range(pool):
             kbuf = torch.empty(n * kb, dtype=torch.uint8, device="cuda")
-            TU.fill_keys(kt, kbuf, n, start=i * n)      # run r consumes stream draws r*N+1 .. (r+1)*N
+            gen(kbuf, i)
             keys.append(kbuf)
             if vb:
                 vbuf = torch.empty(n * vb, dtype=torch.uint8, device="cuda")
                 TU.iota(vb, vbuf, n)
                 vals.append(vbuf)
+        keys_in0 = None
+        if vb:      # keep one input for the stability/gather check of the last step
+            keys_in0 = torch.empty(n * kb, dtype=torch.uint8, device="cuda")
+            keys_in0.copy_(keys[pool - 1])
         torch.cuda.synchronize()
 
-        def step(i):
-            j = i % pool
+        def step(j):
             if vb:
                 rs.sortPairs(keys[j], vals[j], n, tmp, 0, kb * 8, stream)
             else:
                 rs.sortKeys(keys[j], n, tmp, 0, kb * 8, stream)
 
+        # warm-up sorts buffers 0..W-1 (mod pool), which are then regenerated
+        # with the same draws, so the timed steps all see fresh input
         for i in range(warmup):
-            step(i)
-        # warm-up buffers get regenerated so every timed step sorts fresh data
+            step(i % pool)
         for i in range(min(warmup, pool)):
-            TU.fill_keys(kt, keys[i], n, start=(pool + i) * n)
+            gen(keys[i], i)
+            if vb:
+                TU.iota(vb, vals[i], n)
         torch.cuda.synchronize()
         T.profile_enable(True)
         barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for i in range(steps):
-            step(warmup + i)
+            step(i)
         torch.cuda.synchronize()
         barrier()
         t1 = time.perf_counter()
         prof = T.profile_read()
         T.profile_enable(False)
-        rs.checkDeviceError(tmp)
+        rs.checkDeviceError(tmp)      # raises on a look-back / claim timeout in any timed step
         # correctness of the last timed step (outside the timed region)
-        last = (warmup + steps - 1) % pool
+        last = steps - 1
         bad = TU.count_unsorted(kt, keys[last], n, 0, kb * 8)
         if bad:
             raise SystemExit(f"bench: output of the last step is not sorted ({bad} inversions)")
-        recycled = steps + warmup > pool
+        if vb:
+            chk = TU.check_pairs(kt, vb, keys_in0, keys[last], vals[last], n, 0, kb * 8)
+            if chk["gather_mismatch"] or chk["unstable"]:
+                raise SystemExit(f"bench: pairs output of the last step is wrong: {chk}")
+        vendor = None
+        if args.vendor == "auto" and world == 1:
+            del keys_in0
+            vendor = vendor_bench(T, TU, kt, kb, vb, n, keys, vals, gen, stream)
+        recycled = False
         elapsed = t1 - t0
         scaling = "weak"
         global_keys = n
@@ -212,7 +341,7 @@ def main():
         # inputs: rank r of step i holds draws (i*world + r)*n + 1 .. of the
         # splitmix64 stream; values = global index.  The exchange sort is out
         # of place (inputs are never modified), so a pool of 2 stays fresh.
-        pool = max(1, min(2, args.pool))
+        pool = 2
         keys, vals = [], []
         for i in range(pool):
             kbuf = torch.empty(n * kb, dtype=torch.uint8, device="cuda")
@@ -251,6 +380,7 @@ def main():
         if bad:
             raise SystemExit(f"bench: rank {rank} output is not sorted ({bad} inversions)")
         recycled = False
+        vendor = None
         elapsed = t1 - t0
         scaling = "weak"
         global_keys = n * world
@@ -269,12 +399,14 @@ def main():
     # roofline of the dominant kernel: one per-digit pass reads and writes every
     # key (+ value) once -> algorithmic bytes per launch = 2 * n * (K + V)
     roof = None
+    traffic, traffic_src = load_pmc_traffic(wl)
     if prof and prof.get("pass_launches"):
         avg_pass_ms = prof["pass_ms"] / prof["pass_launches"]
         alg_bytes = 2 * n * (kb + vb)
         achieved = alg_bytes / (avg_pass_ms / 1e3) / 1e9
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": load_pmc_traffic(wl),
+                "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
+                "traffic_source": traffic_src,
                 # 3-HBM-pass path: the two top-digit passes are thrs_pass_seg
                 "kernel": "thrs_pass_seg" if prof.get("local_launches") else "thrs_pass",
                 "avg_launch_ms": round(avg_pass_ms, 4),
@@ -299,19 +431,20 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline == "auto":
-        cpu = cpu_baseline(args.cpu_seconds)
+        cpu = cpu_baseline(kt, vb, args.cpu_seconds)
 
     if rank == 0:
         out = {"metric": METRIC, "value": round(value, 3), "unit": "Gkeys/s", "n_gpus": world, "steps": steps,
                "warmup": warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
                "scaling": scaling, "vs_baseline": None, "dtype": DTYPE[kt], "data": "synthetic",
-               "config": {"workload": WORKLOADS[wl][3] if not use_dist else
+               "config": {"workload": WORKLOADS[wl][4] if not use_dist else
                           f"{DTYPE[kt]} keys, {n} per GPU x {world} GPUs, bucket-exchange sort",
                           "keys_per_gpu": n, "global_keys": global_keys, "key": DTYPE[kt],
                           "value": None if not vb else f"{vb}B index payload", "bits": [0, kb * 8],
                           "parallelism": parallelism,
+                          "distribution": dist_name,
                           "inputs": "fresh per step" if not recycled else "pool recycled (some steps re-sort)"},
-               "roofline": roof, "cpu_baseline": cpu}
+               "roofline": roof, "cpu_baseline": cpu, "vendor": vendor}
         if phase:
             out["phases_ms"] = phase
         print(json.dumps(out), flush=True)

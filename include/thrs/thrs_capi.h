@@ -28,7 +28,7 @@ extern "C" {
 typedef struct ihipStream_t* hipStream_t; /* identical to HIP's own typedef */
 #endif
 
-#define THRS_ABI_VERSION 1
+#define THRS_ABI_VERSION 2
 
 typedef enum thrs_status {
   THRS_SUCCESS = 0,
@@ -51,6 +51,32 @@ typedef struct thrs_config {
   int32_t valueType;          /* THRS_VALUE_* */
   int32_t sortOrder;          /* THRS_ORDER_* */
 } thrs_config;
+
+/* Explicit per-call path and tuning choices (no reference counterpart: the
+ * reference has one path).  All-zero = THRS_*_AUTO everywhere = what
+ * thrs_sort_keys / thrs_sort_pairs do.  Every choice produces the same,
+ * bit-identical result; they exist for tests, A/B measurements and callers
+ * that know their key distribution (e.g. the multi-GPU finish, whose buckets
+ * never fit the local sort).  Nothing is read from the environment. */
+enum { THRS_PATH_AUTO = 0, THRS_PATH_LSD = 1, THRS_PATH_BUCKET = 2 };
+enum { THRS_LOCAL_AUTO = 0, THRS_LOCAL_BIG = 1, THRS_LOCAL_SMALL = 2, THRS_LOCAL_BIG32 = 3 };
+enum { THRS_SEG_AUTO = 0, THRS_SEG_TOP_ONLY = 1, THRS_SEG_NONE = 2 };
+enum { THRS_CLAIMS_AUTO = 0, THRS_CLAIMS_XCD_BLOCKS = 1, THRS_CLAIMS_TICKET = 2 };
+enum { THRS_RANK_AUTO = 0, THRS_RANK_ATOMIC = 1, THRS_RANK_BALLOT = 2 };
+typedef struct thrs_options {
+  int32_t path;          /* THRS_PATH_*: LSD = one device pass per digit; BUCKET = the
+                            3-HBM-pass path wherever the key/value types and window
+                            allow it, for any n (AUTO: n in [2^28, 2^30 + 2^26])   */
+  int32_t localGeometry; /* THRS_LOCAL_*: the bucket path's in-LDS sort: 18432- or
+                            9216-key chunks; BIG32 = no 16-bit items (u32 keys)      */
+  int32_t segmented;     /* THRS_SEG_*: XCD-segmented top-digit passes (AUTO: both)   */
+  int32_t tileClaims;    /* THRS_CLAIMS_*: XCD-block tile claims in the digit passes
+                            (AUTO: 4-byte keys without values, n >= 2^29)            */
+  int32_t rank;          /* THRS_RANK_*: in-tile rank by lane-ordered LDS atomics
+                            (AUTO: where the per-device probe confirms the order) or
+                            by the 8-ballot match                                    */
+  int32_t reserved[3];   /* zero */
+} thrs_options;
 
 /* == RadixSort::TemporaryBufferDef (tinyhipradixsort.hpp:806-832).
  * Layout of the caller's temporary buffer: [pSumBuffer][keyOut][valueOut].
@@ -89,6 +115,13 @@ int thrs_sort_keys(const thrs_config* config, void* inputKeyBuffer, uint32_t num
 int thrs_sort_pairs(const thrs_config* config, void* inputKeyBuffer, void* inputValueBuffer, uint32_t numberOfInputs,
                     void* temporaryBuffer, int startBits, int endBits, hipStream_t stream);
 
+/* thrs_sort_keys / thrs_sort_pairs with explicit options (NULL = defaults). */
+int thrs_sort_keys_ex(const thrs_config* config, const thrs_options* options, void* inputKeyBuffer,
+                      uint32_t numberOfInputs, void* temporaryBuffer, int startBits, int endBits, hipStream_t stream);
+int thrs_sort_pairs_ex(const thrs_config* config, const thrs_options* options, void* inputKeyBuffer,
+                       void* inputValueBuffer, uint32_t numberOfInputs, void* temporaryBuffer, int startBits,
+                       int endBits, hipStream_t stream);
+
 /* Multi-GPU building block (no reference counterpart -- the reference is
  * single-GPU): ONE stable LSD pass by the 8-bit digit at
  * bitLocation (the reference's per-pass digit, tinyhipradixsort.hpp:862-867,
@@ -102,10 +135,19 @@ int thrs_partition_pass(const thrs_config* config, const void* keysIn, const voi
                         void* temporaryBuffer, void* keysOut, void* valuesOut, int bitLocation, uint32_t* counts,
                         hipStream_t stream);
 
-/* Synchronising debug check: THRS_ERROR_LOOKBACK_TIMEOUT if any look-back of
- * the last sort that used `temporaryBuffer` gave up its bounded spin (no
- * reference counterpart; the reference would hang instead). */
+/* Device-side failures (no reference counterpart; the reference would hang
+ * where these give up).  A look-back or tile-claim wait is bounded; when the
+ * bound is hit the sort's output is wrong and the failure is recorded twice:
+ *   - in `temporaryBuffer` (until its next sort):
+ *     thrs_check_device_error synchronises `stream` and returns
+ *     THRS_ERROR_LOOKBACK_TIMEOUT if the last sort on it failed;
+ *   - in a per-device sticky word in host memory, which the NEXT thrs_sort_*
+ *     call on that device reports (and clears) before doing anything:
+ *     THRS_ERROR_LOOKBACK_TIMEOUT, without a synchronisation.
+ * thrs_take_device_error reads and clears the sticky word without sorting
+ * (non-blocking: it sees failures of sorts that have finished). */
 int thrs_check_device_error(void* temporaryBuffer, hipStream_t stream);
+int thrs_take_device_error(void);
 
 /* Kernel timing for benchmarks (no reference counterpart; the reference's
  * per-kernel stopwatches are commented out at tinyhipradixsort.hpp:881-928).
@@ -124,8 +166,7 @@ int thrs_profile_read_kind(int kind, double* ms, int* launches);
 /* Rank path of the current device: 1 = one LDS atomic per key (gfx950
  * services conflicting lanes of a fully active wave in lane order; checked by
  * a one-time probe kernel per device), 0 = ballot match (always stable).
- * THRS_RANK=ballot|atomic in the environment overrides.  No reference
- * counterpart. */
+ * No reference counterpart. */
 int thrs_rank_mode(void);
 
 /* Diagnostic: resident workgroups per CU of the 3-pass path's local bucket

@@ -12,6 +12,13 @@
 //   TemporaryBufferDef / getTemporaryBufferBytes    (reference :806-843)
 //   sortKeys / sortPairs                            (reference :845-852)
 //
+// Extensions (no reference counterpart): setOptions / options (explicit path
+// and tuning choices, thrs_options; defaults = the library's choice), and
+// THRS_CHECKED: defined before including this header, every sortKeys /
+// sortPairs synchronises its stream and throws (aborts) on a device-side
+// failure of that sort (thrs_check_device_error) -- without it such a failure
+// is reported by the next sort on the device (thrs_capi.h).
+//
 // What changed underneath: no Orochi and no hipRTC.  Every call goes through
 // the C-ABI of libthrs.so (<thrs/thrs_capi.h>), whose kernels are compiled
 // ahead of time for gfx950.  `extraArgs` (hipRTC flags in the reference) are
@@ -155,24 +162,39 @@ class RadixSort {
   void sortKeys(void* inputKeyBuffer, uint32_t numberOfInputs, void* temporaryBuffer, int startBits, int endBits,
                 oroStream stream) {
     const thrs_config c = cconfig();
-    check(thrs_sort_keys(&c, inputKeyBuffer, numberOfInputs, temporaryBuffer, startBits, endBits,
-                         reinterpret_cast<hipStream_t>(stream)));
+    check(thrs_sort_keys_ex(&c, &m_options, inputKeyBuffer, numberOfInputs, temporaryBuffer, startBits, endBits,
+                            reinterpret_cast<hipStream_t>(stream)));
+    checked(temporaryBuffer, stream);
   }
   void sortPairs(void* inputKeyBuffer, void* inputValueBuffer, uint32_t numberOfInputs, void* temporaryBuffer,
                  int startBits, int endBits, oroStream stream) {
     const thrs_config c = cconfig();
-    check(thrs_sort_pairs(&c, inputKeyBuffer, inputValueBuffer, numberOfInputs, temporaryBuffer, startBits, endBits,
-                          reinterpret_cast<hipStream_t>(stream)));
+    check(thrs_sort_pairs_ex(&c, &m_options, inputKeyBuffer, inputValueBuffer, numberOfInputs, temporaryBuffer,
+                             startBits, endBits, reinterpret_cast<hipStream_t>(stream)));
+    checked(temporaryBuffer, stream);
   }
 
   const Config& config() const { return m_config; }
+
+  // extension: explicit path / tuning choices (thrs_capi.h thrs_options)
+  void setOptions(const thrs_options& options) { m_options = options; }
+  const thrs_options& options() const { return m_options; }
 
  private:
   thrs_config cconfig() const {
     return thrs_config{m_config.keyIs16byteAligned ? 1 : 0, static_cast<int32_t>(m_config.keyType),
                        static_cast<int32_t>(m_config.valueType), static_cast<int32_t>(m_config.sortOrder)};
   }
+  static void checked(void* temporaryBuffer, oroStream stream) {
+#ifdef THRS_CHECKED
+    check(thrs_check_device_error(temporaryBuffer, reinterpret_cast<hipStream_t>(stream)));
+#else
+    (void)temporaryBuffer;
+    (void)stream;
+#endif
+  }
   Config m_config;
+  thrs_options m_options{};
 };
 
 }  // namespace thrs

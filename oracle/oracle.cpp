@@ -161,12 +161,20 @@ void orc_std_sort_keys(int keyType, void* keys, uint64_t n, int descending) {
 // (unittest.cpp:526, 563, 711): libstdc++ parallel mode over OpenMP.
 void orc_parallel_sort_u32(uint32_t* keys, uint64_t n) { __gnu_parallel::sort(keys, keys + n); }
 void orc_parallel_sort_u64(uint64_t* keys, uint64_t n) { __gnu_parallel::sort(keys, keys + n); }
+void orc_parallel_sort_keys(int keyType, void* keys, uint64_t n) {
+  switch (keyType) {
+    case ORC_U32: __gnu_parallel::sort((uint32_t*)keys, (uint32_t*)keys + n); break;
+    case ORC_U64: __gnu_parallel::sort((uint64_t*)keys, (uint64_t*)keys + n); break;
+    case ORC_F32: __gnu_parallel::sort((float*)keys, (float*)keys + n); break;
+    case ORC_F64: __gnu_parallel::sort((double*)keys, (double*)keys + n); break;
+  }
+}
 
 }  // extern "C"
 
 // stableSortPairs<K,V> (unittest.cpp:358-377): std::stable_sort of (key,value)
 // pairs by key with operator<.  valueBytes 4/8/16.
-template <class K, int VB>
+template <class K, int VB, bool PAR = false>
 static void stable_pairs_t(void* keys, void* values, uint64_t n) {
   struct V { uint8_t b[VB]; };
   std::vector<std::pair<K, V>> pairs(n);
@@ -174,18 +182,19 @@ static void stable_pairs_t(void* keys, void* values, uint64_t n) {
     pairs[i].first = ((K*)keys)[i];
     std::memcpy(pairs[i].second.b, (uint8_t*)values + i * VB, VB);
   }
-  std::stable_sort(pairs.begin(), pairs.end(),
-                   [](const std::pair<K, V>& a, const std::pair<K, V>& b) { return a.first < b.first; });
+  auto less = [](const std::pair<K, V>& a, const std::pair<K, V>& b) { return a.first < b.first; };
+  if constexpr (PAR) __gnu_parallel::stable_sort(pairs.begin(), pairs.end(), less);
+  else std::stable_sort(pairs.begin(), pairs.end(), less);
   for (uint64_t i = 0; i < n; ++i) {
     ((K*)keys)[i] = pairs[i].first;
     std::memcpy((uint8_t*)values + i * VB, pairs[i].second.b, VB);
   }
 }
-template <class K>
+template <class K, bool PAR = false>
 static void stable_pairs_k(void* keys, void* values, uint64_t n, int valueBytes) {
-  if (valueBytes == 4) stable_pairs_t<K, 4>(keys, values, n);
-  else if (valueBytes == 8) stable_pairs_t<K, 8>(keys, values, n);
-  else stable_pairs_t<K, 16>(keys, values, n);
+  if (valueBytes == 4) stable_pairs_t<K, 4, PAR>(keys, values, n);
+  else if (valueBytes == 8) stable_pairs_t<K, 8, PAR>(keys, values, n);
+  else stable_pairs_t<K, 16, PAR>(keys, values, n);
 }
 extern "C" {
 void orc_std_stable_sort_pairs(int keyType, int valueBytes, void* keys, void* values, uint64_t n) {
@@ -194,6 +203,17 @@ void orc_std_stable_sort_pairs(int keyType, int valueBytes, void* keys, void* va
     case ORC_U64: stable_pairs_k<uint64_t>(keys, values, n, valueBytes); break;
     case ORC_F32: stable_pairs_k<float>(keys, values, n, valueBytes); break;
     case ORC_F64: stable_pairs_k<double>(keys, values, n, valueBytes); break;
+  }
+}
+
+// the same with __gnu_parallel::stable_sort (all OpenMP threads): the all-core
+// CPU baseline for sortPairs workloads (bench.py cpu_baseline)
+void orc_parallel_stable_sort_pairs(int keyType, int valueBytes, void* keys, void* values, uint64_t n) {
+  switch (keyType) {
+    case ORC_U32: stable_pairs_k<uint32_t, true>(keys, values, n, valueBytes); break;
+    case ORC_U64: stable_pairs_k<uint64_t, true>(keys, values, n, valueBytes); break;
+    case ORC_F32: stable_pairs_k<float, true>(keys, values, n, valueBytes); break;
+    case ORC_F64: stable_pairs_k<double, true>(keys, values, n, valueBytes); break;
   }
 }
 

@@ -58,6 +58,8 @@ def lib():
             L.orc_parallel_sort_u32.argtypes = [vp, u64]
             L.orc_parallel_sort_u64.argtypes = [vp, u64]
             L.orc_std_stable_sort_pairs.argtypes = [i32, i32, vp, vp, u64]
+            L.orc_parallel_stable_sort_pairs.argtypes = [i32, i32, vp, vp, u64]
+            L.orc_parallel_sort_keys.argtypes = [i32, vp, u64]
             L.orc_std_stable_sort_window_u64.argtypes = [vp, vp, u64, i32, i32]
             _lib = L
     return _lib
@@ -189,13 +191,21 @@ def std_sort_keys(key_type: int, keys: np.ndarray, descending: bool = False) -> 
     return k
 
 
-def parallel_sort(keys: np.ndarray) -> np.ndarray:
+def parallel_sort(keys: np.ndarray, key_type: int | None = None) -> np.ndarray:
+    """__gnu_parallel::sort with operator< of the key type (floats as floats)."""
     k = np.ascontiguousarray(keys).copy()
-    if k.dtype == np.uint32:
-        lib().orc_parallel_sort_u32(_p(k), k.shape[0])
-    else:
-        lib().orc_parallel_sort_u64(_p(k), k.shape[0])
+    if key_type is None:
+        key_type = U32 if k.dtype.itemsize == 4 else U64
+    lib().orc_parallel_sort_keys(key_type, _p(k), k.shape[0])
     return k
+
+
+def parallel_stable_sort_pairs(key_type: int, keys: np.ndarray, values: np.ndarray):
+    k = np.ascontiguousarray(keys).copy()
+    v = np.ascontiguousarray(values).copy()
+    vb = v.nbytes // max(1, k.shape[0])
+    lib().orc_parallel_stable_sort_pairs(key_type, vb, _p(k), _p(v), k.shape[0])
+    return k, v
 
 
 def std_stable_sort_pairs(key_type: int, keys: np.ndarray, values: np.ndarray):

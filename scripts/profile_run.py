@@ -14,13 +14,13 @@ import torch  # noqa: E402
 import tinyhipradixsort_amd as T  # noqa: E402
 from tinyhipradixsort_amd import testutil as TU  # noqa: E402
 
-WL = {"c2": (0, 0, 1 << 30), "c3": (0, 4, 1 << 30), "c4": (2, 0, 1 << 28), "c5": (1, 8, 1 << 28)}
+from bench import WORKLOADS  # noqa: E402  (name -> key type, value bytes, n, distribution, description)
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--workload", default="c2")
 ap.add_argument("--steps", type=int, default=3)
 a = ap.parse_args()
-kt, vb, n = WL[a.workload]
+kt, vb, n, dist, _desc = WORKLOADS[a.workload]
 kb = 4 if kt in (0, 2) else 8
 G = 1 << 30
 src = torch.empty(G, dtype=torch.uint8, device="cuda")
@@ -39,7 +39,10 @@ tmp = torch.empty(d.getTemporaryBufferBytesForSortPairs() if vb else d.getTempor
 keys = torch.empty(n * kb, dtype=torch.uint8, device="cuda")
 vals = torch.empty(max(1, n * vb), dtype=torch.uint8, device="cuda")
 for s in range(a.steps + 1):
-    TU.fill_keys(kt, keys, n, start=s * n)
+    if dist == "uniform":
+        TU.fill_keys(kt, keys, n, start=s * n)
+    else:
+        TU.fill_dist(kt, keys, n, dist, start=s * n)
     if vb:
         TU.iota(vb, vals, n)
         rs.sortPairs(keys, vals, n, tmp, 0, kb * 8)

@@ -23,6 +23,8 @@
 #include <string>
 #include <vector>
 
+static thrs_options g_opts{};  // set from the command line (main)
+
 #define TEST_ITERATION 128
 #define TEST_MAX_ARRAY_SIZE 100000
 
@@ -109,6 +111,7 @@ static void testSortKeys(thrs::SortOrder sortOrder = thrs::SortOrder::Ascending)
   config.configureWithKey<KeyType>();
   config.sortOrder = sortOrder;
   thrs::RadixSort radixsort(extraArgs, config);
+  radixsort.setOptions(g_opts);
 
   splitmix64 rng;
   for (int i = 0; i < TEST_ITERATION; i++) {
@@ -145,6 +148,7 @@ UTEST(SortKeys, extremeCase) {  // unittest.cpp:191-225
   thrs::RadixSort::Config config;
   config.configureWithKey<KeyType>();
   thrs::RadixSort radixsort(extraArgs, config);
+  radixsort.setOptions(g_opts);
   splitmix64 rng;
   for (int i = 0; i < TEST_ITERATION; i++) {
     int numberOfInputs = 1 + rng.next() % (TEST_MAX_ARRAY_SIZE - 1);
@@ -172,6 +176,7 @@ UTEST(StartBits, u64) {  // unittest.cpp:248-355
     config.configureWithKey<KeyType>();
     config.sortOrder = sortOrder;
     thrs::RadixSort radixsort(extraArgs, config);
+    radixsort.setOptions(g_opts);
     splitmix64 rng;
     for (int i = 0; i < TEST_ITERATION; i++) {
       int numberOfInputs = 1 + rng.next() % (TEST_MAX_ARRAY_SIZE - 1);
@@ -197,6 +202,7 @@ UTEST(StartBits, u64) {  // unittest.cpp:248-355
   thrs::RadixSort::Config config;
   config.configureWithKeyPair<KeyType, ValueType>();
   thrs::RadixSort radixsort(extraArgs, config);
+  radixsort.setOptions(g_opts);
   splitmix64 rng;
   for (int i = 0; i < TEST_ITERATION; i++) {
     int numberOfInputs = 1 + rng.next() % (TEST_MAX_ARRAY_SIZE - 1);
@@ -250,6 +256,7 @@ static void testSortPairs() {  // unittest.cpp:379-424
   thrs::RadixSort::Config config;
   config.configureWithKeyPair<KeyType, ValueType>();
   thrs::RadixSort radixsort(extraArgs, config);
+  radixsort.setOptions(g_opts);
   splitmix64 rng;
   for (int i = 0; i < TEST_ITERATION; i++) {
     int numberOfInputs = 1 + rng.next() % (TEST_MAX_ARRAY_SIZE - 1);
@@ -297,6 +304,7 @@ UTEST(SortPairs, K32V128) { testSortPairs<uint32_t, u128>(); }
 UTEST(Edge, emptyAndNoop) {
   thrs::RadixSort::Config config;
   thrs::RadixSort radixsort(extraArgs, config);
+  radixsort.setOptions(g_opts);
   thrs::Buffer tmp(radixsort.getTemporaryBufferBytes(0).getTemporaryBufferBytesForSortKeys());
   thrs::Buffer keys(4);
   radixsort.sortKeys(keys.data(), 0, tmp.data(), 0, 32, stream);       // n = 0
@@ -321,6 +329,7 @@ UTEST(Edge, f32SpecialValues) {  // NaN / Inf / +-0 / denormals, pinned by the b
   thrs::RadixSort::Config config;
   config.configureWithKeyPair<float, uint32_t>();
   thrs::RadixSort radixsort(extraArgs, config);
+  radixsort.setOptions(g_opts);
   splitmix64 rng;
   const uint32_t specials[] = {0x00000000u, 0x80000000u, 0x00000001u, 0x80000001u, 0x007FFFFFu, 0x807FFFFFu,
                                0x7F800000u, 0xFF800000u, 0x7FC00000u, 0xFFC00000u, 0x7F800001u, 0xFFFFFFFFu,
@@ -362,6 +371,7 @@ UTEST(Edge, pairsDescendingU32) {
   config.configureWithKeyPair<uint32_t, uint32_t>();
   config.sortOrder = thrs::SortOrder::Descending;
   thrs::RadixSort radixsort(extraArgs, config);
+  radixsort.setOptions(g_opts);
   splitmix64 rng;
   for (int it = 0; it < 16; ++it) {
     const int n = 1 + rng.next() % 99999;
@@ -394,6 +404,7 @@ UTEST(Edge, misalignedKeys) {  // keyIs16byteAligned=false and a 4-byte-offset b
   config.configureWithKey<uint32_t>();
   config.keyIs16byteAligned = false;
   thrs::RadixSort radixsort(extraArgs, config);
+  radixsort.setOptions(g_opts);
   splitmix64 rng;
   const int n = 77777;
   std::vector<uint32_t> keys(n);
@@ -414,6 +425,7 @@ UTEST(Edge, windowsU32) {  // multi-pass windows, odd and even pass counts, u32
   thrs::RadixSort::Config config;
   config.configureWithKeyPair<uint32_t, uint32_t>();
   thrs::RadixSort radixsort(extraArgs, config);
+  radixsort.setOptions(g_opts);
   splitmix64 rng;
   const int windows[][2] = {{0, 8}, {0, 16}, {4, 28}, {8, 32}, {16, 32}, {24, 32}, {3, 27}, {0, 24}};
   for (auto& w : windows) {
@@ -449,6 +461,7 @@ UTEST_LARGE(SortKeys, u32Large) {  // unittest.cpp:688-717 (parallel_sort -> __g
   thrs::RadixSort::Config config;
   config.configureWithKey<KeyType>();
   thrs::RadixSort radixsort(extraArgs, config);
+  radixsort.setOptions(g_opts);
   splitmix64 rng;
   uint32_t numberOfInputs = 1024llu * 1024 * 1024 * 2 + 100;
   thrs::Buffer tmpBuffer(radixsort.getTemporaryBufferBytes(numberOfInputs).getTemporaryBufferBytesForSortKeys());
@@ -468,11 +481,23 @@ UTEST_LARGE(SortKeys, u32Large) {  // unittest.cpp:688-717 (parallel_sort -> __g
 int main(int argc, char** argv) {
   std::string filter;
   bool list = false, large = false;
+  // path / claim / rank choices for the whole matrix (thrs_options): the
+  // tests run it with each non-default choice forced
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     if (a.rfind("--filter=", 0) == 0) filter = a.substr(9);
     else if (a == "--list") list = true;
     else if (a == "--large") large = true;
+    else if (a == "--path=lsd") g_opts.path = THRS_PATH_LSD;
+    else if (a == "--path=bucket") g_opts.path = THRS_PATH_BUCKET;
+    else if (a == "--claims=xcd") g_opts.tileClaims = THRS_CLAIMS_XCD_BLOCKS;
+    else if (a == "--claims=ticket") g_opts.tileClaims = THRS_CLAIMS_TICKET;
+    else if (a == "--rank=atomic") g_opts.rank = THRS_RANK_ATOMIC;
+    else if (a == "--rank=ballot") g_opts.rank = THRS_RANK_BALLOT;
+    else {
+      std::printf("unknown argument %s\n", a.c_str());
+      return 2;
+    }
   }
   if (list) {
     for (auto& c : cases()) std::printf("%s%s\n", c.name, c.large ? " (--large)" : "");

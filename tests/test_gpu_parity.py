@@ -25,13 +25,13 @@ def from_dev(t, dtype, shape):
     return t.cpu().numpy().view(dtype).reshape(shape)
 
 
-def make_sorter(kt, vb, desc):
+def make_sorter(kt, vb, desc, **options):
     import tinyhipradixsort_amd as T
     cfg = T.RadixSort.Config()
     cfg.keyType = T.KeyType(kt)
     cfg.valueType = {0: T.ValueType.U32, 4: T.ValueType.U32, 8: T.ValueType.U64, 16: T.ValueType.U128}[vb]
     cfg.sortOrder = T.SortOrder.Descending if desc else T.SortOrder.Ascending
-    return T.RadixSort([], cfg)
+    return T.RadixSort([], cfg, T.Options(**options))
 
 
 def gpu_sort(torch, rs, item, kt, vb, start, end):
@@ -124,14 +124,13 @@ def test_matrix_vs_oracle(gpu, kt, vb, desc):
 
 def test_rank_probe_and_ballot_fallback(gpu):
     """The LDS-atomic rank path is used only where the lane-order probe passes;
-    the ballot-match fallback must be bit-exact too (forced via THRS_RANK)."""
+    the ballot-match fallback must be bit-exact too (forced: Options.rank)."""
     import tinyhipradixsort_amd as T
     mode = T.lib().thrs_rank_mode()
     assert mode in (0, 1)
     print("rank mode:", "lds-atomic" if mode else "ballot")
     exe = os.path.join(ROOT, "tests", "cpp", "unittest_thrs")
-    env = dict(os.environ, THRS_RANK="ballot")
-    r = subprocess.run([exe, "--filter=SortPairs.K"], capture_output=True, text=True, timeout=600, env=env)
+    r = subprocess.run([exe, "--filter=SortPairs.K", "--rank=ballot"], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:]
 
 
@@ -144,47 +143,41 @@ def test_cpp_port_of_reference_unittest(gpu):
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
 
 
-@pytest.mark.parametrize("xb", ["1", "0"])
-def test_cpp_port_with_claim_mode_forced(gpu, xb):
+@pytest.mark.parametrize("claims", ["xcd", "ticket"])
+def test_cpp_port_with_claim_mode_forced(gpu, claims):
     """The same UTEST matrix with the XCD-block tile claims (thrs_pass_xb)
-    forced on for every configuration and size (THRS_XB=1), and forced off
-    (THRS_XB=0): by default they only run for 4-byte keys at n >= 2^29."""
+    forced on for every configuration and size, and forced off (one-ticket
+    tile ids): by default they only run for 4-byte keys at n >= 2^29."""
     exe = os.path.join(ROOT, "tests", "cpp", "unittest_thrs")
-    env = dict(os.environ, THRS_XB=xb)
-    r = subprocess.run([exe], capture_output=True, text=True, timeout=900, env=env)
+    r = subprocess.run([exe, f"--claims={claims}"], capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
 
 
-@pytest.mark.parametrize("hy", ["1", "0"])
-def test_cpp_port_with_hybrid_forced(gpu, hy):
+@pytest.mark.parametrize("path", ["bucket", "lsd"])
+def test_cpp_port_with_path_forced(gpu, path):
     """The UTEST matrix with the 3-HBM-pass path (bucket passes + local LDS
-    sort, thrs_hybrid.hpp) forced on for every size (THRS_HYBRID=1; by default
-    it runs for n in [2^28, 2^30 + 2^26]) and off (plain LSD passes)."""
+    sort, thrs_hybrid.hpp) forced on for every size (by default it runs for n
+    in [2^28, 2^30 + 2^26]) and off (plain LSD passes)."""
     exe = os.path.join(ROOT, "tests", "cpp", "unittest_thrs")
-    env = dict(os.environ, THRS_HYBRID=hy)
-    r = subprocess.run([exe], capture_output=True, text=True, timeout=900, env=env)
+    r = subprocess.run([exe, f"--path={path}"], capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
 
 
 @pytest.mark.parametrize("geom,seg", [("big", "1"), ("small", "1"), ("big", "0"), ("big", "top"), ("big32", "1")])
 @pytest.mark.parametrize("kt", [O.U32, O.F32])
 @pytest.mark.parametrize("desc", [False, True])
-def test_hybrid_paths_vs_oracle(gpu, kt, desc, geom, seg, monkeypatch):
+def test_hybrid_paths_vs_oracle(gpu, kt, desc, geom, seg):
     """4-byte keys-only sorts with >= 3 digits take the hybrid path (forced
     here for every size; by default it runs for n in [2^28, 2^30 + 2^26]): chunked
     local sort (single- and multi-bucket chunks), and the gated fallback to
     plain LSD when one bucket exceeds the local capacity (18432 keys) --
     including an odd number of low passes (window of 3 digits: gated copy)."""
     torch = gpu
-    monkeypatch.setenv("THRS_HYBRID", "1")
-    # the two top-digit passes XCD-segmented (default), neither, or the top one only
-    monkeypatch.setenv("THRS_SEG", "0" if seg == "0" else "1")
-    monkeypatch.setenv("THRS_SEGA", "1" if seg == "1" else "0")
-    # local-sort geometry: 18432- or 9216-key chunks; u32 keys over the whole
-    # key sort 16-bit items in the big geometry unless THRS_LOC16=0 ("big32")
-    monkeypatch.setenv("THRS_LOCAL", "small" if geom == "small" else "big")
-    monkeypatch.setenv("THRS_LOC16", "0" if geom == "big32" else "1")
-    rs = make_sorter(kt, 0, desc)
+    # the two top-digit passes XCD-segmented (default), neither, or the top one
+    # only; local-sort geometry: 18432- or 9216-key chunks; u32 keys over the
+    # whole key sort 16-bit items in the big geometry unless "big32"
+    rs = make_sorter(kt, 0, desc, path="bucket",
+                     segmented={"1": "auto", "0": "none", "top": "top_only"}[seg], localGeometry=geom)
     dists = {
         "uniform": lambda k: k,
         "low20": lambda k: k & np.array(0xFFFFF, k.dtype),        # 16 buckets -> fallback above 295k keys
@@ -209,14 +202,12 @@ def test_hybrid_paths_vs_oracle(gpu, kt, desc, geom, seg, monkeypatch):
 
 @pytest.mark.parametrize("desc", [False, True])
 @pytest.mark.parametrize("geom", ["big", "small"])
-def test_hybrid_pairs_vs_oracle(gpu, desc, geom, monkeypatch):
+def test_hybrid_pairs_vs_oracle(gpu, desc, geom):
     """sortPairs with u32 keys + u32 values over the whole key takes the hybrid
     path (single-bucket chunks, positions carried in the local sort's items);
     stability on ties, the gated LSD fallback, and partial windows (plain LSD)."""
     torch = gpu
-    monkeypatch.setenv("THRS_HYBRID", "1")  # forced for every size
-    monkeypatch.setenv("THRS_LOCAL", geom)
-    rs = make_sorter(O.U32, 4, desc)
+    rs = make_sorter(O.U32, 4, desc, path="bucket", localGeometry=geom)  # forced for every size
     dists = {
         "uniform": lambda k: k,
         "low20": lambda k: k & np.array(0xFFFFF, k.dtype),
@@ -361,3 +352,41 @@ def test_u32_large_2pow31_plus_100(gpu):
     # the first and last values of the reference's stream, pinned on the host
     head = from_dev(keys[:4 * 8], np.uint32, (8,))
     assert head[0] <= head[-1]
+
+
+@pytest.mark.large
+@pytest.mark.parametrize("dist", ["sorted", "reverse", "extreme", "fewuniq"])
+@pytest.mark.parametrize("kt,vb,n", [(O.U32, 0, 1 << 30),      # C2 shape (3-HBM-pass path / its fallback)
+                                     (O.U32, 4, 1 << 30),      # C3 shape
+                                     (O.F32, 0, 1 << 28),      # C4 shape
+                                     (O.U64, 8, 1 << 26)])
+def test_full_size_low_entropy(gpu, dist, kt, vb, n):
+    """Already-sorted, reverse-sorted, extremeCase (unittest.cpp:191-225) and
+    16-distinct-key inputs at full size: sortedness, multiset fingerprint and,
+    for pairs with index payloads, gather consistency + stability."""
+    torch = gpu
+    from tinyhipradixsort_amd import testutil as TU
+    kb = O.KEY_BYTES[kt]
+    keys = torch.empty(kb * n, dtype=torch.uint8, device="cuda")
+    TU.fill_dist(kt, keys, n, dist)
+    orig = keys.clone() if vb else None
+    torch.cuda.synchronize()
+    fp = TU.fingerprint(kt, keys, n)
+    rs = make_sorter(kt, vb, False)
+    d = rs.getTemporaryBufferBytes(n)
+    if vb:
+        vals = torch.empty(vb * n, dtype=torch.uint8, device="cuda")
+        TU.iota(vb, vals, n)
+        tmp = torch.empty(d.getTemporaryBufferBytesForSortPairs(), dtype=torch.uint8, device="cuda")
+        rs.sortPairs(keys, vals, n, tmp, 0, kb * 8)
+    else:
+        tmp = torch.empty(d.getTemporaryBufferBytesForSortKeys(), dtype=torch.uint8, device="cuda")
+        rs.sortKeys(keys, n, tmp, 0, kb * 8)
+    torch.cuda.synchronize()
+    rs.checkDeviceError(tmp)
+    assert TU.count_unsorted(kt, keys, n, 0, kb * 8) == 0
+    assert TU.fingerprint(kt, keys, n) == fp
+    if vb:
+        r = TU.check_pairs(kt, vb, orig, keys, vals, n, 0, kb * 8)
+        assert r["gather_mismatch"] == 0 and r["unstable"] == 0
+        assert (r["index_sum"], r["index_xor"]) == TU.expected_index_fingerprint(n)

@@ -31,10 +31,10 @@ from dataclasses import dataclass
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libthrs.so")
 TESTUTIL_PATH = os.path.join(_HERE, "libthrs_testutil.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 __all__ = ["KeyType", "ValueType", "SortOrder", "bytesOf", "div_round_up64", "next_multiple64", "Buffer",
-           "RadixSort", "ThrsError", "lib", "LIB_PATH"]
+           "RadixSort", "Options", "ThrsError", "lib", "LIB_PATH", "take_device_error"]
 
 
 class ThrsError(RuntimeError):
@@ -65,6 +65,10 @@ def lib() -> ctypes.CDLL:
         L.thrs_get_temporary_buffer_bytes.argtypes = [ctypes.POINTER(_CConfig), u32, ctypes.POINTER(_CTempDef)]
         L.thrs_sort_keys.argtypes = [ctypes.POINTER(_CConfig), vp, u32, vp, i32, i32, vp]
         L.thrs_sort_pairs.argtypes = [ctypes.POINTER(_CConfig), vp, vp, u32, vp, i32, i32, vp]
+        L.thrs_sort_keys_ex.argtypes = [ctypes.POINTER(_CConfig), ctypes.POINTER(_COptions), vp, u32, vp, i32, i32, vp]
+        L.thrs_sort_pairs_ex.argtypes = [ctypes.POINTER(_CConfig), ctypes.POINTER(_COptions), vp, vp, u32, vp, i32,
+                                         i32, vp]
+        L.thrs_take_device_error.restype = i32
         L.thrs_check_device_error.argtypes = [vp, vp]
         L.thrs_partition_pass.argtypes = [ctypes.POINTER(_CConfig), vp, vp, u32, vp, vp, vp, i32, vp, vp]
         L.thrs_malloc.argtypes = [ctypes.POINTER(vp), i64]
@@ -80,7 +84,9 @@ def lib() -> ctypes.CDLL:
                                         ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32)]
         L.thrs_profile_read_kind.argtypes = [i32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32)]
         L.thrs_rank_mode.restype = i32
-        for f in ("thrs_profile_enable", "thrs_profile_read", "thrs_profile_read_kind", "thrs_get_temporary_buffer_bytes", "thrs_sort_keys", "thrs_sort_pairs", "thrs_check_device_error", "thrs_partition_pass",
+        for f in ("thrs_profile_enable", "thrs_profile_read", "thrs_profile_read_kind",
+                  "thrs_get_temporary_buffer_bytes", "thrs_sort_keys", "thrs_sort_pairs", "thrs_sort_keys_ex",
+                  "thrs_sort_pairs_ex", "thrs_check_device_error", "thrs_partition_pass",
                   "thrs_malloc", "thrs_free", "thrs_memcpy_htod_async", "thrs_memcpy_dtoh", "thrs_memcpy_dtod_async",
                   "thrs_stream_create", "thrs_stream_destroy", "thrs_stream_synchronize"):
             getattr(L, f).restype = i32
@@ -98,6 +104,42 @@ def _check(rc: int):
 class _CConfig(ctypes.Structure):
     _fields_ = [("keyIs16byteAligned", ctypes.c_int32), ("keyType", ctypes.c_int32),
                 ("valueType", ctypes.c_int32), ("sortOrder", ctypes.c_int32)]
+
+
+class _COptions(ctypes.Structure):
+    _fields_ = [("path", ctypes.c_int32), ("localGeometry", ctypes.c_int32), ("segmented", ctypes.c_int32),
+                ("tileClaims", ctypes.c_int32), ("rank", ctypes.c_int32), ("reserved", ctypes.c_int32 * 3)]
+
+
+@dataclass
+class Options:
+    """thrs_options (thrs_capi.h): explicit path / tuning choices, no
+    reference counterpart.  Every choice gives the same bit-exact result; the
+    defaults are the library's own choice.  Values are the names below."""
+    path: str = "auto"            # auto | lsd | bucket
+    localGeometry: str = "auto"   # auto | big | small | big32
+    segmented: str = "auto"       # auto | top_only | none
+    tileClaims: str = "auto"      # auto | xcd_blocks | ticket
+    rank: str = "auto"            # auto | atomic | ballot
+
+    _ENUMS = {"path": ("auto", "lsd", "bucket"), "localGeometry": ("auto", "big", "small", "big32"),
+              "segmented": ("auto", "top_only", "none"), "tileClaims": ("auto", "xcd_blocks", "ticket"),
+              "rank": ("auto", "atomic", "ballot")}
+
+    def _c(self) -> "_COptions":
+        o = _COptions()
+        for f, names in self._ENUMS.items():
+            v = getattr(self, f)
+            if v not in names:
+                raise ThrsError(-1, f"Options.{f}: {v!r} is not one of {names}")
+            setattr(o, f, names.index(v))
+        return o
+
+
+def take_device_error():
+    """Raise (and clear) a device-side failure of any earlier sort on the
+    current device that has finished (thrs_take_device_error; non-blocking)."""
+    _check(lib().thrs_take_device_error())
 
 
 class _CTempDef(ctypes.Structure):
@@ -149,6 +191,15 @@ def _ptr(x) -> int | None:
     if isinstance(x, Buffer):
         return x.data()
     raise TypeError(f"cannot take a device address of {type(x)}")
+
+
+def _n(n) -> int:
+    """numberOfInputs is uint32_t in the reference (hpp:845): refuse what a
+    ctypes c_uint32 would silently truncate."""
+    n = int(n)
+    if not 0 <= n <= 0xFFFFFFFF:
+        raise ThrsError(-1, f"numberOfInputs {n} does not fit uint32_t (tinyhipradixsort.hpp:845)")
+    return n
 
 
 def _stream(s) -> int | None:
@@ -259,8 +310,9 @@ class RadixSort:
         def getOutputValueBuffer(self, p: int) -> int:
             return p + self.pSumBuffer + self.keyOutBuffer
 
-    def __init__(self, extraArgs=(), config: "RadixSort.Config | None" = None):
+    def __init__(self, extraArgs=(), config: "RadixSort.Config | None" = None, options: Options | None = None):
         self.m_config = config if config is not None else RadixSort.Config()
+        self.options = options if options is not None else Options()   # extension: thrs_options
         lib()   # fail loudly here, like the reference's compile-time THRS_ASSERT (hpp:591)
 
     def _c(self) -> _CConfig:
@@ -269,19 +321,20 @@ class RadixSort:
 
     def getTemporaryBufferBytes(self, numberOfMaxInputs: int) -> "RadixSort.TemporaryBufferDef":
         d = _CTempDef()
-        _check(lib().thrs_get_temporary_buffer_bytes(ctypes.byref(self._c()), int(numberOfMaxInputs), ctypes.byref(d)))
+        _check(lib().thrs_get_temporary_buffer_bytes(ctypes.byref(self._c()), _n(numberOfMaxInputs), ctypes.byref(d)))
         return RadixSort.TemporaryBufferDef(d.pSumBuffer, d.keyOutBuffer, d.valueOutBuffer)
 
     def sortKeys(self, inputKeyBuffer, numberOfInputs: int, temporaryBuffer, startBits: int, endBits: int,
                  stream=None):
-        _check(lib().thrs_sort_keys(ctypes.byref(self._c()), _ptr(inputKeyBuffer), int(numberOfInputs),
-                                    _ptr(temporaryBuffer), int(startBits), int(endBits), _stream(stream)))
+        _check(lib().thrs_sort_keys_ex(ctypes.byref(self._c()), ctypes.byref(self.options._c()),
+                                       _ptr(inputKeyBuffer), _n(numberOfInputs), _ptr(temporaryBuffer),
+                                       int(startBits), int(endBits), _stream(stream)))
 
     def sortPairs(self, inputKeyBuffer, inputValueBuffer, numberOfInputs: int, temporaryBuffer, startBits: int,
                   endBits: int, stream=None):
-        _check(lib().thrs_sort_pairs(ctypes.byref(self._c()), _ptr(inputKeyBuffer), _ptr(inputValueBuffer),
-                                     int(numberOfInputs), _ptr(temporaryBuffer), int(startBits), int(endBits),
-                                     _stream(stream)))
+        _check(lib().thrs_sort_pairs_ex(ctypes.byref(self._c()), ctypes.byref(self.options._c()),
+                                        _ptr(inputKeyBuffer), _ptr(inputValueBuffer), _n(numberOfInputs),
+                                        _ptr(temporaryBuffer), int(startBits), int(endBits), _stream(stream)))
 
     def partitionPass(self, inputKeyBuffer, inputValueBuffer, numberOfInputs: int, temporaryBuffer, outputKeyBuffer,
                       outputValueBuffer, bitLocation: int, counts, stream=None):
@@ -289,7 +342,7 @@ class RadixSort:
         bucket counts (device u32[256]); thrs_partition_pass, the bucket
         exchange's partition step (no reference counterpart)."""
         _check(lib().thrs_partition_pass(ctypes.byref(self._c()), _ptr(inputKeyBuffer), _ptr(inputValueBuffer),
-                                         int(numberOfInputs), _ptr(temporaryBuffer), _ptr(outputKeyBuffer),
+                                         _n(numberOfInputs), _ptr(temporaryBuffer), _ptr(outputKeyBuffer),
                                          _ptr(outputValueBuffer), int(bitLocation), _ptr(counts), _stream(stream)))
 
     def checkDeviceError(self, temporaryBuffer, stream=None):

@@ -27,12 +27,6 @@
 #include "thrs_kernels.hpp"
 #include "thrs_hybrid.hpp"
 
-#ifndef THRS_PIPE
-#define THRS_PIPE 0
-#endif
-#ifndef THRS_XB
-#define THRS_XB 1
-#endif
 
 using namespace thrs_dev;
 
@@ -175,18 +169,11 @@ uint64_t* g_stamps = nullptr;   // THRS_STAMPS diagnostic builds only (thrs_debu
 uint64_t* g_lstamps = nullptr;  // same, local sort: [chunk][8] (thrs_debug_set_local_stamps)
 
 // Per-device result of thrs_probe_lds_order: 1 = lane-ordered LDS atomics
-// (fast rank), 0 = ballot-match rank.  -1 = not probed yet.  THRS_RANK=ballot
-// or THRS_RANK=atomic in the environment forces a path.
+// (fast rank), 0 = ballot-match rank.
 int g_rank_mode[64];
 std::once_flag g_rank_once[64];
 
 int probe_rank_mode(hipStream_t stream) {
-#ifdef THRS_FORCE_BALLOT
-  return 0;
-#endif
-  const char* env = getenv("THRS_RANK");
-  if (env && !strcmp(env, "ballot")) return 0;
-  if (env && !strcmp(env, "atomic")) return 1;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
   std::call_once(g_rank_once[dev], [&] {
@@ -212,16 +199,40 @@ int probe_rank_mode(hipStream_t stream) {
   return g_rank_mode[dev];
 }
 
-// THRS_XB=1 / THRS_XB=0 in the environment: force XCD-block claims on / off
-// for every configuration (-1 = size/type heuristic).  Read once.
-int xb_override() {
-  static const int v = [] {
-    const char* e = getenv("THRS_XB");
-    if (e && !strcmp(e, "1")) return 1;
-    if (e && !strcmp(e, "0")) return 0;
-    return -1;
-  }();
-  return v;
+// Per-device sticky error word in host memory (mapped): thrs_err_publish
+// ORs a sort's device error word into it at the end of every sort; the next
+// thrs_sort_* call reads and clears it (thrs_capi.h, "Device-side failures").
+uint32_t* g_sticky[64];          // host view
+uint32_t* g_sticky_dev[64];      // device view
+std::once_flag g_sticky_once[64];
+
+uint32_t* sticky_dev() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  std::call_once(g_sticky_once[dev], [&] {
+    void* h = nullptr;
+    if (hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return;
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+      (void)hipHostFree(h);
+      return;
+    }
+    std::memset(h, 0, 64);
+    g_sticky[dev] = static_cast<uint32_t*>(h);
+    g_sticky_dev[dev] = static_cast<uint32_t*>(d);
+  });
+  return g_sticky_dev[dev];
+}
+// read-and-clear of the current device's sticky word (0 = no failure)
+uint32_t take_sticky() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64 || !g_sticky[dev]) return 0;
+  return __atomic_exchange_n(g_sticky[dev], 0u, __ATOMIC_ACQ_REL);
+}
+
+__global__ void thrs_err_publish(const uint32_t* __restrict__ err, uint32_t* __restrict__ sticky) {
+  const uint32_t e = *err;
+  if (e) __hip_atomic_fetch_or(sticky, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 template <typename F>
@@ -231,43 +242,22 @@ hipError_t allow_lds(F kernel, size_t bytes) {
                              (int)bytes);
 }
 
-// THRS_HYBRID=1 / THRS_HYBRID=0 in the environment: force the 3-HBM-pass path
-// (thrs_hybrid.hpp) on / off wherever it applies (-1 = default: by size).
-// Read on every sort (tests switch it within one process).
-int hybrid_override() {
-  const char* e = getenv("THRS_HYBRID");
-  if (e && !strcmp(e, "1")) return 1;
-  if (e && !strcmp(e, "0")) return 0;
-  return -1;
-}
-
-// THRS_SEG=0 in the environment: the 3-pass path's top-digit pass runs
-// unsegmented (thrs_pass / thrs_pass_xb).  Read on every sort.
-bool seg_enabled() {
-  const char* e = getenv("THRS_SEG");
-  return !(e && !strcmp(e, "0"));
-}
-bool loc16_enabled() {  // THRS_LOC16=0: u32 keys keep the 32-bit local sort (tests, A/B)
-  const char* e = getenv("THRS_LOC16");
-  return !(e && !strcmp(e, "0"));
-}
-bool seg_a_enabled() {  // THRS_SEGA=0: the second-digit pass unsegmented (tests, A/B)
-  const char* e = getenv("THRS_SEGA");
-  return !(e && !strcmp(e, "0"));
-}
-
 // One launch sequence.  Sort mode (counts == nullptr): the result lands in
 // keys/vals.  Partition mode (counts != nullptr, nPass == 1,
 // thrs_partition_pass): the pass writes keyOutBuf/valOutBuf, which are the
 // caller's, and the digit's 256 bucket counts go to `counts`.
 //   LSD path:    histogram of every digit + scan, nPass ping-pong passes,
 //                copy-back after an odd pass count.
-//   hybrid path: 4-byte keys without values, nPass >= 3 (thrs_hybrid.hpp):
-//                bucket histogram + plan, [low-digit passes + copy, gated on
-//                the fallback flag], the two top-digit passes, local sort.
+//   bucket path: 4-byte keys (u32 keys + 4-byte values over the whole key),
+//                nPass >= 3 (thrs_hybrid.hpp): bucket histogram + plan,
+//                [low-digit passes + copy, gated on the fallback flag], the
+//                two top-digit passes (skipped when one bucket holds every
+//                key), local sort.
+// Every hipFuncSetAttribute happens before the first enqueue, so a failure
+// there leaves the caller's buffers untouched.
 template <int KT, int VB, typename ST>
 int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, void* valOutBuf, int startBits, int nPass,
-             bool desc, const Plan& plan, hipStream_t stream, uint32_t* counts = nullptr) {
+             bool desc, const Plan& plan, const thrs_options& opt, hipStream_t stream, uint32_t* counts = nullptr) {
   using U = typename KeyTraits<KT>::U;
   using VW = typename ValueWord<VB>::T;
   using G = PassGeom<sizeof(U), VB>;
@@ -297,48 +287,105 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   VW* valOut = static_cast<VW*>(valOutBuf);
 
   const U orderMask = desc ? (U)~(U)0 : (U)0;
-  const int hyEnv = hybrid_override();
   // 4-byte keys without values; u32 keys with 4-byte values over the whole key
-  constexpr bool kHybridType = sizeof(U) == 4 && (VB == 0 || (VB == 4 && KT == 0));
+  constexpr bool kBucketType = sizeof(U) == 4 && (VB == 0 || (VB == 4 && KT == 0));
   const bool fullWindow = startBits == 0 && nPass * 8 >= (int)(8 * sizeof(U));
-  // Size window (uniform keys: n / 65536 keys per bucket; docs/EXPERIMENTS.md
-  // row 29).  The local sort costs about the same per chunk whatever its size,
-  // so below ~0.75 * 2^30 the two passes it replaces are cheaper; above
-  // 2^30 + 2^26 the largest of 65536 uniform buckets (mean + ~4.5 sigma)
-  // outgrows kLocCap and the fallback would pay for the bucket histogram in
-  // vain.  THRS_HYBRID=1 forces the path for any n (tests), =0 turns it off.
-  // Two local-sort geometries (thrs_hybrid.hpp LocG): LocSmall (9216-key
-  // chunks, uniform buckets of 4-8K keys) for n in [2^28, 2^29], LocBig
-  // (18432) above, up to 2^30 + 2^26 (docs/EXPERIMENTS.md rows 29, 33).
+  // Size window of the default (uniform keys: n / 65536 keys per bucket;
+  // docs/EXPERIMENTS.md row 29): the local sort costs about the same per chunk
+  // whatever its size, so below 2^28 the two passes it replaces are cheaper;
+  // above 2^30 + 2^26 the largest of 65536 uniform buckets (mean + ~4.5 sigma)
+  // outgrows the chunk capacity and the fallback would pay for the bucket
+  // histogram in vain.  THRS_PATH_BUCKET forces the path for any n (tests).
+  // Local geometries (thrs_hybrid.hpp LocG): LocSmall (9216-key chunks,
+  // uniform buckets of 4-8K keys) for n <= 2^29, LocBig (18432) above.
   const uint64_t nn = n;
   const bool sizeOk = nn >= (1ull << 28) && nn <= (1ull << 30) + (1ull << 26);
-  const char* locEnv = getenv("THRS_LOCAL");  // big / small: force the geometry (tests)
-  const bool smallLocal = locEnv && !strcmp(locEnv, "small") ? true
-                          : locEnv && !strcmp(locEnv, "big") ? false
-                                                              : nn <= (1ull << 29);
-  const bool hybrid = kHybridType && !counts && nPass >= 3 && (hyEnv == 1 || (hyEnv < 0 && sizeOk)) &&
+  const bool smallLocal = opt.localGeometry == THRS_LOCAL_SMALL ? true
+                          : (opt.localGeometry == THRS_LOCAL_BIG || opt.localGeometry == THRS_LOCAL_BIG32)
+                              ? false
+                              : nn <= (1ull << 29);
+  const bool bucket = kBucketType && !counts && nPass >= 3 &&
+                      (opt.path == THRS_PATH_BUCKET || (opt.path == THRS_PATH_AUTO && sizeOk)) &&
                       (VB == 0 || fullWindow);
   const int nLow = nPass - 2;
   // u32 keys over the whole key, large chunks: the local sort on 16-bit items
   // (thrs_hybrid.hpp thrs_local16) over single-bucket chunks
-  const bool local16 = hybrid && KT == 0 && VB == 0 && fullWindow && !smallLocal && loc16_enabled();
+  const bool local16 = bucket && KT == 0 && VB == 0 && fullWindow && !smallLocal &&
+                       opt.localGeometry != THRS_LOCAL_BIG32;
+  const bool segTop = opt.segmented != THRS_SEG_NONE;
+  const bool segA = opt.segmented == THRS_SEG_AUTO;
+  const bool atomicRank = opt.rank == THRS_RANK_ATOMIC ? true
+                          : opt.rank == THRS_RANK_BALLOT ? false
+                                                         : probe_rank_mode(stream) != 0;
+  // XCD-block claims (thrs_pass_xb) pay off where runs are short and the
+  // grid is large: 4-byte keys without values, n >= 2^29 (docs/EXPERIMENTS.md
+  // row 19: +4-6% there, neutral at 2^28, -2..-6% for pairs / f32 at 2^28).
+  const bool useXb = opt.tileClaims == THRS_CLAIMS_XCD_BLOCKS ? true
+                     : opt.tileClaims == THRS_CLAIMS_TICKET ? false
+                                                            : (sizeof(U) == 4 && VB == 0 && n >= (1u << 29));
+  uint32_t* sticky = sticky_dev();
+  if (!sticky) return THRS_ERROR_HIP;
+
+  // ---- kernels and their LDS opt-ins, before anything is enqueued
+  const size_t lds = G::LDS_BYTES;
+  auto kernel = useXb ? (atomicRank ? thrs_pass_xb<KT, VB, ST, true> : thrs_pass_xb<KT, VB, ST, false>)
+                      : (atomicRank ? thrs_pass<KT, VB, ST, true> : thrs_pass<KT, VB, ST, false>);
+  auto sk = atomicRank ? thrs_pass_seg<KT, VB, ST, true> : thrs_pass_seg<KT, VB, ST, false>;
+  const int histPasses = bucket ? nLow : nPass;
+  const size_t histLds = (size_t)histPasses * kBins * hist_copies<(int)sizeof(U)>() * 4;
+  if (allow_lds(thrs_hist<KT>, histLds) != hipSuccess || allow_lds(kernel, lds) != hipSuccess)
+    return THRS_ERROR_HIP;
+  if (bucket) {
+    if (allow_lds(thrs_hist_joint<KT>, kJointLds) != hipSuccess || allow_lds(sk, lds) != hipSuccess)
+      return THRS_ERROR_HIP;
+    if constexpr (kBucketType) {
+      if (local16) {
+        if constexpr (KT == 0 && VB == 0)
+          if (allow_lds(atomicRank ? thrs_local16<true, Loc16> : thrs_local16<false, Loc16>, Loc16::LDS) !=
+              hipSuccess)
+            return THRS_ERROR_HIP;
+      } else if constexpr (VB == 4) {
+        if (allow_lds(atomicRank ? thrs_local_pairs<true, LocBig> : thrs_local_pairs<false, LocBig>,
+                      LocBig::lds<U>()) != hipSuccess ||
+            allow_lds(atomicRank ? thrs_local_pairs<true, LocSmall> : thrs_local_pairs<false, LocSmall>,
+                      LocSmall::lds<U>()) != hipSuccess)
+          return THRS_ERROR_HIP;
+      } else {
+        if (allow_lds(atomicRank ? thrs_local<KT, true, LocBig> : thrs_local<KT, false, LocBig>, LocBig::lds<U>()) !=
+                hipSuccess ||
+            allow_lds(atomicRank ? thrs_local<KT, true, LocSmall> : thrs_local<KT, false, LocSmall>,
+                      LocSmall::lds<U>()) != hipSuccess)
+          return THRS_ERROR_HIP;
+      }
+    }
+  }
+  uint32_t grid = (uint32_t)plan.nTiles;
+  if (useXb) {
+    int perCU = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, kernel, G::THREADS, lds) != hipSuccess || perCU < 1)
+      perCU = 1;
+    grid = (uint32_t)std::min<uint64_t>(plan.nTiles, (uint64_t)perCU * cu_count());
+  }
+  int segPerCU = 0;
+  if (bucket &&
+      (hipOccupancyMaxActiveBlocksPerMultiprocessor(&segPerCU, sk, G::THREADS, lds) != hipSuccess || segPerCU < 1))
+    segPerCU = 1;
 
   // header (histograms, tile counters, error word) + first status table; the
-  // hybrid path with an odd number of (skippable) low passes starts on set 1
+  // bucket path with an odd number of (skippable) low passes starts on set 1
   // too, and zeroes its bucket histogram
-  const uint64_t sets = (hybrid && (nLow & 1)) ? 2 : 1;
+  const uint64_t sets = (bucket && (nLow & 1)) ? 2 : 1;
   if (hipMemsetAsync(scratch, 0, kHeaderBytes + sets * plan.setBytes, stream) != hipSuccess) return THRS_ERROR_HIP;
-  if (hybrid && hipMemsetAsync(joint, 0, kJointZero, stream) != hipSuccess) return THRS_ERROR_HIP;
+  if (bucket && hipMemsetAsync(joint, 0, kJointZero, stream) != hipSuccess) return THRS_ERROR_HIP;
   char* claim = scratch + kHeaderBytes + 2 * plan.setBytes;  // 8 per-pass claim areas
 
   {  // histograms of every pass in one read of the keys
     ProfScope prof(stream, 0);
     const int vec = (reinterpret_cast<uintptr_t>(keys) % 16) == 0;
     const uint64_t want = ((uint64_t)n + kHistThreads * 64 - 1) / (kHistThreads * 64);
-    const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cu_count() * THRS_HIST_GRID_MULT));
-    if (hybrid) {
-      if (allow_lds(thrs_hist_joint<KT>, kJointLds) != hipSuccess) return THRS_ERROR_HIP;
-      hipLaunchKernelGGL(thrs_hist_joint<KT>, dim3(grid), dim3(kHistThreads), kJointLds, stream,
+    const int hgrid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cu_count() * THRS_HIST_GRID_MULT));
+    if (bucket) {
+      hipLaunchKernelGGL(thrs_hist_joint<KT>, dim3(hgrid), dim3(kHistThreads), kJointLds, stream,
                          static_cast<const U*>(keys), n, orderMask, startBits + 8 * nLow, vec, joint,
                          reinterpret_cast<uint32_t*>(hyb + kSegHistAOff));
       // chunks: whole buckets; neighbouring buckets below kLocCap/2 keys share one
@@ -346,83 +393,50 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                          chunkB0, meta, smallLocal ? LocSmall::CAP : LocBig::CAP,
                          (VB || local16) ? -1 : (smallLocal ? kLocSmallLogT : kLocLogT),  // -1: single-bucket chunks
                          reinterpret_cast<uint32_t*>(hyb + kSegInfoOff), reinterpret_cast<uint32_t*>(hyb + kSegBaseOff),
-                         (uint32_t)G::TILE, reinterpret_cast<const uint32_t*>(hyb + kSegHistAOff), (uint32_t)grid,
+                         (uint32_t)G::TILE, reinterpret_cast<const uint32_t*>(hyb + kSegHistAOff), (uint32_t)hgrid,
                          reinterpret_cast<uint32_t*>(hyb + kSegInfoAOff), reinterpret_cast<uint32_t*>(hyb + kSegBaseAOff));
       // the low digits' histograms + bases: needed only on the fallback path
-      const size_t lds = (size_t)nLow * kBins * hist_copies<(int)sizeof(U)>() * 4;
-      if (allow_lds(thrs_hist<KT>, lds) != hipSuccess) return THRS_ERROR_HIP;
-      hipLaunchKernelGGL(thrs_hist<KT>, dim3(grid), dim3(kHistThreads), lds, stream, static_cast<const U*>(keys), n,
-                         orderMask, startBits, nLow, vec, hist, meta + kMetaFallback);
+      hipLaunchKernelGGL(thrs_hist<KT>, dim3(hgrid), dim3(kHistThreads), histLds, stream, static_cast<const U*>(keys),
+                         n, orderMask, startBits, nLow, vec, hist, meta + kMetaFallback);
       hipLaunchKernelGGL(thrs_scan, dim3(1), dim3(kThreads), 0, stream, hist, base, nLow, meta + kMetaFallback);
     } else {
-      const size_t lds = (size_t)nPass * kBins * hist_copies<(int)sizeof(U)>() * 4;
-      if (allow_lds(thrs_hist<KT>, lds) != hipSuccess) return THRS_ERROR_HIP;
-      hipLaunchKernelGGL(thrs_hist<KT>, dim3(grid), dim3(kHistThreads), lds, stream, static_cast<const U*>(keys), n,
-                         orderMask, startBits, nPass, vec, hist, nullptr);
+      hipLaunchKernelGGL(thrs_hist<KT>, dim3(hgrid), dim3(kHistThreads), histLds, stream, static_cast<const U*>(keys),
+                         n, orderMask, startBits, nPass, vec, hist, nullptr);
       hipLaunchKernelGGL(thrs_scan, dim3(1), dim3(kThreads), 0, stream, hist, base, nPass, nullptr);
     }
     if (counts && hipMemcpyAsync(counts, hist, kBins * sizeof(uint32_t), hipMemcpyDeviceToDevice, stream) != hipSuccess)
       return THRS_ERROR_HIP;
   }
 
-  const size_t lds = G::LDS_BYTES;
-  const bool atomicRank = probe_rank_mode(stream) != 0;
-  auto kernel = atomicRank ? thrs_pass<KT, VB, ST, true> : thrs_pass<KT, VB, ST, false>;
-  uint32_t grid = (uint32_t)plan.nTiles;
-  // XCD-block claims (thrs_pass_xb) pay off where runs are short and the
-  // grid is large: 4-byte keys without values, n >= 2^29 (docs/EXPERIMENTS.md
-  // row 19: +4-6% there, neutral at 2^28, -2..-6% for pairs / f32 at 2^28).
-  const int xbEnv = xb_override();  // THRS_XB=1 / 0 in the environment forces it on / off (tests)
-#ifdef THRS_XB_ALL
-  const bool useXb = true;  // experiment: every configuration
-  (void)xbEnv;
-#else
-  const bool useXb = xbEnv >= 0 ? xbEnv == 1 : (THRS_XB && sizeof(U) == 4 && VB == 0 && n >= (1u << 29));
-#endif
-  if (useXb) {
-    kernel = atomicRank ? thrs_pass_xb<KT, VB, ST, true> : thrs_pass_xb<KT, VB, ST, false>;
-    if (allow_lds(kernel, lds) != hipSuccess) return THRS_ERROR_HIP;
-    int perCU = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, kernel, G::THREADS, lds) != hipSuccess || perCU < 1)
-      perCU = 1;
-    grid = (uint32_t)std::min<uint64_t>(plan.nTiles, (uint64_t)perCU * cu_count());
-  }
-#if THRS_PIPE
-  if constexpr (G::ROUNDS == 1) {  // persistent: as many workgroups as fit at once
-    kernel = atomicRank ? thrs_pass_pipe<KT, VB, ST, true> : thrs_pass_pipe<KT, VB, ST, false>;
-    if (allow_lds(kernel, lds) != hipSuccess) return THRS_ERROR_HIP;
-    int perCU = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, kernel, G::THREADS, lds) != hipSuccess || perCU < 1)
-      perCU = 1;
-    grid = (uint32_t)std::min<uint64_t>(plan.nTiles, (uint64_t)perCU * cu_count());
-  }
-#endif
-  if (allow_lds(kernel, lds) != hipSuccess) return THRS_ERROR_HIP;
   if (useXb && hipMemsetAsync(claim, 0, (size_t)nPass * plan.claimBytes, stream) != hipSuccess)
     return THRS_ERROR_HIP;
 
   // pass p: digit at startBits + 8p, tables of set p&1; gate != nullptr runs
-  // it only if *gate == 1 (the hybrid path's fallback flag)
-  auto launch_pass = [&](int p, U* kin, U* kout, VW* vin, VW* vout, const uint32_t* gate) {
+  // it only if bit *gate of gateMask is set (meta words written by thrs_plan)
+  auto launch_pass = [&](int p, U* kin, U* kout, VW* vin, VW* vout, const uint32_t* gate, uint32_t gateMask) {
     const bool more = p + 1 < nPass;
     ST* next = more ? status[(p + 1) & 1] : nullptr;
     GroupTables<ST> g = grp[p & 1];
     g.gaNext = more ? grp[(p + 1) & 1].ga : nullptr;
     g.gpNext = more ? grp[(p + 1) & 1].gp : nullptr;
-    ProfScope prof(stream, gate ? 3 : 1);  // gated passes (hybrid fallback) are timed apart
+    ProfScope prof(stream, gate && gateMask == kGateFallback ? 3 : 1);  // fallback-only passes are timed apart
     hipLaunchKernelGGL(kernel, dim3(grid), dim3(G::THREADS), lds, stream, kin, kout, vin, vout, n, orderMask,
                        startBits + 8 * p, base + p * kBins, status[p & 1], next,
                        useXb ? reinterpret_cast<uint32_t*>(claim + p * plan.claimBytes) : counters + p, err, g,
-                       g_stamps ? g_stamps + (uint64_t)p * plan.nTiles * kStampSlots : nullptr, gate, 1u);
+                       g_stamps ? g_stamps + (uint64_t)p * plan.nTiles * kStampSlots : nullptr, gate, gateMask);
+  };
+  auto publish_error = [&]() -> int {
+    hipLaunchKernelGGL(thrs_err_publish, dim3(1), dim3(1), 0, stream, err, sticky);
+    return hipGetLastError() == hipSuccess ? THRS_SUCCESS : THRS_ERROR_HIP;
   };
 
-  if (!hybrid) {
+  if (!bucket) {
     U* kin = static_cast<U*>(keys);
     U* kout = keyOut;
     VW* vin = static_cast<VW*>(vals);
     VW* vout = valOut;
     for (int p = 0; p < nPass; ++p) {
-      launch_pass(p, kin, kout, vin, vout, nullptr);
+      launch_pass(p, kin, kout, vin, vout, nullptr, 0u);
       std::swap(kin, kout);
       std::swap(vin, vout);
     }
@@ -433,61 +447,63 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
       if (VB && hipMemcpyAsync(vals, valOut, (size_t)n * VB, hipMemcpyDeviceToDevice, stream) != hipSuccess)
         return THRS_ERROR_HIP;
     }
-    return THRS_SUCCESS;
+    return publish_error();
   }
 
-  // ---- hybrid: fallback-only low passes, then the two top digits, then local
-  if constexpr (kHybridType) {
+  // ---- bucket path: fallback-only low passes, the two top digits, local sort
+  if constexpr (kBucketType) {
     U* K = static_cast<U*>(keys);
     VW* V = static_cast<VW*>(vals);
+    uint32_t* fallback = meta + kMetaFallback;
+    uint32_t* mode = meta + kMetaMode;
     {
       U* kin = K;
       U* kout = keyOut;
       VW* vin = V;
       VW* vout = valOut;
       for (int p = 0; p < nLow; ++p) {
-        launch_pass(p, kin, kout, vin, vout, meta + kMetaFallback);
+        launch_pass(p, kin, kout, vin, vout, fallback, kGateFallback);
         std::swap(kin, kout);
         std::swap(vin, vout);
       }
       if (nLow & 1) {  // fallback result is in keyOut: the top-digit passes read K
         hipLaunchKernelGGL(thrs_copy_gated, dim3(2048), dim3(256), 0, stream,
                            reinterpret_cast<const uint32_t*>(keyOut), reinterpret_cast<uint32_t*>(K), (uint64_t)n,
-                           meta + kMetaFallback, 1u);
+                           fallback, 1u);
         if (VB)
           hipLaunchKernelGGL(thrs_copy_gated, dim3(2048), dim3(256), 0, stream,
                              reinterpret_cast<const uint32_t*>(valOut), reinterpret_cast<uint32_t*>(V),
-                             (uint64_t)n * VB / 4, meta + kMetaFallback, 1u);
+                             (uint64_t)n * VB / 4, fallback, 1u);
       }
     }
-    // the two top digits: XCD-segmented passes (thrs_kernels.hpp
+    // The two top digits: XCD-segmented passes (thrs_kernels.hpp
     // thrs_pass_seg) -- the second digit over position segments (the bucket
-    // histogram's workgroup ranges), the top digit over second-digit ranges
-    auto sk = atomicRank ? thrs_pass_seg<KT, VB, ST, true> : thrs_pass_seg<KT, VB, ST, false>;
-    if (allow_lds(sk, lds) != hipSuccess) return THRS_ERROR_HIP;
-    int segPerCU = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&segPerCU, sk, G::THREADS, lds) != hipSuccess || segPerCU < 1)
-      segPerCU = 1;
+    // histogram's workgroup ranges), the top digit over second-digit ranges.
+    // Gates on meta[kMetaMode]: mode 0 (local path) the segmented second-digit
+    // pass, mode 1 (fallback) the plain one (the position segments' counts are
+    // those of the INPUT order, not the low passes' output), mode 2 (one
+    // bucket holds every key: both top digits constant) neither, and no
+    // top-digit pass either (both are identities, and skipping both keeps the
+    // result in K).
     auto launch_seg = [&](int p, U* kin, U* kout, VW* vin, VW* vout, uint64_t infoOff, uint64_t baseOff,
-                          const uint32_t* gate, uint32_t want) {
+                          const uint32_t* gate, uint32_t gateMask) {
       ProfScope prof(stream, 1);
       hipLaunchKernelGGL(sk, dim3((uint32_t)segPerCU * cu_count()), dim3(G::THREADS), lds, stream, kin, kout, vin,
                          vout, orderMask, startBits + 8 * p, reinterpret_cast<uint32_t*>(hyb + infoOff),
-                         reinterpret_cast<const uint32_t*>(hyb + baseOff), status[p & 1], err, grp[p & 1], gate, want);
+                         reinterpret_cast<const uint32_t*>(hyb + baseOff), status[p & 1], err, grp[p & 1], gate,
+                         gateMask);
     };
     const uint64_t sw = plan.wideStatus ? 8 : 4;
     const int setB = (nLow + 1) & 1;
-    if (seg_a_enabled()) {
-      // The position segments' digit counts are those of the INPUT order:
-      // after the fallback's low passes the plain pass runs instead (both
-      // gated on the flag).  The table set is clean either way: zeroed up
-      // front, or rows [0, nTiles) cleared by the last fallback pass.  Neither
-      // clears rows for the top-digit pass: zero that set.
-      launch_seg(nLow, K, keyOut, V, valOut, kSegInfoAOff, kSegBaseAOff, meta + kMetaFallback, 0u);
-      launch_pass(nLow, K, keyOut, V, valOut, meta + kMetaFallback);
+    if (segA) {
+      // The table set is clean either way: zeroed up front, or rows [0,
+      // nTiles) cleared by the last fallback pass.  Neither clears rows for
+      // the top-digit pass: zero that set.
+      launch_seg(nLow, K, keyOut, V, valOut, kSegInfoAOff, kSegBaseAOff, mode, kGateMode0);
+      launch_pass(nLow, K, keyOut, V, valOut, mode, kGateMode1);
       if (hipMemsetAsync(status[setB], 0, plan.setBytes, stream) != hipSuccess) return THRS_ERROR_HIP;
     } else {
-      launch_pass(nLow, K, keyOut, V, valOut, nullptr);
+      launch_pass(nLow, K, keyOut, V, valOut, mode, kGateMode0 | kGateMode1);
       // the segmented pass's tile ids reach past nTiles (per-segment
       // rounding): clear those rows (pass nLow cleared rows [0, nTiles))
       const uint64_t nGroups0 = (plan.nTiles + kGroup - 1) / kGroup;
@@ -498,74 +514,71 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                          stream) != hipSuccess)
         return THRS_ERROR_HIP;
     }
-    if (seg_enabled())
-      launch_seg(nLow + 1, keyOut, K, valOut, V, kSegInfoOff, kSegBaseOff, nullptr, 0u);
+    if (segTop)
+      launch_seg(nLow + 1, keyOut, K, valOut, V, kSegInfoOff, kSegBaseOff, mode, kGateMode0 | kGateMode1);
     else
-      launch_pass(nLow + 1, keyOut, K, valOut, V, nullptr);
+      launch_pass(nLow + 1, keyOut, K, valOut, V, mode, kGateMode0 | kGateMode1);
     {
       ProfScope prof(stream, 2);
       // never more workgroups than chunks can exist: <= 256 (one per top digit)
       // + 2 per non-empty bucket, and <= the number of buckets
       const uint64_t maxChunks = std::min<uint64_t>(kBuckets, 256 + 2 * (uint64_t)n);
-      auto launch_local = [&](auto geom) -> int {
+      auto launch_local = [&](auto geom) {
         using LG = decltype(geom);
         const size_t llds = LG::template lds<U>();
         if constexpr (VB == 4) {
           auto lk = atomicRank ? thrs_local_pairs<true, LG> : thrs_local_pairs<false, LG>;
-          if (allow_lds(lk, llds) != hipSuccess) return THRS_ERROR_HIP;
           hipLaunchKernelGGL(lk, dim3((uint32_t)maxChunks), dim3(LG::THREADS), llds, stream,
                              reinterpret_cast<uint32_t*>(K), reinterpret_cast<uint32_t*>(V), (uint32_t)orderMask,
                              chunkOff, chunkB0, meta);
         } else {
           auto lk = atomicRank ? thrs_local<KT, true, LG> : thrs_local<KT, false, LG>;
-          if (allow_lds(lk, llds) != hipSuccess) return THRS_ERROR_HIP;
-          int perCU = 0;
-          if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, lk, LG::THREADS, llds) != hipSuccess || perCU < 1)
-            perCU = 1;
-          const uint32_t lgrid = THRS_LOC_PERSIST ? (uint32_t)std::min<uint64_t>(maxChunks, (uint64_t)perCU * cu_count())
-                                                  : (uint32_t)maxChunks;
-          hipLaunchKernelGGL(lk, dim3(lgrid), dim3(LG::THREADS), llds, stream, K, orderMask, startBits, nLow,
-                             chunkOff, chunkB0, meta, g_lstamps);
+          hipLaunchKernelGGL(lk, dim3((uint32_t)maxChunks), dim3(LG::THREADS), llds, stream, K, orderMask, startBits,
+                             nLow, chunkOff, chunkB0, meta, g_lstamps);
         }
-        return THRS_SUCCESS;
       };
       if (local16) {
         if constexpr (KT == 0 && VB == 0) {
           auto lk = atomicRank ? thrs_local16<true, Loc16> : thrs_local16<false, Loc16>;
-          const char* padEnv = getenv("THRS_LOC16_LDS");  // EXPERIMENT: more LDS per workgroup (fewer per CU)
-          const size_t l16 = padEnv ? std::max<size_t>(Loc16::LDS, (size_t)atol(padEnv)) : Loc16::LDS;
-          if (allow_lds(lk, l16) != hipSuccess) return THRS_ERROR_HIP;
-          hipLaunchKernelGGL(lk, dim3((uint32_t)maxChunks), dim3(Loc16::THREADS), l16, stream,
+          hipLaunchKernelGGL(lk, dim3((uint32_t)maxChunks), dim3(Loc16::THREADS), Loc16::LDS, stream,
                              reinterpret_cast<uint32_t*>(K), (uint32_t)orderMask, chunkOff, chunkB0, meta);
         }
+      } else if (smallLocal) {
+        launch_local(LocSmall{});
       } else {
-        const int rc = smallLocal ? launch_local(LocSmall{}) : launch_local(LocBig{});
-        if (rc) return rc;
+        launch_local(LocBig{});
       }
     }
     if (hipGetLastError() != hipSuccess) return THRS_ERROR_HIP;
   }
-  return THRS_SUCCESS;
+  return publish_error();
 }
 
 template <int KT, int VB>
 int run_st(void* keys, void* vals, uint32_t n, void* tmp, void* ko, void* vo, int startBits, int nPass, bool desc,
-           const Plan& plan, hipStream_t stream, uint32_t* counts) {
+           const Plan& plan, const thrs_options& opt, hipStream_t stream, uint32_t* counts) {
   if (plan.wideStatus)
-    return run_sort<KT, VB, uint64_t>(keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, stream, counts);
-  return run_sort<KT, VB, uint32_t>(keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, stream, counts);
+    return run_sort<KT, VB, uint64_t>(keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, opt, stream, counts);
+  return run_sort<KT, VB, uint32_t>(keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, opt, stream, counts);
 }
 
 template <int KT>
 int run_vb(int vb, void* keys, void* vals, uint32_t n, void* tmp, void* ko, void* vo, int startBits, int nPass,
-           bool desc, const Plan& plan, hipStream_t stream, uint32_t* counts = nullptr) {
+           bool desc, const Plan& plan, const thrs_options& opt, hipStream_t stream, uint32_t* counts = nullptr) {
   switch (vb) {
-    case 0: return run_st<KT, 0>(keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, stream, counts);
-    case 4: return run_st<KT, 4>(keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, stream, counts);
-    case 8: return run_st<KT, 8>(keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, stream, counts);
-    case 16: return run_st<KT, 16>(keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, stream, counts);
+    case 0: return run_st<KT, 0>(keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, opt, stream, counts);
+    case 4: return run_st<KT, 4>(keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, opt, stream, counts);
+    case 8: return run_st<KT, 8>(keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, opt, stream, counts);
+    case 16: return run_st<KT, 16>(keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, opt, stream, counts);
   }
   return THRS_ERROR_INVALID_VALUE;
+}
+
+bool valid_options(const thrs_options& o) {
+  return o.path >= THRS_PATH_AUTO && o.path <= THRS_PATH_BUCKET && o.localGeometry >= THRS_LOCAL_AUTO &&
+         o.localGeometry <= THRS_LOCAL_BIG32 && o.segmented >= THRS_SEG_AUTO && o.segmented <= THRS_SEG_NONE &&
+         o.tileClaims >= THRS_CLAIMS_AUTO && o.tileClaims <= THRS_CLAIMS_TICKET && o.rank >= THRS_RANK_AUTO &&
+         o.rank <= THRS_RANK_BALLOT;
 }
 
 // Scratch is sized for the larger of the keys-only and pairs tile plans so
@@ -581,8 +594,12 @@ int temp_def(int keyType, int valueType, uint32_t n, thrs_temp_def* out) {
   return THRS_SUCCESS;
 }
 
-int sort_impl(const thrs_config* cfg, void* keys, void* vals, bool pairs, uint32_t n, void* tmp, int startBits,
-              int endBits, hipStream_t stream) {
+int sort_impl(const thrs_config* cfg, const thrs_options* options, void* keys, void* vals, bool pairs, uint32_t n,
+              void* tmp, int startBits, int endBits, hipStream_t stream) {
+  // a failure of an earlier sort on this device is reported first (and cleared)
+  if (take_sticky()) return THRS_ERROR_LOOKBACK_TIMEOUT;
+  const thrs_options opt = options ? *options : thrs_options{};
+  if (!valid_options(opt)) return THRS_ERROR_INVALID_VALUE;
   if (!cfg || !valid_key(cfg->keyType) || (pairs && !valid_value(cfg->valueType))) return THRS_ERROR_INVALID_VALUE;
   if (cfg->sortOrder != THRS_ORDER_ASCENDING && cfg->sortOrder != THRS_ORDER_DESCENDING) return THRS_ERROR_INVALID_VALUE;
   if (((endBits - startBits) % 8) != 0) return THRS_ERROR_BIT_RANGE;  // tinyhipradixsort.hpp:856
@@ -606,16 +623,17 @@ int sort_impl(const thrs_config* cfg, void* keys, void* vals, bool pairs, uint32
   void* ko = static_cast<char*>(tmp) + def.pSumBuffer;
   void* vo = static_cast<char*>(tmp) + def.pSumBuffer + def.keyOutBuffer;
   switch (cfg->keyType) {
-    case THRS_KEY_U32: return run_vb<0>(vb, keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, stream);
-    case THRS_KEY_U64: return run_vb<1>(vb, keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, stream);
-    case THRS_KEY_F32: return run_vb<2>(vb, keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, stream);
-    case THRS_KEY_F64: return run_vb<3>(vb, keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, stream);
+    case THRS_KEY_U32: return run_vb<0>(vb, keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, opt, stream);
+    case THRS_KEY_U64: return run_vb<1>(vb, keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, opt, stream);
+    case THRS_KEY_F32: return run_vb<2>(vb, keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, opt, stream);
+    case THRS_KEY_F64: return run_vb<3>(vb, keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, opt, stream);
   }
   return THRS_ERROR_INVALID_VALUE;
 }
 
 int partition_impl(const thrs_config* cfg, const void* keysIn, const void* valsIn, uint32_t n, void* tmp,
                    void* keysOut, void* valsOut, int bitLocation, uint32_t* counts, hipStream_t stream) {
+  if (take_sticky()) return THRS_ERROR_LOOKBACK_TIMEOUT;
   if (!cfg || !valid_key(cfg->keyType)) return THRS_ERROR_INVALID_VALUE;
   if (cfg->sortOrder != THRS_ORDER_ASCENDING && cfg->sortOrder != THRS_ORDER_DESCENDING) return THRS_ERROR_INVALID_VALUE;
   const bool pairs = valsIn != nullptr;
@@ -628,13 +646,14 @@ int partition_impl(const thrs_config* cfg, const void* keysIn, const void* valsI
   const int vb = pairs ? value_bytes_of(cfg->valueType) : 0;
   const Plan plan = make_plan(cfg->keyType, vb, n);
   const bool desc = cfg->sortOrder == THRS_ORDER_DESCENDING;
+  const thrs_options opt{};
   void* ki = const_cast<void*>(keysIn);
   void* vi = const_cast<void*>(valsIn);
   switch (cfg->keyType) {
-    case THRS_KEY_U32: return run_vb<0>(vb, ki, vi, n, tmp, keysOut, valsOut, bitLocation, 1, desc, plan, stream, counts);
-    case THRS_KEY_U64: return run_vb<1>(vb, ki, vi, n, tmp, keysOut, valsOut, bitLocation, 1, desc, plan, stream, counts);
-    case THRS_KEY_F32: return run_vb<2>(vb, ki, vi, n, tmp, keysOut, valsOut, bitLocation, 1, desc, plan, stream, counts);
-    case THRS_KEY_F64: return run_vb<3>(vb, ki, vi, n, tmp, keysOut, valsOut, bitLocation, 1, desc, plan, stream, counts);
+    case THRS_KEY_U32: return run_vb<0>(vb, ki, vi, n, tmp, keysOut, valsOut, bitLocation, 1, desc, plan, opt, stream, counts);
+    case THRS_KEY_U64: return run_vb<1>(vb, ki, vi, n, tmp, keysOut, valsOut, bitLocation, 1, desc, plan, opt, stream, counts);
+    case THRS_KEY_F32: return run_vb<2>(vb, ki, vi, n, tmp, keysOut, valsOut, bitLocation, 1, desc, plan, opt, stream, counts);
+    case THRS_KEY_F64: return run_vb<3>(vb, ki, vi, n, tmp, keysOut, valsOut, bitLocation, 1, desc, plan, opt, stream, counts);
   }
   return THRS_ERROR_INVALID_VALUE;
 }
@@ -668,13 +687,23 @@ THRS_API int thrs_get_temporary_buffer_bytes(const thrs_config* cfg, uint32_t n,
 }
 
 THRS_API int thrs_sort_keys(const thrs_config* config, void* keys, uint32_t n, void* tmp, int startBits, int endBits,
-                   hipStream_t stream) {
-  return sort_impl(config, keys, nullptr, false, n, tmp, startBits, endBits, stream);
+                            hipStream_t stream) {
+  return sort_impl(config, nullptr, keys, nullptr, false, n, tmp, startBits, endBits, stream);
 }
 
 THRS_API int thrs_sort_pairs(const thrs_config* config, void* keys, void* values, uint32_t n, void* tmp, int startBits,
-                    int endBits, hipStream_t stream) {
-  return sort_impl(config, keys, values, true, n, tmp, startBits, endBits, stream);
+                             int endBits, hipStream_t stream) {
+  return sort_impl(config, nullptr, keys, values, true, n, tmp, startBits, endBits, stream);
+}
+
+THRS_API int thrs_sort_keys_ex(const thrs_config* config, const thrs_options* options, void* keys, uint32_t n,
+                               void* tmp, int startBits, int endBits, hipStream_t stream) {
+  return sort_impl(config, options, keys, nullptr, false, n, tmp, startBits, endBits, stream);
+}
+
+THRS_API int thrs_sort_pairs_ex(const thrs_config* config, const thrs_options* options, void* keys, void* values,
+                                uint32_t n, void* tmp, int startBits, int endBits, hipStream_t stream) {
+  return sort_impl(config, options, keys, values, true, n, tmp, startBits, endBits, stream);
 }
 
 THRS_API int thrs_partition_pass(const thrs_config* config, const void* keysIn, const void* valuesIn, uint32_t n,
@@ -690,8 +719,14 @@ THRS_API int thrs_check_device_error(void* tmp, hipStream_t stream) {
           hipSuccess ||
       hipStreamSynchronize(stream) != hipSuccess)
     return THRS_ERROR_HIP;
-  return err ? THRS_ERROR_LOOKBACK_TIMEOUT : THRS_SUCCESS;
+  if (err) {
+    (void)take_sticky();  // reported here: the next sort does not repeat it
+    return THRS_ERROR_LOOKBACK_TIMEOUT;
+  }
+  return THRS_SUCCESS;
 }
+
+THRS_API int thrs_take_device_error(void) { return take_sticky() ? THRS_ERROR_LOOKBACK_TIMEOUT : THRS_SUCCESS; }
 
 THRS_API int thrs_profile_enable(int enable) {
   std::lock_guard<std::mutex> g(g_prof_mu);

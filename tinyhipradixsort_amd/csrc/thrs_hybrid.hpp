@@ -35,29 +35,37 @@
 namespace thrs_dev {
 
 constexpr uint32_t kBuckets = 65536;  // 16-bit bucket = the window's top two digits
-enum { kMetaChunks = 0, kMetaFallback = 1 };
+// meta[kMetaMode]: 0 = local path (no bucket above the local capacity);
+// 1 = fallback: plain LSD passes; 2 = fallback and ONE bucket holds every key,
+// so both top digits are constant and their passes are identities (skipped)
+enum { kMetaChunks = 0, kMetaFallback = 1, kMetaMode = 3 };
+// gate masks of the gated launches: bit v set = run when the gate word is v
+constexpr uint32_t kGateFallback = 1u << 1;  // on meta[kMetaFallback]: fallback only
+constexpr uint32_t kGateMode0 = 1u << 0, kGateMode1 = 1u << 1, kGateMode2 = 1u << 2;  // on meta[kMetaMode]
 
 // ------------------------------------------------------------ joint histogram
 // LDS: bucket counts as 15-bit fields, two per word (bits 0-14 | guard 15 |
 // 16-30 | guard 31): 128 KiB for 65536 buckets.  The add that carries a field
-// into its guard bit (field was 0x7FFF) clears the guard again and moves 32768
-// to the global count, so no carry ever reaches the neighbouring field and
-// any skew is counted exactly.  (The two top digits' histograms are the row
-// and column sums of this one: thrs_plan.)
+// into its guard bit clears the guard again and moves 32768 to the global
+// count; with at most 32768 increments per barrier epoch (thrs_hist_joint) no
+// carry can reach the neighbouring field, so any skew is counted exactly.
+// (The two top digits' histograms are the row and column sums of this one:
+// thrs_plan.)
 #ifndef THRS_LOC_STORE_HOIST
 #define THRS_LOC_STORE_HOIST 1  // local sort write-out: all stage reads before the stores
-#endif
-#ifndef THRS_LOC_RANKFIRST
-#define THRS_LOC_RANKFIRST 0  // EXPERIMENT: rank into zeroed counters, no counting pass (slower: EXPERIMENTS.md row 38)
 #endif
 #ifndef THRS_HJ_UN
 #define THRS_HJ_UN 4  // 16-byte loads in flight per lane
 #endif
-#ifndef THRS_HJ_NORTN
-#define THRS_HJ_NORTN 0
-#endif
 constexpr uint32_t kJointWords = kBuckets / 2;
-constexpr size_t kJointLds = (size_t)kJointWords * 4 + kBins * 4;  // + the range's second-digit counts
+// Carries (32768 keys of one bucket) are logged in LDS and flushed once per
+// distinct bucket at the end: a constant input would otherwise send every
+// workgroup's carries to ONE global word (~32K same-address atomics at C2).
+// A workgroup of len keys carries at most len / 32768 times (128 at C2);
+// past kCarryLog entries carries go straight to global memory.
+constexpr uint32_t kCarryLog = 1024;
+// s_joint[kJointWords] | s_d2[256] (the range's second-digit counts) | s_log[kCarryLog] | s_logN
+constexpr size_t kJointLds = (size_t)kJointWords * 4 + kBins * 4 + kCarryLog * 4 + 16;
 
 // Workgroup i of the bucket histogram reads the contiguous key range
 // [i*len, (i+1)*len) (len a multiple of 4: 16-byte loads stay aligned), and
@@ -80,46 +88,68 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
   using U = typename KeyTraits<KT>::U;
   extern __shared__ __attribute__((aligned(16))) uint32_t s_joint[];
   uint32_t* s_d2 = s_joint + kJointWords;
+  uint32_t* s_log = s_d2 + kBins;
+  uint32_t* s_logN = s_log + kCarryLog;
   const uint32_t tid = threadIdx.x;
   for (uint32_t i = tid; i < kJointWords + kBins; i += kHistThreads) s_joint[i] = 0;
+  if (tid == 0) *s_logN = 0;
   __syncthreads();
   const uint64_t len = hj_len(n, gridDim.x);
   const uint64_t lo = min((uint64_t)n, (uint64_t)blockIdx.x * len), hi = min((uint64_t)n, lo + len);
   uint32_t* segH = segHist + (blockIdx.x * kSegs / gridDim.x) * kBins;
 
+  const uint32_t lane = tid & 63;
   auto bucket_of = [&](U k) -> uint32_t {
     return (uint32_t)((KeyTraits<KT>::bits(k) ^ orderMask) >> bucketShift) & 0xFFFFu;
   };
-  auto add = [&](uint32_t b) -> uint32_t {
-#if THRS_HJ_NORTN  // EXPERIMENT: no-return LDS atomics, no overflow check (exact only below 32768 per bin and WG)
-    __hip_atomic_fetch_add(&s_joint[b >> 1], 1u << ((b & 1u) << 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    return 0u;
-#endif
-    return __hip_atomic_fetch_add(&s_joint[b >> 1], 1u << ((b & 1u) << 4), __ATOMIC_RELAXED,
+  // Adds are wave-aggregated as in wave_count_items (sorted input would
+  // otherwise make every add a 64-way same-address conflict): a wave whose 16
+  // elements all fall in one bucket adds 1024 from lane 0; elements whose
+  // bucket is uniform over the wave add 64 from lane 0; the rest add 1 per lane.
+  auto add = [&](uint32_t b, uint32_t inc) -> uint32_t {
+    return __hip_atomic_fetch_add(&s_joint[b >> 1], inc << ((b & 1u) << 4), __ATOMIC_RELAXED,
                                   __HIP_MEMORY_SCOPE_WORKGROUP);
   };
-  auto check = [&](uint32_t b, uint32_t old) {
+  // The add that carried the field from below 0x8000 to 0x8000 or above
+  // (guard bit set) takes 0x8000 back out and credits it globally.
+  auto check = [&](uint32_t b, uint32_t old, uint32_t inc) {
     const uint32_t sh = (b & 1u) << 4;
-    if (((old >> sh) & 0x7FFFu) == 0x7FFFu) {  // this add set the guard bit
+    const uint32_t f = (old >> sh) & 0xFFFFu;
+    if (inc && f < 0x8000u && f + inc >= 0x8000u) {
       __hip_atomic_fetch_sub(&s_joint[b >> 1], 0x8000u << sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      atomicAdd(&joint[b], 0x8000u);
-      atomicAdd(&segH[b & 255u], 0x8000u);
+      const uint32_t slot = __hip_atomic_fetch_add(s_logN, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (slot < kCarryLog) {
+        s_log[slot] = b;
+      } else {
+        atomicAdd(&joint[b], 0x8000u);
+        atomicAdd(&segH[b & 255u], 0x8000u);
+      }
     }
   };
-
+  // Exactness bound: between two workgroup barriers the workgroup adds at
+  // most kEpoch = 32768 increments, and every carry of the epoch has been
+  // taken out (lgkmcnt(0)) before its barrier.  So an epoch starts with every
+  // field below 0x8000 and ends at most at 0x7FFF + 0x8000 = 0xFFFF: no carry
+  // ever reaches the neighbouring field, whatever the skew or the wave
+  // scheduling.  Iteration counts are uniform over the workgroup (lanes past
+  // the range are masked), so every wave meets every barrier.
+  constexpr uint32_t kEpoch = 32768;
   constexpr uint64_t gstride = kHistThreads;  // the workgroup's own range
   uint64_t tailStart = lo;
-  if (vec) {  // 16-byte loads, 4 in flight per lane (keys base 16-B aligned, checked on host)
+  if (vec) {  // 16-byte loads, UN in flight per lane (keys base 16-B aligned, checked on host)
     constexpr int PER = 16 / sizeof(U);
     constexpr int UN = THRS_HJ_UN;
-    const uint64_t nv = hi / PER;
+    constexpr uint32_t ITERS_PER_EPOCH = kEpoch / (kHistThreads * UN * PER);
+    static_assert(ITERS_PER_EPOCH >= 1, "one iteration must fit an epoch");
+    const uint64_t v0 = lo / PER, nv = hi / PER;   // lo is a multiple of 4 (hj_len)
     const uint4* kv = reinterpret_cast<const uint4*>(keys);
-    uint64_t i = lo / PER + tid;
-    for (; i + (UN - 1) * gstride < nv; i += UN * gstride) {
+    const uint64_t nIter = nv > v0 ? (nv - v0 + UN * gstride - 1) / (UN * gstride) : 0;
+    for (uint64_t it = 0; it < nIter; ++it) {
+      const uint64_t i = v0 + it * UN * gstride + tid;
       uint4 q[UN];
 #pragma unroll
-      for (int u = 0; u < UN; ++u) q[u] = kv[i + u * gstride];
-      uint32_t b[UN * PER], o[UN * PER];
+      for (int u = 0; u < UN; ++u) q[u] = (i + u * gstride < nv) ? kv[i + u * gstride] : uint4{0, 0, 0, 0};
+      uint32_t b[UN * PER], o[UN * PER] = {}, inc[UN * PER];
 #pragma unroll
       for (int u = 0; u < UN; ++u) {
         if constexpr (sizeof(U) == 4) {
@@ -132,39 +162,72 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
           b[u * 2 + 1] = bucket_of(((uint64_t)q[u].w << 32) | q[u].z);
         }
       }
+      constexpr int E = UN * PER;
+      if (v0 + (it + 1) * UN * gstride <= nv) {  // every element of every lane is in the range
+        uint32_t b0;
+        const uint32_t mode = wave_mode<E>([&](int e) { return b[e]; }, E, b0);
+        if (mode == kAllUniform) {
+          if (lane == 0) check(b0, add(b0, 64u * E), 64u * E);
+        } else if (mode == kMixed) {
 #pragma unroll
-      for (int e = 0; e < UN * PER; ++e) o[e] = add(b[e]);
+          for (int e = 0; e < E; ++e) o[e] = add(b[e], 1u);
 #pragma unroll
-      for (int e = 0; e < UN * PER; ++e) check(b[e], o[e]);
-    }
-    for (; i < nv; i += gstride) {
-      const uint4 q = kv[i];
-      uint32_t b[PER];
-      if constexpr (sizeof(U) == 4) {
-        b[0] = bucket_of(q.x); b[1] = bucket_of(q.y); b[2] = bucket_of(q.z); b[3] = bucket_of(q.w);
+          for (int e = 0; e < E; ++e) check(b[e], o[e], 1u);
+        } else {
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            const bool uni = wave_uniform(b[e]);
+            inc[e] = uni ? (lane == 0 ? 64u : 0u) : 1u;
+            if (inc[e]) o[e] = add(b[e], inc[e]);
+          }
+#pragma unroll
+          for (int e = 0; e < E; ++e) check(b[e], o[e], inc[e]);
+        }
       } else {
-        b[0] = bucket_of(((uint64_t)q.y << 32) | q.x);
-        b[1] = bucket_of(((uint64_t)q.w << 32) | q.z);
-      }
 #pragma unroll
-      for (int e = 0; e < PER; ++e) check(b[e], add(b[e]));
+        for (int e = 0; e < E; ++e) {
+          inc[e] = (i + (e / PER) * gstride < nv) ? 1u : 0u;
+          if (inc[e]) o[e] = add(b[e], 1u);
+        }
+#pragma unroll
+        for (int e = 0; e < E; ++e) check(b[e], o[e], inc[e]);
+      }
+      if ((it + 1) % ITERS_PER_EPOCH == 0) lds_barrier();
     }
     tailStart = max(lo, nv * PER);
   }
-  for (uint64_t i = tailStart + tid; i < hi; i += gstride) {
-    const uint32_t b = bucket_of(keys[i]);
-    check(b, add(b));
+  {  // scalar keys (unaligned base, and the < PER keys past the last 16-B word)
+    const uint64_t nIter = hi > tailStart ? (hi - tailStart + gstride - 1) / gstride : 0;
+    constexpr uint32_t ITERS_PER_EPOCH = kEpoch / kHistThreads;
+    for (uint64_t it = 0; it < nIter; ++it) {
+      const uint64_t i = tailStart + it * gstride + tid;
+      if (i < hi) {
+        const uint32_t b = bucket_of(keys[i]);
+        check(b, add(b, 1u), 1u);
+      }
+      if ((it + 1) % ITERS_PER_EPOCH == 0) lds_barrier();
+    }
   }
   __syncthreads();
+  // logged carries: the first log entry of each bucket flushes all of them
+  const uint32_t nLog = min(*s_logN, kCarryLog);
+  for (uint32_t t = tid; t < nLog; t += kHistThreads) {
+    const uint32_t b = s_log[t];
+    uint32_t mult = 0;
+    bool first = true;
+    for (uint32_t u = 0; u < nLog; ++u) {
+      const uint32_t x = s_log[u];
+      mult += x == b;
+      first = first && !(x == b && u < t);
+    }
+    if (first) {
+      atomicAdd(&joint[b], mult * 0x8000u);
+      atomicAdd(&segH[b & 255u], mult * 0x8000u);
+    }
+  }
   for (uint32_t i = tid; i < kBuckets; i += kHistThreads) {
     const uint32_t c = (s_joint[i >> 1] >> ((i & 1u) << 4)) & 0xFFFFu;
     if (c) atomicAdd(&joint[i], c);
-#ifdef THRS_HJ_FLUSH3  // EXPERIMENT: two more flushes (net zero) to price the flush
-    if (c) {
-      atomicAdd(&joint[i], c);
-      atomicSub(&joint[i], c);
-    }
-#endif
   }
   // the range's second-digit counts (column sums; lanes d, d+1 share a word)
   static_assert(kHistThreads == 4 * kBins, "four top-digit quarters per second digit");
@@ -222,13 +285,17 @@ __global__ __launch_bounds__(kPlanThreads) void thrs_plan(const uint32_t* __rest
   // bucket 4096w + 64i + l, so every load and every chunk-table store is
   // lane-consecutive; prefixes in bucket order come from wave scans.
   constexpr int WAVES = kPlanThreads / 64, STEPS = (int)kBuckets / kPlanThreads;  // 16, 64
-  __shared__ uint32_t s_col[WAVES][kBins], s_row[kBins], s_wsum[WAVES], s_wopen[WAVES], s_wlast[WAVES], s_flag;
+  __shared__ uint32_t s_col[WAVES][kBins], s_row[kBins], s_wsum[WAVES], s_wopen[WAVES], s_wlast[WAVES], s_flag, s_one;
   // top-digit histogram of every second-digit segment [32s, 32s+32) (the
   // segmented top-digit pass, thrs_pass_seg) and the second digit's bases
   __shared__ uint32_t s_seg[kSegs][kBins], s_b2[kBins];
   const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const uint32_t* src = joint + w * (64 * STEPS) + lane;
-  if (tid == 0) s_flag = 0;
+  if (tid == 0) {
+    s_flag = 0;
+    s_one = 0;
+  }
+  __syncthreads();  // before any wave can set them (a wave may finish sweep 1 before wave 0 starts)
   // logT < 0: single-bucket chunks (every non-empty bucket, and every bucket
   // after one, opens a chunk); else T = 2^logT (a shift, not a division)
   const bool single = logT < 0;
@@ -242,7 +309,7 @@ __global__ __launch_bounds__(kPlanThreads) void thrs_plan(const uint32_t* __rest
   // sweep 1: wave totals, the fallback test, row (top digit) and column
   // (second digit) sums.  Bucket 4096w + 64i + l: row 16w + i/4, column 64(i%4) + l.
   uint32_t tot = 0, col[4] = {0, 0, 0, 0};
-  bool big = false;
+  bool big = false, one = false;
 #pragma unroll 8
   for (int q4 = 0; q4 < STEPS / 4; ++q4) {
     uint32_t rs = 0;
@@ -250,6 +317,7 @@ __global__ __launch_bounds__(kPlanThreads) void thrs_plan(const uint32_t* __rest
     for (int q = 0; q < 4; ++q) {
       const uint32_t x = src[64 * (4 * q4 + q)];
       big |= x > cap;
+      one |= x == n;
       col[q] += x;
       rs += x;
       // bucket (top 16w + q4, second 64q + l): segment 2q + l/32, one half-wave each
@@ -271,6 +339,7 @@ __global__ __launch_bounds__(kPlanThreads) void thrs_plan(const uint32_t* __rest
   if (lane == 0) s_wsum[w] = tot;
   if (lane == 63) s_wlast[w] = src[64 * (STEPS - 1)];
   if (big) s_flag = 1;
+  if (one) s_one = 1;
   __syncthreads();
   uint32_t wbase = 0;
   for (uint32_t ww = 0; ww < w; ++ww) wbase += s_wsum[ww];
@@ -387,17 +456,13 @@ __global__ __launch_bounds__(kPlanThreads) void thrs_plan(const uint32_t* __rest
     chunkB0[nChunks] = kBuckets;
     meta[kMetaChunks] = nChunks;
     meta[kMetaFallback] = s_flag;
-    meta[2] = 0;  // kMetaClaim: the persistent local sort's chunk counter
+    meta[kMetaMode] = s_flag ? (s_one ? 2u : 1u) : 0u;
   }
 }
 
 // ------------------------------------------------------------- local sort
-// Persistent workgroups (one per CU, 16 waves), each looping over chunks
-// claimed from a counter; the NEXT chunk's keys are loaded into registers
-// while the current one is sorted in LDS, so HBM traffic and LDS work overlap
-// (the LDS rounds are bank-conflict bound: ~9 random-address LDS ops per key).
-//
-// Per chunk: KPT keys per lane in registers (item j of lane l of wave w =
+// One workgroup per chunk (a persistent form with next-chunk prefetch was
+// slower: docs/EXPERIMENTS.md).  Per chunk: KPT keys per lane in registers (item j of lane l of wave w =
 // chunk position w*64*KPT + j*64 + l, the order the stable rank walks -- as
 // in pass_tile).  Each round: per-wave digit counts (LDS atomics) -> one wave
 // scans the 256 digits and turns the counts into per-wave running offsets ->
@@ -416,9 +481,6 @@ __global__ __launch_bounds__(kPlanThreads) void thrs_plan(const uint32_t* __rest
 #define THRS_LOC_CFG 8, 36  // waves, keys per lane of the large geometry: 2 workgroups per CU
 #endif
 constexpr int kLocCfg[2] = {THRS_LOC_CFG};
-#ifndef THRS_LOC_PERSIST
-#define THRS_LOC_PERSIST 0  // 1: persistent workgroups with next-chunk prefetch; 0: one workgroup per chunk
-#endif
 // Local-sort geometry: WAVES waves x KPT keys per lane = CAP slots per chunk.
 //   LocBig   8 x 36 = 18432 keys, 2 WGs / CU (72 KiB stage + 8 KiB counters):
 //            buckets of 2^30-key sorts (~16K keys)
@@ -437,7 +499,6 @@ constexpr uint32_t kLocCap = LocBig::CAP;  // 18432 keys
 // geometry serves never merge (a merged chunk's bucket round has few distinct
 // digits, i.e. same-address atomics)
 constexpr int kLocLogT = 12, kLocSmallLogT = 11;
-enum { kMetaClaim = 2 };
 template <typename U> constexpr size_t local_lds_bytes() { return LocBig::lds<U>(); }
 
 // raw 4-byte key whose getKeyBits image is y (inverse of KeyTraits::bits, for
@@ -546,13 +607,8 @@ __device__ __forceinline__ int loc_rounds(typename KeyTraits<KT>::U (&k)[LG::KPT
   // part in any round: they rank after every real key, so skipping them
   // changes no real key's slot (scalar test: limw is wave-uniform)
   const int32_t limw = __builtin_amdgcn_readfirstlane((int32_t)ch.size - (int32_t)(w * CHUNK));
-#if defined(THRS_LOC_EXP) && THRS_LOC_EXP == 2
-  const int roundsRun = ch.rounds > 0 ? 1 : 0;  // EXPERIMENT ONLY (wrong output): one round
-#elif defined(THRS_LOC_EXP) && THRS_LOC_EXP == 1
-  const int roundsRun = 0;  // EXPERIMENT ONLY (wrong output): no rounds
-#else
+  const int nItems = limw <= 0 ? 0 : min(KPT, (limw + 63) >> 6);  // items j with j*64 < limw
   const int roundsRun = ch.rounds;
-#endif
   for (int r = 0; r < roundsRun; ++r) {
     const int shift = r < nLow ? startBits + 8 * r : startBits + 8 * nLow;
     const uint32_t sub = r < nLow ? 0u : ch.b0;
@@ -561,39 +617,12 @@ __device__ __forceinline__ int loc_rounds(typename KeyTraits<KT>::U (&k)[LG::KPT
     };
 #pragma unroll
     for (int i = 0; i < kBins / 64; ++i) cnt[i * 64 + lane] = 0;
-#if THRS_LOC_RANKFIRST
-    // rank first, into the wave's zeroed counters (lane-ordered atomics:
-    // items in (j, lane) order = chunk order); the counters then hold the
-    // wave's digit counts, the scan turns them into the wave's digit offsets,
-    // and the scatter adds offset and rank -- a broadcast-friendly read per
-    // key instead of a separate counting atomic
-    constexpr int NP = (KPT + 1) / 2;
-    uint32_t rk[NP];  // two 16-bit ranks per register (ranks < 64 * KPT)
-#pragma unroll
-    for (int q = 0; q < NP; ++q) rk[q] = 0;
-#pragma unroll
-    for (int j = 0; j < KPT; ++j) {
-      if (j * 64 < limw) {
-        const uint32_t dj = digit_of(k[j]);
-        uint32_t x;
-        if constexpr (ATOMIC_RANK) {
-          x = __hip_atomic_fetch_add(&cnt[dj], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        } else {
-          uint32_t mlo, mhi;
-          match_digit(dj, mlo, mhi);
-          const uint32_t cc = cnt[dj];
-          x = __builtin_amdgcn_mbcnt_hi(mhi, __builtin_amdgcn_mbcnt_lo(mlo, cc));
-          cnt[dj] = __builtin_popcount(mhi) + __builtin_popcount(mlo) + cc;
-        }
-        rk[j >> 1] |= x << ((j & 1) * 16);
-      }
-    }
-#else
+    // (no wave aggregation here: these kernels sit at their VGPR limit, and
+    // the inputs that make a local round's digits wave-uniform -- constant
+    // low bytes -- are rare; sorted input is not among them)
 #pragma unroll
     for (int j = 0; j < KPT; ++j)
-      if (j * 64 < limw)
-        __hip_atomic_fetch_add(&cnt[digit_of(k[j])], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#endif
+      if (j < nItems) __hip_atomic_fetch_add(&cnt[digit_of(k[j])], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     lds_barrier();
     {  // threads d < 256: digit d's total over the waves -> block exclusive scan
        // (wave totals through stage words: the stage is free between the
@@ -630,46 +659,19 @@ __device__ __forceinline__ int loc_rounds(typename KeyTraits<KT>::U (&k)[LG::KPT
 #define THRS_LOC_RB 12
 #endif
     constexpr int RB = THRS_LOC_RB;
-#if THRS_LOC_RANKFIRST
 #pragma unroll
     for (int j0 = 0; j0 < KPT; j0 += RB) {
       uint32_t sl[RB];
 #pragma unroll
       for (int jj = 0; jj < RB; ++jj) {
         const int j = j0 + jj;
-        if (j < KPT && j * 64 < limw) sl[jj] = cnt[digit_of(k[j])] + ((rk[j >> 1] >> ((j & 1) * 16)) & 0xFFFFu);
+        if (j < KPT && j < nItems) sl[jj] = wave_rank<ATOMIC_RANK>(cnt, digit_of(k[j]), lane, false);
       }
 #pragma unroll
       for (int jj = 0; jj < RB; ++jj)
-        if (j0 + jj < KPT && (j0 + jj) * 64 < limw) stage[sl[jj]] = k[j0 + jj];
+        if (j0 + jj < KPT && j0 + jj < nItems) stage[sl[jj]] = k[j0 + jj];
       __builtin_amdgcn_sched_barrier(0);
     }
-#else
-#pragma unroll
-    for (int j0 = 0; j0 < KPT; j0 += RB) {
-      uint32_t sl[RB];
-#pragma unroll
-      for (int jj = 0; jj < RB; ++jj) {
-        const int j = j0 + jj;
-        if (j < KPT && j * 64 < limw) {
-          const uint32_t dj = digit_of(k[j]);
-          if constexpr (ATOMIC_RANK) {
-            sl[jj] = __hip_atomic_fetch_add(&cnt[dj], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          } else {
-            uint32_t mlo, mhi;
-            match_digit(dj, mlo, mhi);
-            const uint32_t cc = cnt[dj];
-            sl[jj] = __builtin_amdgcn_mbcnt_hi(mhi, __builtin_amdgcn_mbcnt_lo(mlo, cc));
-            cnt[dj] = __builtin_popcount(mhi) + __builtin_popcount(mlo) + cc;
-          }
-        }
-      }
-#pragma unroll
-      for (int jj = 0; jj < RB; ++jj)
-        if (j0 + jj < KPT && (j0 + jj) * 64 < limw) stage[sl[jj]] = k[j0 + jj];
-      __builtin_amdgcn_sched_barrier(0);
-    }
-#endif
     lds_barrier();
     loc_stamp(st, 2 + (r & 1));
     if (r + 1 < roundsRun) {
@@ -735,61 +737,27 @@ __global__ __launch_bounds__(LG::THREADS) void thrs_local(typename KeyTraits<KT>
   if (meta[kMetaFallback] != 0) return;  // the plain LSD passes sorted everything
   const uint32_t nChunks = meta[kMetaChunks];
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-#if !THRS_LOC_PERSIST
-  {
-    const uint32_t c = blockIdx.x;
-    if (c >= nChunks) return;
-    uint64_t* st = stamps ? stamps + (uint64_t)c * kLocStampSlots : nullptr;
-    loc_stamp(st, 0);
-    const LocChunk ch = loc_chunk<KT>(c, nLow, chunkOff, chunkB0);
-    if (ch.size == 0) return;
-    U k[LG::KPT];
-    loc_load<KT, LG>(k, keys, ch, loc_pad<KT>(ch.b0, nLow, startBits, (uint32_t)orderMask));
-#ifdef THRS_STAMPS
-    if (st) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      loc_stamp(st, 1);
-      if (threadIdx.x == 0) {
-        uint32_t hw, xcc;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-        st[6] = hw;
-        st[7] = xcc_id();
-      }
-    }
-#endif
-    loc_sort_chunk<KT, ATOMIC_RANK, LG>(k, keys, ch, orderMask, startBits, nLow, smem, st);
-    return;
-  }
-#endif
-  // the claimed chunk id is handed over in stage word 0: free between a
-  // chunk's write-out (its reads end at the barrier before the claim) and the
-  // next chunk's first scan (every thread has read the id by then)
-  uint32_t* s_claim = reinterpret_cast<uint32_t*>(smem);
-  auto claim = [&]() -> uint32_t {  // one barrier; callers are past every read of the previous claim
-    if (threadIdx.x == 0) *s_claim = atomicAdd(&meta[kMetaClaim], 1u);
-    lds_barrier();
-    return __builtin_amdgcn_readfirstlane(*s_claim);
-  };
-  uint32_t c = claim();
+  const uint32_t c = blockIdx.x;
   if (c >= nChunks) return;
-  LocChunk ch = loc_chunk<KT>(c, nLow, chunkOff, chunkB0);
+  uint64_t* st = stamps ? stamps + (uint64_t)c * kLocStampSlots : nullptr;
+  loc_stamp(st, 0);
+  const LocChunk ch = loc_chunk<KT>(c, nLow, chunkOff, chunkB0);
+  if (ch.size == 0) return;
   U k[LG::KPT];
   loc_load<KT, LG>(k, keys, ch, loc_pad<KT>(ch.b0, nLow, startBits, (uint32_t)orderMask));
-  for (;;) {
-    const uint32_t cn = claim();
-    U kn[LG::KPT];
-    LocChunk chn{};
-    if (cn < nChunks) {  // next chunk's loads in flight during this chunk's LDS rounds
-      chn = loc_chunk<KT>(cn, nLow, chunkOff, chunkB0);
-      loc_load<KT, LG>(kn, keys, chn, loc_pad<KT>(chn.b0, nLow, startBits, (uint32_t)orderMask));
+#ifdef THRS_STAMPS
+  if (st) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    loc_stamp(st, 1);
+    if (threadIdx.x == 0) {
+      uint32_t hw;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+      st[6] = hw;
+      st[7] = xcc_id();
     }
-    if (ch.size) loc_sort_chunk<KT, ATOMIC_RANK, LG>(k, keys, ch, orderMask, startBits, nLow, smem);
-    if (cn >= nChunks) break;
-    lds_barrier();  // every wave is past the write-out's stage reads
-#pragma unroll
-    for (int j = 0; j < LG::KPT; ++j) k[j] = kn[j];
-    ch = chn;
   }
+#endif
+  loc_sort_chunk<KT, ATOMIC_RANK, LG>(k, keys, ch, orderMask, startBits, nLow, smem, st);
 }
 
 // ------------------------------------------------- local sort, 16-bit items
@@ -801,10 +769,17 @@ __global__ __launch_bounds__(LG::THREADS) void thrs_local(typename KeyTraits<KT>
 // The rounds are those of loc_rounds (count, scan, lane-ordered rank,
 // scatter, reload) on 16-bit items; the keys are rebuilt on the way out.
 // u32 only: f32 keys' +0 and -0 share one image.
+// The stage is padded by one word (two items) per 64 items: item slot s lives
+// at (s / 64) * 66 + s % 64.  Structured inputs scatter with regular strides
+// (sorted keys: a wave's 64 slots ~288 apart, all on 2 of the 32 store banks);
+// the pad spreads them.  A wave's 64 consecutive slots stay contiguous.
 template <int W, int K> struct Loc16G {
   static constexpr int WAVES = W, KPT = K, THREADS = 64 * W, NP = (K + 1) / 2;
   static constexpr uint32_t CAP = (uint32_t)THREADS * K;
-  static constexpr size_t LDS = (size_t)CAP * 2 + (size_t)W * kBins * 4;
+  static constexpr uint32_t ROW = 66;                                // u16 slots per 64 items
+  static constexpr size_t STAGE_BYTES = (size_t)(CAP / 64) * ROW * 2;
+  static constexpr size_t LDS = STAGE_BYTES + (size_t)W * kBins * 4;
+  __device__ static uint32_t at(uint32_t s) { return (s >> 6) * ROW + (s & 63u); }
 };
 using Loc16 = Loc16G<8, 36>;
 static_assert(Loc16::CAP == LocBig::CAP, "same chunk capacity as the 32-bit geometry (thrs_plan's cap)");
@@ -824,14 +799,15 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(6))
   const uint32_t hiBits = chunkB0[c] << 16;  // the bucket: the image's top 16 bits
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint16_t* stage = reinterpret_cast<uint16_t*>(smem);
-  uint32_t* s_cnt = reinterpret_cast<uint32_t*>(smem + (size_t)LG::CAP * 2);  // [waves][256]
+  uint32_t* s_cnt = reinterpret_cast<uint32_t*>(smem + LG::STAGE_BYTES);  // [waves][256]
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6);
   uint32_t* cnt = s_cnt + w * kBins;
-  const uint16_t* stw = stage + w * CHUNK + lane;
+  const uint16_t* stw = stage + w * KPT * LG::ROW + lane;  // item j of this lane: stw[j * ROW]
   int32_t lim = (int32_t)size - (int32_t)(w * CHUNK + lane);
   pin(reinterpret_cast<uint32_t&>(lim));
   const int32_t limw = __builtin_amdgcn_readfirstlane((int32_t)size - (int32_t)(w * CHUNK));
+  const int nItems = limw <= 0 ? 0 : min(KPT, (limw + 63) >> 6);  // items j with j*64 < limw
   uint32_t* src = keys + start + w * CHUNK + lane;
 
   // items: low 16 bits of the image, two per register; padding 0xFFFF ranks
@@ -857,8 +833,7 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(6))
     for (int i = 0; i < kBins / 64; ++i) cnt[i * 64 + lane] = 0;
 #pragma unroll
     for (int j = 0; j < KPT; ++j)
-      if (j * 64 < limw)
-        __hip_atomic_fetch_add(&cnt[digit_of(j)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (j < nItems) __hip_atomic_fetch_add(&cnt[digit_of(j)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     lds_barrier();
     {  // digit totals over the waves -> block exclusive scan -> per-wave running offsets
       uint32_t* s_wt = reinterpret_cast<uint32_t*>(smem);  // stage words: free until the scatter
@@ -891,30 +866,19 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(6))
 #pragma unroll
       for (int jj = 0; jj < RB; ++jj) {
         const int j = j0 + jj;
-        if (j < KPT && j * 64 < limw) {
-          const uint32_t dj = digit_of(j);
-          if constexpr (ATOMIC_RANK) {
-            sl[jj] = __hip_atomic_fetch_add(&cnt[dj], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          } else {
-            uint32_t mlo, mhi;
-            match_digit(dj, mlo, mhi);
-            const uint32_t cc = cnt[dj];
-            sl[jj] = __builtin_amdgcn_mbcnt_hi(mhi, __builtin_amdgcn_mbcnt_lo(mlo, cc));
-            cnt[dj] = __builtin_popcount(mhi) + __builtin_popcount(mlo) + cc;
-          }
-        }
+        if (j < KPT && j < nItems) sl[jj] = wave_rank<ATOMIC_RANK>(cnt, digit_of(j), lane, false);
       }
 #pragma unroll
       for (int jj = 0; jj < RB; ++jj)
-        if (j0 + jj < KPT && (j0 + jj) * 64 < limw) stage[sl[jj]] = (uint16_t)item(j0 + jj);
+        if (j0 + jj < KPT && j0 + jj < nItems) stage[LG::at(sl[jj])] = (uint16_t)item(j0 + jj);
       __builtin_amdgcn_sched_barrier(0);
     }
     lds_barrier();
     if (r == 0) {
 #pragma unroll
       for (int j = 0; j < KPT; j += 2) {
-        const uint32_t a = (j * 64 < limw) ? (uint32_t)stw[j * 64] : 0xFFFFu;
-        const uint32_t b = (j + 1 < KPT && (j + 1) * 64 < limw) ? (uint32_t)stw[(j + 1) * 64] : 0xFFFFu;
+        const uint32_t a = (j * 64 < limw) ? (uint32_t)stw[j * LG::ROW] : 0xFFFFu;
+        const uint32_t b = (j + 1 < KPT && (j + 1) * 64 < limw) ? (uint32_t)stw[(j + 1) * LG::ROW] : 0xFFFFu;
         it[j >> 1] = a | (b << 16);
       }
     }
@@ -923,7 +887,7 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(6))
   // stores: a read inside the condition would be waited for one at a time
   uint32_t o[KPT];
 #pragma unroll
-  for (int j = 0; j < KPT; ++j) o[j] = stw[j * 64];
+  for (int j = 0; j < KPT; ++j) o[j] = stw[j * LG::ROW];
 #pragma unroll
   for (int j = 0; j < KPT; ++j)
     if (j * 64 < lim) src[j * 64] = (hiBits | o[j]) ^ orderMask;

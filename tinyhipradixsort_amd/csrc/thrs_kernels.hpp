@@ -116,6 +116,106 @@ __device__ __forceinline__ void match_digit(uint32_t d, uint32_t& mlo, uint32_t&
   }
 }
 
+// ---- wave-aggregated LDS counting and ranking.  Conflicting lanes of one
+// LDS atomic are serviced one per cycle: when all 64 lanes of a wave carry the
+// same digit (sorted, reverse-sorted and constant inputs do this on most
+// items) a per-lane atomic costs 64 cycles of the CU's LDS pipe.  A wave
+// classifies its N items once (wave_mode, scalar result):
+//   kAllUniform  every item of every lane has the digit d0: one atomic of
+//                64*N for the whole wave, slots base + 64j + lane;
+//   kSomeUniform its first or last item is uniform (a wave straddling a digit
+//                boundary of sorted input): each item is tested (one ballot)
+//                and a uniform one takes one atomic of 64 from lane 0;
+//   kMixed       random input: one atomic per lane and item, no extra test.
+// Every lane of the wave is active in all of these.
+enum : uint32_t { kMixed = 0, kSomeUniform = 1, kAllUniform = 2 };
+
+__device__ __forceinline__ bool wave_uniform(uint32_t d) {
+  const uint32_t d0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)d);
+  return __ballot(d == d0) == ~0ull;
+}
+// items j in [0, nItems) (wave-uniform, >= 1) take part; d0 = item 0's digit in lane 0
+template <int N, typename F>
+__device__ __forceinline__ uint32_t wave_mode(F digit, int nItems, uint32_t& d0) {
+  d0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)digit(0));
+  uint32_t diff = 0;
+#pragma unroll
+  for (int j = 0; j < N; ++j)
+    if (j < nItems) diff |= digit(j) ^ d0;
+  if (__ballot(diff != 0) == 0) return kAllUniform;
+  bool some = wave_uniform(digit(0));
+#pragma unroll
+  for (int j = 1; j < N; ++j)
+    if (j == nItems - 1) some = some || wave_uniform(digit(j));
+  return some ? kSomeUniform : kMixed;
+}
+
+// true iff digit(j) is the same for every j < N in every lane; d0 = that digit
+template <int N, typename F>
+__device__ __forceinline__ bool wave_all_uniform(F digit, uint32_t& d0) {
+  d0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)digit(0));
+  uint32_t diff = 0;
+#pragma unroll
+  for (int j = 0; j < N; ++j) diff |= digit(j) ^ d0;
+  return __ballot(diff != 0) == 0;
+}
+
+// cnt[d] += 1 for every lane; uni: d is the same in every lane
+__device__ __forceinline__ void wave_count(uint32_t* cnt, uint32_t d, uint32_t lane, bool uni) {
+  if (uni) {
+    if (lane == 0) __hip_atomic_fetch_add(&cnt[d], 64u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  } else {
+    __hip_atomic_fetch_add(&cnt[d], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+}
+// count items j in [0, nItems) of every lane, by mode
+template <int N, typename F>
+__device__ __forceinline__ void wave_count_items(uint32_t* cnt, uint32_t mode, uint32_t d0, uint32_t lane, F digit,
+                                                 int nItems) {
+  if (mode == kAllUniform) {
+    if (lane == 0)
+      __hip_atomic_fetch_add(&cnt[d0], 64u * (uint32_t)nItems, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  } else if (mode == kSomeUniform) {
+#pragma unroll
+    for (int j = 0; j < N; ++j)
+      if (j < nItems) wave_count(cnt, digit(j), lane, wave_uniform(digit(j)));
+  } else {
+#pragma unroll
+    for (int j = 0; j < N; ++j)
+      if (j < nItems) __hip_atomic_fetch_add(&cnt[digit(j)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+}
+
+// Stable rank of this lane's item among the wave's items with the same digit,
+// added to (and advancing) the wave's running counter cnt[d]: the returned
+// slot.  ATOMIC_RANK: one ds_add_rtn_u32 per lane, whose conflicting lanes
+// return in lane order on gfx950 (probed per device, thrs_probe_lds_order);
+// otherwise the 8-ballot match.  uni: slot = base + lane.
+template <bool ATOMIC_RANK>
+__device__ __forceinline__ uint32_t wave_rank(uint32_t* cnt, uint32_t d, uint32_t lane, bool uni) {
+  if (uni) {
+    uint32_t old = 0;
+    if (lane == 0) old = __hip_atomic_fetch_add(&cnt[d], 64u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return (uint32_t)__builtin_amdgcn_readlane((int)old, 0) + lane;
+  }
+  if constexpr (ATOMIC_RANK) {
+    return __hip_atomic_fetch_add(&cnt[d], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  } else {
+    uint32_t mlo, mhi;
+    match_digit(d, mlo, mhi);
+    const uint32_t c = cnt[d];
+    const uint32_t slot = __builtin_amdgcn_mbcnt_hi(mhi, __builtin_amdgcn_mbcnt_lo(mlo, c));
+    cnt[d] = __builtin_popcount(mhi) + __builtin_popcount(mlo) + c;
+    return slot;
+  }
+}
+// kAllUniform: the wave's N items take slots base .. base + 64N (one atomic)
+__device__ __forceinline__ uint32_t wave_rank_all(uint32_t* cnt, uint32_t d0, uint32_t lane, uint32_t items) {
+  uint32_t old = 0;
+  if (lane == 0) old = __hip_atomic_fetch_add(&cnt[d0], 64u * items, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  return (uint32_t)__builtin_amdgcn_readlane((int)old, 0);
+}
+
 // Inclusive scan over the 64 lanes of a wave, in DPP (no LDS round trips:
 // __shfl_up compiles to ds_bpermute, ~100+ cycles each): row_shr 1, 2, 4, 8
 // scan each row of 16 lanes, then row_bcast:15 / row_bcast:31 carry rows
@@ -264,6 +364,15 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+// Bound on the polls of a look-back or tile-claim wait (each poll sleeps ~64
+// clocks): hitting it sets the sort's error word (thrs_capi.h "Device-side
+// failures") instead of hanging the GPU.  -DTHRS_SPIN_MAX=0 builds the
+// fault-injection library of the error-path tests (libthrs_spin0.so).
+#ifndef THRS_SPIN_MAX
+#define THRS_SPIN_MAX (1u << 22)
+#endif
+constexpr uint32_t kSpinMax = THRS_SPIN_MAX;
+
 // Look-back window: predecessors read per round trip.
 #ifndef THRS_LOOK_WINDOW
 #define THRS_LOOK_WINDOW 8
@@ -377,7 +486,8 @@ template <int KB, int VB> struct PassGeom {
   static constexpr int THREADS = 64 * WAVES;
   static constexpr uint32_t TILE = (uint32_t)THREADS * KPT;
   static constexpr uint32_t STAGE = TILE / ROUNDS;
-  static constexpr uint32_t LDS_BYTES = STAGE * (KB + VB) + (WAVES + 1) * kBins * 4 + 16 * 4 + kStampLds;
+  // stage | s_cnt[WAVES][256] | s_gofs[256] | s_misc[16] | stamps | s_sink[WAVES][64]
+  static constexpr uint32_t LDS_BYTES = STAGE * (KB + VB) + (WAVES + 1) * kBins * 4 + 16 * 4 + kStampLds + WAVES * 64 * 4;
   static_assert(TILE <= 65536, "slots are kept as 16-bit halves");
   static_assert(kGroup == 0 || (uint64_t)kGroup * TILE < kArrival, "group counts must fit below the arrival bits");
   static_assert((STAGE & (STAGE - 1)) == 0 && STAGE % THREADS == 0, "stage must be a power of two");
@@ -498,7 +608,7 @@ struct GroupWalk {
       }
 #endif
       if (stall && walking()) {
-        if (++spins > (1u << 22)) {  // bounded spin: never hang the GPU
+        if (++spins > kSpinMax) {  // bounded spin: never hang the GPU
           atomicOr(errFlag, 1u);
           break;
         }
@@ -637,11 +747,32 @@ __device__ __forceinline__ void pass_tile(
     return dd;
   };
 
-  // ---- B: per-wave histogram (order-free LDS atomics) -> tile counts
+  // ---- B: per-wave histogram (order-free LDS atomics) -> tile counts.
+  // A wave whose every item has one digit (sorted / constant input: one LDS
+  // atomic per key would be a 64-way same-address conflict) points its
+  // per-key atomics at a private sink word per lane instead (conflict-free)
+  // and adds 64*KPT to the digit once; slots are then base + 64j + lane.
+  // Branch-free selects: this kernel is at the VGPR limit.
   uint32_t* cnt = s_cnt + w * kBins;
+  uint32_t* sink = s_misc + 16 + kStampLds / 4 + w * 64 + lane;
+  // hint: items 0 and KPT-1 carry one digit d0 in every lane (sorted input);
+  // the count loop verifies the others, and a wrong hint recounts (rare).
+  const uint32_t d0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)digit_of(k[0], 0));
+  const bool hint = full && __ballot(digit_of(k[0], 0) != d0 || digit_of(k[KPT - 1], KPT - 1) != d0) == 0;
+  uint32_t diff = 0;
 #pragma unroll
-  for (int j = 0; j < KPT; ++j)
-    __hip_atomic_fetch_add(&cnt[digit_of(k[j], j)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  for (int j = 0; j < KPT; ++j) {
+    const uint32_t dj = digit_of(k[j], j);
+    diff |= dj ^ d0;
+    __hip_atomic_fetch_add(hint ? sink : &cnt[dj], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  const bool allU = hint && __ballot(diff != 0) == 0;
+  if (hint && !allU) {  // some item differs: count for real
+#pragma unroll
+    for (int j = 0; j < KPT; ++j)
+      __hip_atomic_fetch_add(&cnt[digit_of(k[j], j)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  if (allU && lane == 0) __hip_atomic_fetch_add(&cnt[d0], 64u * KPT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   lds_barrier();
   THRS_STAMP(2);
 
@@ -715,54 +846,43 @@ __device__ __forceinline__ void pass_tile(
   THRS_STAMP(3);
 
   // ---- C: stable rank = running per-wave offset + same-digit keys in lower
-  // lanes of the item.  ATOMIC_RANK: one ds_add_rtn_u32 per key -- with every
-  // lane active, conflicting lanes of one LDS atomic are serviced in lane
-  // order on gfx950, so the returned counter IS the stable slot (verified at
-  // run time per device by thrs_probe_lds_order; otherwise the ballot match).
+  // lanes of the item (wave_rank: one ds_add_rtn_u32 per key, or one per
+  // wave when its digit is uniform; the ballot match without ATOMIC_RANK).
+  // all-uniform wave: item j of lane l takes slot base + 64j + l, base = the
+  // wave's running offset of d0 (a broadcast read); its atomics hit the sink
   uint32_t sl[(KPT + 1) / 2];  // final slots, two 16-bit halves per register
 #pragma unroll
   for (int j = 0; j < (KPT + 1) / 2; ++j) sl[j] = 0;
+  const uint32_t ubase = (uint32_t)__builtin_amdgcn_readfirstlane((int)cnt[d0]);  // scalar
 #pragma unroll
   for (int j = 0; j < KPT; ++j) {
     pin(k[j]);  // keep item j's digit/address math inside iteration j (register pressure)
-    const uint32_t dj = digit_of(k[j], j);
     uint32_t slot;
     if constexpr (ATOMIC_RANK) {
-      slot = __hip_atomic_fetch_add(&cnt[dj], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      slot = __hip_atomic_fetch_add(allU ? sink : &cnt[digit_of(k[j], j)], 1u, __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_WORKGROUP);
     } else {
-      uint32_t mlo, mhi;
-      match_digit(dj, mlo, mhi);
-      const uint32_t c = cnt[dj];
-      slot = __builtin_amdgcn_mbcnt_hi(mhi, __builtin_amdgcn_mbcnt_lo(mlo, c));
-      cnt[dj] = __builtin_popcount(mhi) + __builtin_popcount(mlo) + c;
+      slot = wave_rank<false>(cnt, digit_of(k[j], j), lane, false);
     }
-    sl[j / 2] |= slot << (16 * (j & 1));
-    pin(sl[j / 2]);  // materialise the slot now (else it is sunk to phase E, keeping masks alive)
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  THRS_STAMP(4);
-  if constexpr (ROUNDS == 1) {
-    // one LDS round: place the tile in sorted order now, freeing the key
-    // registers before the walk (the post-walk barrier orders it for E)
-#pragma unroll
-    for (int j = 0; j < KPT; ++j) {
-      const uint32_t slot = (sl[j / 2] >> (16 * (j & 1))) & 0xFFFFu;
+    slot = allU ? ubase + 64u * j + lane : slot;
+    if constexpr (ROUNDS == 1) {
+      // one LDS round: place the key in sorted order now (frees its register
+      // before the walk; the post-walk barrier orders it for phase E)
       stage_k[slot] = k[j];
       if constexpr (VB != 0) stage_v[slot] = v[j];
+    } else {
+      sl[j / 2] |= slot << (16 * (j & 1));
+      pin(sl[j / 2]);  // materialise the slot now (else it is sunk to phase E, keeping masks alive)
     }
+    __builtin_amdgcn_sched_barrier(0);
   }
+  auto slot_of = [&](int j) -> uint32_t { return (sl[j / 2] >> (16 * (j & 1))) & 0xFFFFu; };
+  THRS_STAMP(4);
 
 
   // ---- D: decoupled look-back for digit d, kLookWindow rows per round trip;
   // a not-yet-published word stops the window and is re-polled.
-#ifdef THRS_FAKE_WALK
-  // EXPERIMENT ONLY (wrong output): no look-back; offsets approximated from
-  // this tile's own counts (uniform keys -> nearly the real write pattern)
-  if (tid < 256) s_gofs[d] = myBase + tile * realTot - localStart;
-  if (false) {
-#else
   if constexpr (kGroup > 0) {
-#endif
     if (tid < 256) gw.finish(THRS_EARLY_WINDOW && tile != 0, realTot, myBase, localStart, s_gofs, s_misc, errFlag,
                              stamps);
 #if !THRS_LATE_CLEAR
@@ -806,7 +926,7 @@ __device__ __forceinline__ void pass_tile(
         }
         if (done) break;
         if (stall) {
-          if (++spins > (1u << 22)) {  // bounded spin: never hang the GPU
+          if (++spins > kSpinMax) {  // bounded spin: never hang the GPU
             atomicOr(errFlag, 1u);
             break;
           }
@@ -847,7 +967,7 @@ __device__ __forceinline__ void pass_tile(
 #endif
 #pragma unroll
       for (int j = 0; j < KPT; ++j) {
-        const uint32_t slot = (sl[j / 2] >> (16 * (j & 1))) & 0xFFFFu;
+        const uint32_t slot = slot_of(j);
         if ((slot >> STAGE_SHIFT) == (uint32_t)r) {
 #if THRS_RELOAD_KEYS
           // padding items of a partial tile (j*64 >= lim) lie past n: never read them
@@ -869,11 +989,7 @@ __device__ __forceinline__ void pass_tile(
       if (full || slot < valid) {
         const U key = stage_k[i];
         const uint32_t dd = (uint32_t)((KeyTraits<KT>::bits(key) ^ orderMask) >> shift) & 0xFFu;
-#ifdef THRS_FAKE_WALK
-        const uint32_t dst = min(s_gofs[dd] + slot, (uint32_t)(keyStart + valid - 1));  // stay in bounds
-#else
         const uint32_t dst = s_gofs[dd] + slot;
-#endif
         keysOut[dst] = key;
         if constexpr (VB != 0) valsOut[dst] = stage_v[i];
       }
@@ -923,8 +1039,8 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
     uint32_t n, typename KeyTraits<KT>::U orderMask, int shift, const uint32_t* __restrict__ digitBase,
     ST* __restrict__ status, ST* __restrict__ statusNext, uint32_t* __restrict__ tileCounter,
     uint32_t* __restrict__ errFlag, GroupTables<ST> grp, uint64_t* __restrict__ stamps,
-    const uint32_t* __restrict__ gate, uint32_t gateWant) {
-  if (gate && *gate != gateWant) return;  // pass not needed on this launch path (thrs_plan decides)
+    const uint32_t* __restrict__ gate, uint32_t gateMask) {
+  if (gate && !((gateMask >> *gate) & 1u)) return;  // not needed on this launch path (thrs_plan decides)
   using G = PassGeom<sizeof(typename KeyTraits<KT>::U), VB>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint32_t* s_cnt = reinterpret_cast<uint32_t*>(smem + G::STAGE * (sizeof(typename KeyTraits<KT>::U) + VB));
@@ -934,12 +1050,7 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
 #endif
   const uint32_t tid = threadIdx.x;
   if (tid == 0) {
-#if defined(THRS_FAKE_WALK) && defined(THRS_FAKE_STATIC_TILE)
-    s_misc[0] = blockIdx.x;  // EXPERIMENT ONLY: no walk, so no wait: static ids cannot deadlock
-    (void)tileCounter;
-#else
     s_misc[0] = atomicAdd(tileCounter, 1u);
-#endif
     s_misc[1] = s_misc[2] = s_misc[3] = 0;  // diagnostic maxima (THRS_STAMPS)
   }
   for (uint32_t i = tid; i < (uint32_t)(G::WAVES * kBins); i += G::THREADS) s_cnt[i] = 0;
@@ -961,70 +1072,6 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
                                      tile_valid<G::TILE>(n, tile), orderMask, shift, myBase, status,
                                      statusNext, errFlag, tile, 0, grp, smem, stamps, k, v, NoMid{});
 }
-
-// Persistent form (THRS_PIPE): a fixed grid of workgroups loops over tiles.
-// Between a tile's walk and its write-out the workgroup takes the next tile id
-// and issues that tile's loads, so they are in flight while the stage drains
-// (the tile's own prefix is published as early as in thrs_pass).  Needs a
-// single LDS round (the tile sits in the stage, not in registers, during the
-// walk).  Every tile id handed out belongs to a running workgroup, so every
-// walk terminates.
-template <int KT, int VB, typename ST, bool ATOMIC_RANK>
-__global__ __launch_bounds__((PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::THREADS))
-__attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::WPE))) void thrs_pass_pipe(
-    const typename KeyTraits<KT>::U* __restrict__ keysIn, typename KeyTraits<KT>::U* __restrict__ keysOut,
-    const typename ValueWord<VB>::T* __restrict__ valsIn, typename ValueWord<VB>::T* __restrict__ valsOut,
-    uint32_t n, typename KeyTraits<KT>::U orderMask, int shift, const uint32_t* __restrict__ digitBase,
-    ST* __restrict__ status, ST* __restrict__ statusNext, uint32_t* __restrict__ tileCounter,
-    uint32_t* __restrict__ errFlag, GroupTables<ST> grp, uint64_t* __restrict__ stamps,
-    const uint32_t* __restrict__ gate, uint32_t gateWant) {
-  if (gate && *gate != gateWant) return;  // pass not needed on this launch path (thrs_plan decides)
-  using U = typename KeyTraits<KT>::U;
-  using VW = typename ValueWord<VB>::T;
-  using G = PassGeom<sizeof(U), VB>;
-  static_assert(G::ROUNDS == 1, "the persistent pass keeps a whole tile in the LDS stage");
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  uint32_t* s_cnt = reinterpret_cast<uint32_t*>(smem + G::STAGE * (sizeof(U) + VB));
-  uint32_t* s_misc = s_cnt + (G::WAVES + 1) * kBins;
-  const uint32_t tid = threadIdx.x;
-  const uint32_t nTiles = (uint32_t)(((uint64_t)n + G::TILE - 1) / G::TILE);
-  if (tid == 0) s_misc[0] = atomicAdd(tileCounter, 1u);
-  for (uint32_t i = tid; i < (uint32_t)(G::WAVES * kBins); i += G::THREADS) s_cnt[i] = 0;
-  const uint32_t myBase = digitBase[tid & 255u];
-  lds_barrier();
-  uint32_t tile = s_misc[0];
-  if (tile >= nTiles) return;
-  U k[G::KPT];
-  VW v[VB ? G::KPT : 1];
-  load_tile<KT, VB>(keysIn, valsIn, (uint64_t)tile * G::TILE, tile_valid<G::TILE>(n, tile), k, v);
-  for (;;) {
-#ifdef THRS_STAMPS
-    if (stamps && tid == 0) {
-      uint64_t* s_stamp = reinterpret_cast<uint64_t*>(s_misc + 16);
-      for (int i = 0; i < kStampSlots; ++i) s_stamp[i] = 0;
-      s_stamp[0] = __builtin_amdgcn_s_memrealtime();
-      s_stamp[7] = xcc_id();
-      s_misc[1] = s_misc[2] = s_misc[3] = 0;
-    }
-#endif
-    uint32_t next = 0xFFFFFFFFu;
-    auto mid = [&]() __attribute__((always_inline)) {
-      if (tid == 0) s_misc[8] = atomicAdd(tileCounter, 1u);
-      lds_barrier();
-      next = s_misc[8];
-      if (next < nTiles) load_tile<KT, VB>(keysIn, valsIn, (uint64_t)next * G::TILE, tile_valid<G::TILE>(n, next), k, v);
-    };
-    pass_tile<KT, VB, ST, ATOMIC_RANK>(keysIn, keysOut, valsIn, valsOut, (uint64_t)tile * G::TILE,
-                                       tile_valid<G::TILE>(n, tile), orderMask, shift, myBase, status,
-                                       statusNext, errFlag, tile, 0, grp, smem, stamps, k, v, mid);
-    // every wave is past its write-out: the stage, s_gofs and s_cnt are free
-    for (uint32_t i = tid; i < (uint32_t)(G::WAVES * kBins); i += G::THREADS) s_cnt[i] = 0;
-    lds_barrier();
-    tile = next;
-    if (tile >= nTiles) break;
-  }
-}
-
 
 // ============================================================ XCD-block claims
 // Tiles are claimed in BLOCKS of kXcdBlock consecutive tiles, one open block
@@ -1079,7 +1126,7 @@ __device__ __forceinline__ uint32_t xb_claim(uint32_t* claimState, uint32_t stri
   if (o == kXbOpenAt) xb_open(gblock, &tab[j + 1], nBlocks);
   uint32_t e = load_agent(&tab[j]);
   for (uint32_t spin = 0; e == 0; ++spin) {
-    if (spin > (1u << 22)) {  // bounded: never hang the GPU
+    if (spin >= kSpinMax) {  // bounded: never hang the GPU
       atomicOr(errFlag, 2u);
       return kXbDone;
     }
@@ -1101,8 +1148,8 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
     uint32_t n, typename KeyTraits<KT>::U orderMask, int shift, const uint32_t* __restrict__ digitBase,
     ST* __restrict__ status, ST* __restrict__ statusNext, uint32_t* __restrict__ claimState,
     uint32_t* __restrict__ errFlag, GroupTables<ST> grp, uint64_t* __restrict__ stamps,
-    const uint32_t* __restrict__ gate, uint32_t gateWant) {
-  if (gate && *gate != gateWant) return;  // pass not needed on this launch path (thrs_plan decides)
+    const uint32_t* __restrict__ gate, uint32_t gateMask) {
+  if (gate && !((gateMask >> *gate) & 1u)) return;  // not needed on this launch path (thrs_plan decides)
   using U = typename KeyTraits<KT>::U;
   using VW = typename ValueWord<VB>::T;
   using G = PassGeom<sizeof(U), VB>;
@@ -1163,12 +1210,12 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
     const typename ValueWord<VB>::T* __restrict__ valsIn, typename ValueWord<VB>::T* __restrict__ valsOut,
     typename KeyTraits<KT>::U orderMask, int shift, uint32_t* __restrict__ segInfo,
     const uint32_t* __restrict__ segBase, ST* __restrict__ status, uint32_t* __restrict__ errFlag,
-    GroupTables<ST> grp, const uint32_t* __restrict__ gate, uint32_t gateWant) {
+    GroupTables<ST> grp, const uint32_t* __restrict__ gate, uint32_t gateMask) {
   using U = typename KeyTraits<KT>::U;
   using VW = typename ValueWord<VB>::T;
   using G = PassGeom<sizeof(U), VB>;
   constexpr uint32_t T = G::TILE;
-  if (gate && *gate != gateWant) return;
+  if (gate && !((gateMask >> *gate) & 1u)) return;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint32_t* s_cnt = reinterpret_cast<uint32_t*>(smem + G::STAGE * (sizeof(U) + VB));
   uint32_t* s_misc = s_cnt + (G::WAVES + 1) * kBins;
@@ -1177,11 +1224,7 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
   const uint32_t tid = threadIdx.x;
   if (tid < 2 * (kSegs + 1)) (tid <= (uint32_t)kSegs ? segPos[tid] : segTiles[tid - kSegs - 1]) = segInfo[tid];
   __syncthreads();
-#ifdef THRS_SEG_HOME0
-  const uint32_t home = 0;  // EXPERIMENT: every workgroup takes the segments in order (no XCD affinity)
-#else
   const uint32_t home = xcc_id() & (kSegs - 1);
-#endif
   uint32_t done = 0;  // thread 0: segments found exhausted
   U k[G::KPT];
   VW v[VB ? G::KPT : 1];

@@ -38,6 +38,53 @@ __global__ void k_fill(int keyType, void* out, uint64_t n, uint64_t start, uint6
   }
 }
 
+// raw key whose getKeyBits image is y (inverse of KeyTraits::bits)
+__device__ __forceinline__ uint64_t unbits(int keyType, uint64_t y) {
+  switch (keyType) {
+    case THRS_KEY_F32: return (y & 0x80000000ull) ? (y ^ 0x80000000ull) : (~y & 0xFFFFFFFFull);
+    case THRS_KEY_F64: return (y >> 63) ? (y ^ 0x8000000000000000ull) : ~y;
+    default: return y;
+  }
+}
+
+// Non-uniform key distributions (bench.py workloads c2_*, low-entropy tests):
+//   1 sorted   image of key i in [floor(i*2^W/n), floor((i+1)*2^W/n)): a
+//              stratified sorted uniform sample (the digit runs of sorting
+//              uniform keys, which is what a sort of already-sorted data sees)
+//   2 reverse  the same, descending
+//   3 extreme  all zero except key n/3 = 1 and key 2n/3 = 42
+//              (SortKeys.extremeCase, unittest.cpp:191-225)
+//   4 fewuniq  16 distinct uniform keys, chosen per key by the stream
+__global__ void k_fill_dist(int keyType, void* out, uint64_t n, uint64_t start, uint64_t state, int dist) {
+  const bool k32 = keyType == THRS_KEY_U32 || keyType == THRS_KEY_F32;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t r = draw(state, start + i + 1);
+    uint64_t raw = 0;
+    if (dist == 1 || dist == 2) {
+      const uint64_t j = dist == 1 ? i : n - 1 - i;
+      uint64_t y;
+      if (k32) {
+        const uint64_t lo = (j << 32) / n, hi = ((j + 1) << 32) / n;
+        y = lo + (hi > lo ? r % (hi - lo) : 0);
+      } else {
+        const uint64_t step = ~0ull / n;
+        y = j * step + (step ? r % step : 0);
+      }
+      raw = unbits(keyType, y);
+    } else if (dist == 3) {
+      raw = i == n / 3 ? 1 : (i == 2 * n / 3 ? 42 : 0);
+    } else if (dist == 4) {
+      raw = draw(state, 1000003ull + (r & 15));
+      if (keyType == THRS_KEY_F32) raw &= 0xFF7FFFFFull;
+      if (keyType == THRS_KEY_F64) raw &= 0xFFEFFFFFFFFFFFFFull;
+    } else {
+      raw = keyType == THRS_KEY_F32 ? (r & 0xFF7FFFFFull) : keyType == THRS_KEY_F64 ? (r & 0xFFEFFFFFFFFFFFFFull) : r;
+    }
+    if (k32) ((uint32_t*)out)[i] = (uint32_t)raw;
+    else ((uint64_t*)out)[i] = raw;
+  }
+}
+
 // values = input index (sequentialValues / ValueType(i), unittest.cpp:118-125, 394-397);
 // u128 = {i, i} as in K64V128 (unittest.cpp:471-481).
 __global__ void k_iota(int valueBytes, void* out, uint64_t n, uint64_t start) {
@@ -151,6 +198,14 @@ extern "C" {
 THRS_API int thrsu_fill_keys(int keyType, void* out, uint64_t n, uint64_t start, uint64_t state, hipStream_t stream) {
   if (!n) return THRS_SUCCESS;
   hipLaunchKernelGGL(k_fill, dim3(grid_for(n)), dim3(256), 0, stream, keyType, out, n, start, state);
+  return ok(hipGetLastError());
+}
+
+THRS_API int thrsu_fill_dist(int keyType, void* out, uint64_t n, uint64_t start, uint64_t state, int dist,
+                             hipStream_t stream) {
+  if (!n) return THRS_SUCCESS;
+  if (dist < 0 || dist > 4) return THRS_ERROR_INVALID_VALUE;
+  hipLaunchKernelGGL(k_fill_dist, dim3(grid_for(n)), dim3(256), 0, stream, keyType, out, n, start, state, dist);
   return ok(hipGetLastError());
 }
 

@@ -36,13 +36,12 @@ over libthrs.so, which raises if the library is missing.
 """
 from __future__ import annotations
 
-import os
 import time
 from dataclasses import dataclass, field
 
 import numpy as np
 
-from . import KeyType, RadixSort, SortOrder, ValueType, bytesOf
+from . import KeyType, Options, RadixSort, SortOrder, ValueType, bytesOf
 
 BINS = 256
 
@@ -102,6 +101,7 @@ class HipLocalOps:
 
     def __init__(self, config: RadixSort.Config):
         self.rs = RadixSort([], config)
+        self.rs_lsd = RadixSort([], config, Options(path="lsd"))
         self._tmp = None
         self.lsd_finish = False  # set by DistributedRadixSort for world > 1 (see sort)
 
@@ -129,20 +129,13 @@ class HipLocalOps:
         # A rank's keys share 256/world top digits, so the 3-HBM-pass path's
         # 16-bit buckets would hold ~world * 2^14 keys each: always over the
         # local sort's capacity, i.e. its fallback plus a wasted bucket
-        # histogram.  The finish runs the plain LSD path unless THRS_HYBRID is
-        # set by the caller.
-        forced = os.environ.get("THRS_HYBRID")
-        off = self.lsd_finish and forced is None
-        if off:
-            os.environ["THRS_HYBRID"] = "0"
-        try:
-            if vals is None:
-                self.rs.sortKeys(keys, n, tmp, start_bits, end_bits)
-            else:
-                self.rs.sortPairs(keys, vals, n, tmp, start_bits, end_bits)
-        finally:
-            if off:
-                os.environ.pop("THRS_HYBRID", None)
+        # histogram.  For world > 1 the finish asks for the plain LSD path
+        # (an explicit per-call option: DESIGN.md s4).
+        rs = self.rs_lsd if self.lsd_finish else self.rs
+        if vals is None:
+            rs.sortKeys(keys, n, tmp, start_bits, end_bits)
+        else:
+            rs.sortPairs(keys, vals, n, tmp, start_bits, end_bits)
 
 
 # ----------------------------------------------------------------- the sorter

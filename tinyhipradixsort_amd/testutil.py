@@ -19,12 +19,13 @@ def tlib() -> ctypes.CDLL:
         vp, u64, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int
         ull_p = ctypes.POINTER(ctypes.c_ulonglong)
         L.thrsu_fill_keys.argtypes = [i32, vp, u64, u64, u64, vp]
+        L.thrsu_fill_dist.argtypes = [i32, vp, u64, u64, u64, i32, vp]
         L.thrsu_iota.argtypes = [i32, vp, u64, u64, vp]
         L.thrsu_check_sorted.argtypes = [i32, i32, vp, u64, i32, i32, ull_p, vp]
         L.thrsu_fingerprint.argtypes = [i32, vp, u64, ull_p, vp]
         L.thrsu_check_pairs.argtypes = [i32, i32, i32, vp, vp, vp, u64, i32, i32, ull_p, vp]
         L.thrsu_copy.argtypes = [vp, vp, u64, i32, vp]
-        for f in ("thrsu_copy", "thrsu_fill_keys", "thrsu_iota", "thrsu_check_sorted", "thrsu_fingerprint", "thrsu_check_pairs"):
+        for f in ("thrsu_copy", "thrsu_fill_keys", "thrsu_fill_dist", "thrsu_iota", "thrsu_check_sorted", "thrsu_fingerprint", "thrsu_check_pairs"):
             getattr(L, f).restype = i32
         _tl = L
     return _tl
@@ -33,6 +34,17 @@ def tlib() -> ctypes.CDLL:
 def fill_keys(key_type: int, out, n: int, start: int = 0, state: int = 0, stream=None):
     """Keys = randomizeValues over splitmix64 draws start+1..start+n (unittest.cpp:96-116)."""
     _check(tlib().thrsu_fill_keys(int(key_type), _ptr(out), n, start, state, _stream(stream)))
+
+
+DISTS = {"uniform": 0, "sorted": 1, "reverse": 2, "extreme": 3, "fewuniq": 4}
+
+
+def fill_dist(key_type: int, out, n: int, dist: str, start: int = 0, state: int = 0, stream=None):
+    """Keys of a named distribution (thrs_testutil.hip k_fill_dist): uniform
+    (= fill_keys), sorted / reverse (stratified sorted uniform sample),
+    extreme (unittest.cpp:191-225's all-zero array with two set keys),
+    fewuniq (16 distinct uniform keys)."""
+    _check(tlib().thrsu_fill_dist(int(key_type), _ptr(out), n, start, state, DISTS[dist], _stream(stream)))
 
 
 def iota(value_bytes: int, out, n: int, start: int = 0, stream=None):
