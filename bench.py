@@ -64,6 +64,8 @@ def parse():
     p.add_argument("--vendor", default="auto", choices=["auto", "off"],
                    help="time hipcub::DeviceRadixSort on the same inputs (N=1 only)")
     p.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
+    p.add_argument("--ref-gpu", default="auto", choices=["auto", "off"],
+                   help="time the reference's own kernels (oracle/_ref) on the same inputs (N=1 only)")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--quiet", action="store_true")
     p.add_argument("--force-dist", action="store_true",
@@ -138,6 +140,39 @@ def cpu_baseline(kt: int, vb: int, n_target_s: float) -> dict:
             "sample": f"{best['name']} of {best['n']} splitmix64 {DTYPE[kt]} keys, median of {best['runs']} runs, "
                       f"{threads} threads ({cpu_model()}); 1-thread leg in `legs`",
             "legs": legs}
+
+
+def reference_gpu_bench(TU, kt, kb, vb, n, keys, vals, gen, stream, runs: int = 2):
+    """The REFERENCE's own kernels on this MI355X (oracle/_ref: kernel.cu via
+    hipRTC, launched with its pass loop, tinyhipradixsort.hpp:854-944) on the
+    same inputs, event-timed per run on fresh input.  A baseline, never `value`."""
+    import torch
+    try:
+        from oracle import ref as R
+    except ImportError:
+        return None
+    if not R.kernels_available():
+        return None
+    vt = {0: 0, 4: 0, 8: 1, 16: 2}[vb]
+    tmp = torch.empty(sum(R.temp_bytes(kt, vt, n)), dtype=torch.uint8, device="cuda")
+    times = []
+    for r in range(runs):
+        j = r % len(keys)
+        gen(keys[j], j)
+        if vb:
+            TU.iota(vb, vals[j], n)
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        R.sort(kt, vt, False, keys[j], vals[j] if vb else None, n, tmp, 0, kb * 8, stream)
+        b.record(stream)
+        torch.cuda.synchronize()
+        times.append(a.elapsed_time(b))
+        if TU.count_unsorted(kt, keys[j], n, 0, kb * 8):
+            return None
+    ms = statistics.median(times)
+    return {"name": "reference kernels (kernel.cu via hipRTC, gfx950) + its pass loop", "value": round(n / ms / 1e6, 3),
+            "unit": "Gkeys/s", "ms_per_sort": round(ms, 3), "runs": runs, "inputs": "same generator, fresh per run"}
 
 
 def vendor_bench(T, TU, kt, kb, vb, n, keys, vals, gen, stream, runs: int = 3):
@@ -324,10 +359,12 @@ def main():
             chk = TU.check_pairs(kt, vb, keys_in0, keys[last], vals[last], n, 0, kb * 8)
             if chk["gather_mismatch"] or chk["unstable"]:
                 raise SystemExit(f"bench: pairs output of the last step is wrong: {chk}")
-        vendor = None
+        vendor = ref_gpu = None
         if args.vendor == "auto" and world == 1:
             del keys_in0
             vendor = vendor_bench(T, TU, kt, kb, vb, n, keys, vals, gen, stream)
+        if args.ref_gpu == "auto" and world == 1 and dist_kind == "uniform":
+            ref_gpu = reference_gpu_bench(TU, kt, kb, vb, n, keys, vals, gen, stream)
         recycled = False
         elapsed = t1 - t0
         scaling = "weak"
@@ -380,7 +417,7 @@ def main():
         if bad:
             raise SystemExit(f"bench: rank {rank} output is not sorted ({bad} inversions)")
         recycled = False
-        vendor = None
+        vendor = ref_gpu = None
         elapsed = t1 - t0
         scaling = "weak"
         global_keys = n * world
@@ -444,7 +481,7 @@ def main():
                           "parallelism": parallelism,
                           "distribution": dist_name,
                           "inputs": "fresh per step" if not recycled else "pool recycled (some steps re-sort)"},
-               "roofline": roof, "cpu_baseline": cpu, "vendor": vendor}
+               "roofline": roof, "cpu_baseline": cpu, "vendor": vendor, "reference_gpu": ref_gpu}
         if phase:
             out["phases_ms"] = phase
         print(json.dumps(out), flush=True)

@@ -110,3 +110,11 @@ def test_lsd_empty_and_noop():
     x = np.array([5, 3, 9], np.uint32)
     k, _ = O.lsd_sort(O.U32, x, None, 16, 16)
     assert k.tolist() == [5, 3, 9]
+
+
+def test_golden_is_pinned_by_the_reference():
+    """tests/golden/pin_golden.py recorded that the reference's own kernels
+    (make_golden_ref.py on MI355X) produce every committed digest."""
+    p = GOLDEN.get("pinned_by")
+    assert p and p["rows"] == sum(len(r) for r in GOLDEN["cases"].values()) == 17 * 128
+    assert "reference kernels" in p["source"]
