@@ -14,8 +14,10 @@ metric: "Gkeys/s and achieved HBM GB/s (% of peak), u32 keys N=2^30, 1/2/4/8 GPU
   histogram + one pass per digit.
 * N>1: launched by torch.distributed.run, one rank per GPU; each rank holds
   2^30 u32 keys (weak scaling) and one step is the bucket-exchange sort of all
-  N*2^30 keys (local digit histogram -> RCCL all-gather of counts -> local
-  partition -> RCCL all-to-all -> local LSD finish).
+  N*2^30 keys (stable top-digit partition -> RCCL all-gather of counts ->
+  exact global-rank split (digit refinement over small all-gathers, split
+  buckets sorted locally) -> RCCL all-to-all -> local LSD finish): every rank
+  ends with exactly N*2^30/N keys, whatever the distribution.
 
 Timing: W warm-up steps, then barrier + synchronize, K steps, synchronize +
 barrier; the max over ranks.  rank 0 prints ONE JSON line.  `roofline` uses the
@@ -382,7 +384,10 @@ def main():
         keys, vals = [], []
         for i in range(pool):
             kbuf = torch.empty(n * kb, dtype=torch.uint8, device="cuda")
-            TU.fill_keys(kt, kbuf, n, start=(i * world + rank) * n)
+            if dist_kind == "uniform":
+                TU.fill_keys(kt, kbuf, n, start=(i * world + rank) * n)
+            else:
+                TU.fill_dist(kt, kbuf, n, dist_kind, start=(i * world + rank) * n)
             keys.append(kbuf)
             if vb:
                 vbuf = torch.empty(n * vb, dtype=torch.uint8, device="cuda")

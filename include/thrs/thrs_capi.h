@@ -135,6 +135,16 @@ int thrs_partition_pass(const thrs_config* config, const void* keysIn, const voi
                         void* temporaryBuffer, void* keysOut, void* valuesOut, int bitLocation, uint32_t* counts,
                         hipStream_t stream);
 
+/* Multi-GPU building block (no reference counterpart): the exact-split
+ * refinement of the bucket exchange.  counts[256] (device u32, zeroed first)
+ * receives, by d, the number of keys in keys[0, n) whose transformed key t =
+ * getKeyBits(key) ^ ORDER_MASK (kernel.cu:18-24, 46-69) satisfies
+ * (t & prefixMask) == prefixValue and ((t >> bitLocation) & 0xFF) == d.
+ * Masks are 64-bit; for 4-byte keys only their low 32 bits are used.  keys
+ * needs no particular alignment (any sub-range of a key buffer). */
+int thrs_digit_histogram(const thrs_config* config, const void* keys, uint32_t numberOfInputs, uint64_t prefixMask,
+                         uint64_t prefixValue, int bitLocation, uint32_t* counts, hipStream_t stream);
+
 /* Device-side failures (no reference counterpart; the reference would hang
  * where these give up).  A look-back or tile-claim wait is bounded; when the
  * bound is hit the sort's output is wrong and the failure is recorded twice:

@@ -41,7 +41,14 @@ class OracleOps:
             pv = torch.from_numpy(np.ascontiguousarray(vals.numpy().reshape(n, self.vb)[order]).reshape(-1).copy())
         return pk, pv, torch.from_numpy(np.bincount(d, minlength=256).astype(np.int32))
 
-    def sort(self, keys, vals, n, s, e):
+    def histogram(self, keys, n, mask, value, bit):
+        k = keys.numpy().view(self.dt)[:n]
+        t = O.key_bits_np(self.kt, k, self.desc)
+        sel = (t & np.uint64(mask)) == np.uint64(value)
+        d = ((t[sel] >> np.uint64(bit)) & np.uint64(0xFF)).astype(np.int64)
+        return torch.from_numpy(np.bincount(d, minlength=256).astype(np.int32))
+
+    def sort(self, keys, vals, n, s, e, finish=True):
         if n == 0:
             return
         k = keys.numpy().view(self.dt)[:n]
@@ -63,6 +70,9 @@ CASES = [
     (O.U32, 4, [3000, 3000], 8, 24, False, "fewbits"),        # many ties -> stability across ranks
     (O.F64, 16, [1500, 1700], 0, 64, True, "random"),
     (O.U32, 4, [2000, 2000], 32, 40, False, "random"),        # all passes are identities
+    (O.U64, 8, [3000, 2500], 0, 64, False, "extreme"),        # one key value: split by (rank, position)
+    (O.U32, 4, [4000, 100], 0, 32, False, "fewbits"),         # skewed sizes and few distinct keys
+    (O.U32, 4, [3000, 3000], 16, 24, False, "extreme"),       # one digit: no refinement level
 ]
 
 
@@ -112,9 +122,9 @@ def _worker(rank, world, port, cases):
             assert np.array_equal(got_k, ek[off:off + n_out]), (ci, rank, "keys")
             if vb:
                 assert np.array_equal(vo.numpy().reshape(n_out, vb), ev[off:off + n_out]), (ci, rank, "values")
-            if kind == "random" and s < e and pass_reads_bits(kt, s, e):
+            if pass_reads_bits(kt, s, e):   # exact balance: global positions [rN/G, (r+1)N/G)
                 total = glob.shape[0]
-                assert abs(n_out - total / world) <= total / world * 0.25 + 64, (ci, rank, n_out)
+                assert n_out == (rank + 1) * total // world - rank * total // world, (ci, rank, n_out)
     finally:
         dist.destroy_process_group()
 
@@ -129,36 +139,92 @@ def free_port():
         return so.getsockname()[1]
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_bucket_exchange_gloo(world):
-    mp.spawn(_worker, args=(world, free_port(), CASES), nprocs=world, join=True)
+    cases = CASES if world < 8 else [c for c in CASES if c[6] != "random"] + CASES[:2]
+    mp.spawn(_worker, args=(world, free_port(), cases), nprocs=world, join=True)
 
 
-def test_assign_ranges_balanced_uniform():
-    c = np.full(256, 1000)
-    for g in (1, 2, 4, 8):
-        b = D.assign_ranges(c, g)
-        assert b[0] == 0 and b[-1] == 256 and len(b) == g + 1
-        assert all(b[i + 1] - b[i] == 256 // g for i in range(g))
+def _simulate(ranks, kt, s, e, desc=False):
+    """The host split logic on in-memory ranks (numpy histograms): returns
+    each rank's received keys after the finish, to compare with one stable sort."""
+    world = len(ranks)
+    locs = D.pass_locations(O.KEY_BYTES[kt], s, e)
+    parts, counts = [], []
+    for k in ranks:
+        t = O.key_bits_np(kt, k, desc)
+        d = ((t >> np.uint64(locs[-1])) & np.uint64(0xFF)).astype(np.int64)
+        o = np.argsort(d, kind="stable")
+        parts.append(k[o])
+        counts.append(np.bincount(d, minlength=256))
+    counts = np.array(counts)
+    targets = D.make_targets(counts, world, locs[-1])
+    for loc in reversed(locs[:-1]):
+        act = [tg for tg in targets if tg.refining]
+        if not act:
+            break
+        hist = np.zeros((world, len(act), 256), np.int64)
+        for r in range(world):
+            off = np.concatenate([[0], np.cumsum(counts[r])])
+            for i, tg in enumerate(act):
+                kk = parts[r][off[tg.bucket]:off[tg.bucket + 1]]
+                t = O.key_bits_np(kt, kk, desc)
+                sel = (t & np.uint64(tg.mask)) == np.uint64(tg.value)
+                hist[r, i] = np.bincount(((t[sel] >> np.uint64(loc)) & np.uint64(0xFF)).astype(np.int64),
+                                         minlength=256)
+        D.refine(targets, hist, loc)
+    for r in range(world):          # sort split buckets locally
+        off = np.concatenate([[0], np.cumsum(counts[r])])
+        for b in {tg.bucket for tg in targets if tg.inside}:
+            seg = parts[r][off[b]:off[b + 1]]
+            parts[r][off[b]:off[b + 1]] = O.lsd_sort(kt, seg, None, s, e, desc)[0]
+    cuts = D.cut_points(counts, targets)
+    out = []
+    for g in range(world):
+        recv = np.concatenate([parts[r][cuts[r, g]:cuts[r, g + 1]] for r in range(world)])
+        out.append(O.lsd_sort(kt, recv, None, s, e, desc)[0])
+    return out
 
 
-def test_assign_ranges_skew_and_empty():
-    c = np.zeros(256, np.int64)
-    c[0] = 10
-    c[42] = 1_000_000
-    b = D.assign_ranges(c, 4)
-    assert b == sorted(b) and b[0] == 0 and b[-1] == 256
-    assert D.assign_ranges(np.zeros(256), 3) == [0, 0, 0, 256]
+@pytest.mark.parametrize("world", [2, 5, 8])
+@pytest.mark.parametrize("kind", ["random", "extreme", "fewbits", "onebucket"])
+def test_exact_split_host_logic(world, kind):
+    rng = np.random.default_rng(world * 10 + len(kind))
+    sizes = [int(x) for x in rng.integers(0, 3000, world)]
+    ranks = []
+    for r, n in enumerate(sizes):
+        k = O.randomize_np(O.U32, O.splitmix64_stream(777 * r, n))
+        if kind == "extreme":
+            k = np.zeros(n, np.uint32)
+        elif kind == "fewbits":
+            k = (k & np.uint32(0x01000103)).astype(np.uint32)
+        elif kind == "onebucket":
+            k = (k & np.uint32(0x00FFFFFF)).astype(np.uint32)   # one top digit, many keys
+        ranks.append(k)
+    out = _simulate(ranks, O.U32, 0, 32)
+    glob = np.concatenate(ranks)
+    exp = O.lsd_sort(O.U32, glob, None, 0, 32)[0]
+    total = glob.shape[0]
+    got = np.concatenate(out)
+    assert np.array_equal(got, exp)
+    for g in range(world):
+        assert out[g].shape[0] == (g + 1) * total // world - g * total // world
 
 
-def test_exchange_plan_conserves():
-    rng = np.random.default_rng(1)
-    a = rng.integers(0, 500, size=(4, 256))
-    plans = [D.exchange_plan(a, r) for r in range(4)]
-    send = np.array([p.send for p in plans])
-    recv = np.array([p.recv for p in plans])
-    assert (send == recv.T).all()
-    assert send.sum() == a.sum() and all(p.bounds == plans[0].bounds for p in plans)
+def test_exact_split_stability_of_equal_keys():
+    """All keys equal: the split follows (rank, position) -- checked through
+    the cut points directly."""
+    counts = np.zeros((3, 256), np.int64)
+    counts[:, 7] = [5, 0, 7]
+    targets = D.make_targets(counts, 3, 24)
+    for loc in (16, 8, 0):
+        act = [t for t in targets if t.refining]
+        hist = np.zeros((3, len(act), 256), np.int64)
+        hist[:, :, 0] = counts[:, 7][:, None]
+        D.refine(targets, hist, loc)
+    cuts = D.cut_points(counts, targets)
+    # 12 keys, 4 per rank: rank0 takes r0[0:4]; rank1 takes r0[4], r2[0:3]; rank2 takes r2[3:7]
+    assert cuts.tolist() == [[0, 4, 5, 5], [0, 0, 0, 0], [0, 0, 3, 7]]
 
 
 def test_pass_locations():

@@ -76,10 +76,8 @@ def _worker(rank, world, port, out_dir):
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
-        cases = [(O.U32, 4, [300001, 250007], 0, 32, False), (O.F32, 0, [65536 * 3, 1000], 0, 32, True),
-                 (O.U64, 8, [120000, 90001], 16, 48, False)]
-        for ci, (kt, vb, sizes, s, e, desc) in enumerate(cases):
-            glob = O.randomize_np(kt, O.splitmix64_stream(ci * 10 ** 6, sum(sizes)))
+        for ci, (kt, vb, sizes, s, e, desc) in enumerate(CASES):
+            glob = _keys(ci, kt, sum(sizes))
             lo = sum(sizes[:rank])
             kd = torch.from_numpy(glob[lo:lo + sizes[rank]].view(np.uint8).copy()).cuda()
             vd = None
@@ -96,16 +94,30 @@ def _worker(rank, world, port, out_dir):
         dist.destroy_process_group()
 
 
+CASES = [(O.U32, 4, [300001, 250007], 0, 32, False), (O.F32, 0, [65536 * 3, 1000], 0, 32, True),
+         (O.U64, 8, [120000, 90001], 16, 48, False),
+         (O.U32, 4, [200000, 150001], 0, 32, False),      # extremeCase-shaped: all zero but two keys
+         (O.U64, 8, [100000, 100000], 0, 64, False)]      # one top-digit bucket, many keys
+
+
+def _keys(ci, kt, n):
+    k = O.randomize_np(kt, O.splitmix64_stream(ci * 10 ** 6, n))
+    if ci == 3:
+        k = np.zeros(n, np.uint32)
+        k[n // 3], k[2 * n // 3] = 1, 42
+    if ci == 4:
+        k = k & np.uint64(0x00FFFFFFFFFFFFFF)
+    return k
+
+
 def test_two_ranks_one_gpu(gpu, tmp_path):
     import torch.multiprocessing as mp
     with socket.socket() as so:
         so.bind(("127.0.0.1", 0))
         port = so.getsockname()[1]
     mp.spawn(_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
-    cases = [(O.U32, 4, [300001, 250007], 0, 32, False), (O.F32, 0, [65536 * 3, 1000], 0, 32, True),
-             (O.U64, 8, [120000, 90001], 16, 48, False)]
-    for ci, (kt, vb, sizes, s, e, desc) in enumerate(cases):
-        glob = O.randomize_np(kt, O.splitmix64_stream(ci * 10 ** 6, sum(sizes)))
+    for ci, (kt, vb, sizes, s, e, desc) in enumerate(CASES):
+        glob = _keys(ci, kt, sum(sizes))
         idx = np.arange(sum(sizes), dtype=np.uint32 if vb == 4 else np.uint64) if vb else None
         ek, ev = O.lsd_sort(kt, glob, idx, s, e, desc)
         gk = np.concatenate([np.load(tmp_path / f"c{ci}_r{r}_k.npy") for r in range(2)]).view(NP_KEY[kt])
@@ -113,6 +125,47 @@ def test_two_ranks_one_gpu(gpu, tmp_path):
         if vb:
             gv = np.concatenate([np.load(tmp_path / f"c{ci}_r{r}_v.npy") for r in range(2)]).view(idx.dtype)
             assert np.array_equal(gv, ev), ci
-        # balanced to a bucket's granularity on uniform input
+        # exact balance: rank 0 holds global positions [0, N/2)
         n0 = np.load(tmp_path / f"c{ci}_r0_k.npy").size // O.KEY_BYTES[kt]
-        assert abs(n0 - sum(sizes) / 2) < sum(sizes) * 0.02
+        assert n0 == sum(sizes) // 2, (ci, n0)
+
+
+@pytest.mark.parametrize("kt,desc", [(O.U32, False), (O.F32, True), (O.U64, False), (O.F64, True)])
+def test_digit_histogram_vs_numpy(gpu, kt, desc):
+    """thrs_digit_histogram (the exact split's refinement) on an unaligned
+    sub-range, with a prefix mask."""
+    import tinyhipradixsort_amd as T
+    torch = gpu
+    n = 200003
+    k = O.randomize_np(kt, O.splitmix64_stream(42, n))
+    k[: n // 2] &= np.array(0xFF0000FF if O.KEY_BYTES[kt] == 4 else 0xFF000000000000FF, k.dtype)
+    cfg = T.RadixSort.Config(keyType=T.KeyType(kt), sortOrder=T.SortOrder.Descending if desc else T.SortOrder.Ascending)
+    rs = T.RadixSort([], cfg)
+    kd = torch.from_numpy(k.view(np.uint8).copy()).cuda()
+    kb = O.KEY_BYTES[kt]
+    t = O.key_bits_np(kt, k, desc)
+    h = torch.empty(256, dtype=torch.int32, device="cuda")
+    for (mask, value, bit) in [(0, 0, 0), (0xFF << (kb * 8 - 8), int(t[7]) & (0xFF << (kb * 8 - 8)), 8),
+                               ((0xFF << (kb * 8 - 8)) | 0xFF, int(t[3]) & ((0xFF << (kb * 8 - 8)) | 0xFF), 16)]:
+        lo, hi = 3, n - 5                                # a sub-range at an unaligned offset
+        rs.digitHistogram(kd[lo * kb:hi * kb], hi - lo, mask, value, bit, h)
+        torch.cuda.synchronize()
+        tt = t[lo:hi]
+        sel = (tt & np.uint64(mask)) == np.uint64(value)
+        exp = np.bincount(((tt[sel] >> np.uint64(bit)) & np.uint64(0xFF)).astype(np.int64), minlength=256)
+        assert np.array_equal(h.cpu().numpy().astype(np.int64), exp), (mask, value, bit)
+
+
+def test_bench_force_dist_runs_rccl_at_world_1(gpu):
+    """bench.py --force-dist: the bucket exchange through the nccl (= RCCL)
+    backend at world size 1 -- the code path of the N-GPU bench lines."""
+    import json
+    import subprocess
+    import sys
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29611", RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--force-dist", "--n", str(1 << 22),
+                        "--steps", "2", "--warmup", "1", "--cpu-baseline", "off"],
+                       capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 1 and line["value"] > 0 and "bucket-exchange" in line["config"]["parallelism"]

@@ -69,6 +69,8 @@ def lib() -> ctypes.CDLL:
         L.thrs_sort_pairs_ex.argtypes = [ctypes.POINTER(_CConfig), ctypes.POINTER(_COptions), vp, vp, u32, vp, i32,
                                          i32, vp]
         L.thrs_take_device_error.restype = i32
+        L.thrs_digit_histogram.argtypes = [ctypes.POINTER(_CConfig), vp, u32, u64, u64, i32, vp, vp]
+        L.thrs_digit_histogram.restype = i32
         L.thrs_check_device_error.argtypes = [vp, vp]
         L.thrs_partition_pass.argtypes = [ctypes.POINTER(_CConfig), vp, vp, u32, vp, vp, vp, i32, vp, vp]
         L.thrs_malloc.argtypes = [ctypes.POINTER(vp), i64]
@@ -344,6 +346,15 @@ class RadixSort:
         _check(lib().thrs_partition_pass(ctypes.byref(self._c()), _ptr(inputKeyBuffer), _ptr(inputValueBuffer),
                                          _n(numberOfInputs), _ptr(temporaryBuffer), _ptr(outputKeyBuffer),
                                          _ptr(outputValueBuffer), int(bitLocation), _ptr(counts), _stream(stream)))
+
+    def digitHistogram(self, inputKeyBuffer, numberOfInputs: int, prefixMask: int, prefixValue: int,
+                       bitLocation: int, counts, stream=None):
+        """counts[d] (device u32[256], zeroed first) = keys whose transformed
+        key t has t & prefixMask == prefixValue and digit d at bitLocation
+        (thrs_digit_histogram, the multi-GPU split refinement)."""
+        _check(lib().thrs_digit_histogram(ctypes.byref(self._c()), _ptr(inputKeyBuffer), _n(numberOfInputs),
+                                          int(prefixMask) & (2**64 - 1), int(prefixValue) & (2**64 - 1),
+                                          int(bitLocation), _ptr(counts), _stream(stream)))
 
     def checkDeviceError(self, temporaryBuffer, stream=None):
         """Synchronising: raises if a look-back spin bound was hit in the last sort."""

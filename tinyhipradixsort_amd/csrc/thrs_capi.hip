@@ -712,6 +712,30 @@ THRS_API int thrs_partition_pass(const thrs_config* config, const void* keysIn, 
   return partition_impl(config, keysIn, valuesIn, n, tmp, keysOut, valuesOut, bitLocation, counts, stream);
 }
 
+THRS_API int thrs_digit_histogram(const thrs_config* config, const void* keys, uint32_t n, uint64_t prefixMask,
+                                  uint64_t prefixValue, int bitLocation, uint32_t* counts, hipStream_t stream) {
+  if (!config || !valid_key(config->keyType) || !counts) return THRS_ERROR_INVALID_VALUE;
+  if (config->sortOrder != THRS_ORDER_ASCENDING && config->sortOrder != THRS_ORDER_DESCENDING)
+    return THRS_ERROR_INVALID_VALUE;
+  const int kb = key_bytes_of(config->keyType);
+  if (bitLocation < 0 || bitLocation + 8 > kb * 8) return THRS_ERROR_INVALID_VALUE;
+  if (n && !keys) return THRS_ERROR_INVALID_VALUE;
+  if (hipMemsetAsync(counts, 0, kBins * sizeof(uint32_t), stream) != hipSuccess) return THRS_ERROR_HIP;
+  if (n == 0) return THRS_SUCCESS;
+  const bool desc = config->sortOrder == THRS_ORDER_DESCENDING;
+  const uint64_t want = ((uint64_t)n + kHistThreads * 8 - 1) / (kHistThreads * 8);
+  const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cu_count()));
+  if (kb == 4)
+    hipLaunchKernelGGL(thrs_digit_hist_u32, dim3(grid), dim3(kHistThreads), 0, stream,
+                       static_cast<const uint32_t*>(keys), n, config->keyType, desc ? 0xFFFFFFFFu : 0u,
+                       (uint32_t)prefixMask, (uint32_t)prefixValue, bitLocation, counts);
+  else
+    hipLaunchKernelGGL(thrs_digit_hist_u64, dim3(grid), dim3(kHistThreads), 0, stream,
+                       static_cast<const uint64_t*>(keys), n, config->keyType, desc ? ~0ull : 0ull, prefixMask,
+                       prefixValue, bitLocation, counts);
+  return hipGetLastError() == hipSuccess ? THRS_SUCCESS : THRS_ERROR_HIP;
+}
+
 THRS_API int thrs_check_device_error(void* tmp, hipStream_t stream) {
   if (!tmp) return THRS_ERROR_INVALID_VALUE;
   uint32_t err = 0;

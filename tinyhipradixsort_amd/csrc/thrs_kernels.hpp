@@ -343,6 +343,59 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist(const typename KeyTrai
   }
 }
 
+// Digit histogram of the keys matching a prefix (multi-GPU split refinement,
+// tinyhipradixsort_amd/dist.py): counts[d] += #keys whose transformed key t
+// has (t & prefixMask) == prefixValue and digit d at bit `shift`.  One read,
+// any alignment; LDS bins in 32 bank-private copies (conflict-free whatever the
+// skew), merged with one device atomic per bin and workgroup.
+__global__ __launch_bounds__(kHistThreads) void thrs_digit_hist_u32(const uint32_t* __restrict__ keys, uint32_t n,
+                                                                    int keyType, uint32_t orderMask,
+                                                                    uint32_t prefixMask, uint32_t prefixValue,
+                                                                    int shift, uint32_t* __restrict__ counts) {
+  __shared__ uint32_t s_h[kBins * 32];
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t i = tid; i < kBins * 32; i += kHistThreads) s_h[i] = 0;
+  __syncthreads();
+  uint32_t* my = s_h + (tid & 31);
+  for (uint64_t i = (uint64_t)blockIdx.x * kHistThreads + tid; i < n; i += (uint64_t)gridDim.x * kHistThreads) {
+    const uint32_t k = keys[i];
+    const uint32_t t = (keyType == 2 ? KeyTraits<2>::bits(k) : k) ^ orderMask;
+    if ((t & prefixMask) == prefixValue)
+      __hip_atomic_fetch_add(&my[((t >> shift) & 0xFFu) * 32], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  __syncthreads();
+  for (uint32_t b = tid; b < (uint32_t)kBins; b += kHistThreads) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) c += s_h[b * 32 + ((j + b) & 31)];
+    if (c) atomicAdd(&counts[b], c);
+  }
+}
+__global__ __launch_bounds__(kHistThreads) void thrs_digit_hist_u64(const uint64_t* __restrict__ keys, uint32_t n,
+                                                                    int keyType, uint64_t orderMask,
+                                                                    uint64_t prefixMask, uint64_t prefixValue,
+                                                                    int shift, uint32_t* __restrict__ counts) {
+  __shared__ uint32_t s_h[kBins * 32];
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t i = tid; i < kBins * 32; i += kHistThreads) s_h[i] = 0;
+  __syncthreads();
+  uint32_t* my = s_h + (tid & 31);
+  for (uint64_t i = (uint64_t)blockIdx.x * kHistThreads + tid; i < n; i += (uint64_t)gridDim.x * kHistThreads) {
+    const uint64_t k = keys[i];
+    const uint64_t t = (keyType == 3 ? KeyTraits<3>::bits(k) : k) ^ orderMask;
+    if ((t & prefixMask) == prefixValue)
+      __hip_atomic_fetch_add(&my[(uint32_t)((t >> shift) & 0xFFu) * 32], 1u, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  __syncthreads();
+  for (uint32_t b = tid; b < (uint32_t)kBins; b += kHistThreads) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) c += s_h[b * 32 + ((j + b) & 31)];
+    if (c) atomicAdd(&counts[b], c);
+  }
+}
+
 // exclusive scan of each pass's histogram -> global digit bases
 __global__ __launch_bounds__(kThreads) void thrs_scan(const uint32_t* __restrict__ hist, uint32_t* __restrict__ base,
                                                       int nPass, const uint32_t* __restrict__ gate = nullptr) {

@@ -4,32 +4,38 @@ The reference is single-GPU (no collectives anywhere); this is
 the new row s8(e).  One process per GPU; rank r holds a contiguous slice of the
 global input, and rank order is the global order for stability.  The result
 is bit-exact with ONE stable single-GPU sort (tinyhipradixsort.hpp:854-944) of
-the concatenation rank 0 || rank 1 || ... : rank g ends up holding a
-contiguous slice of that sorted sequence.
+the concatenation rank 0 || rank 1 || ... : rank g ends up holding global
+sorted positions [floor(gN/G), floor((g+1)N/G)) -- exactly balanced, whatever
+the key distribution (SURVEY.md s7 hard part 7, s8(e).3).
 
-One sort = five steps:
+One sort:
 
-  1. partition  thrs_partition_pass: ONE stable LSD pass by the digit the
-                reference's LAST pass uses (bit location startBits + 8(P-1),
-                the top digit of the effective window), out of place, which
+  1. partition  thrs_partition_pass: ONE stable pass by the window's TOP digit
+                (bit location of the reference's last pass), out of place; it
                 also yields that digit's 256 bucket counts.
-  2. counts     all_gather of the 256 counts of every rank (1 KiB each) and
-                one device->host copy: all_to_all needs split sizes on the host.
-  3. plan       contiguous digit ranges [b_g, b_g+1) per destination, chosen
-                on the global counts so every rank receives ~total/G keys.
+  2. counts     all_gather of every rank's 256 counts (host copy: all_to_all
+                needs host split sizes).
+  3. split      target g = floor(gN/G) falls in some top-digit bucket b_g at
+                offset o_g.  If o_g > 0 the boundary is refined digit by digit
+                (thrs_digit_histogram of the keys of b_g matching the digits
+                fixed so far, all_gather, pick the digit that holds o_g) until
+                the full sort key v_g is known; the keys equal to v_g are then
+                split in global (source rank, source position) order.  Every
+                rank computes every rank's cut points from the gathered counts.
+                Buckets holding a boundary are sorted locally (stable, same
+                window) so each cut is one position.
   4. exchange   all_to_all_single of keys (then values); rank g receives the
-                segments in source-rank order and each segment in source order.
-  5. finish     a full local sort of the received keys over the same window.
+                segments in source-rank order, each in source order.
+  5. finish     a local stable sort of the received keys over the window.
 
-Why this is exact: for two keys with equal sort bits the top digit is equal,
-so both go to the same destination; they arrive ordered by (source rank,
-source position) -- their global order -- and the local sort is stable.  For
-unequal keys the top digit decides the destination first, and the local
-sort orders within one.  Balance is to a granularity of one top-digit bucket;
-a single-bucket-heavy input (unittest.cpp:191-225's extremeCase) lands on one
-rank, which is correct but unbalanced ("multi-GPU").
+Why this is exact: rank g receives exactly the keys of global ranks
+[T_g, T_g+1) (keys below v_g, plus the first equal ones by (rank, position)).
+Equal keys arrive ordered by (source rank, source position): the partition is
+stable, a split bucket's local sort is stable, segments arrive in source
+order, and the finish is stable -- so the concatenation over ranks is the
+global stable sort.
 
-The local steps are pluggable (`ops`) only so the host logic -- planning,
+The local steps are pluggable (`ops`) only so the host logic -- splitting,
 split sizes, exchange order -- can be tested on CPU ranks over gloo with the
 oracle standing in; the default, and the only product path, is HipLocalOps
 over libthrs.so, which raises if the library is missing.
@@ -56,43 +62,94 @@ def pass_locations(key_bytes: int, start_bits: int, end_bits: int) -> list[int]:
     return [b for b in range(start_bits, end_bits, 8) if b < key_bytes * 8]
 
 
-def assign_ranges(global_counts, world: int) -> list[int]:
-    """Digit bounds b_0=0 <= b_1 <= ... <= b_G=256: destination g receives
-    buckets [b_g, b_g+1).  b_g is the bucket boundary whose exclusive prefix
-    count is closest to g*total/G (ties to the lower boundary), never below
-    b_g-1."""
-    c = np.asarray(global_counts, dtype=np.int64).reshape(BINS)
-    excl = np.concatenate([[0], np.cumsum(c)])           # excl[b] = keys in buckets < b
-    total = int(excl[-1])
-    bounds = [0]
+@dataclass
+class Target:
+    """Global sorted position `pos` = the first key of rank g's output."""
+    pos: int
+    bucket: int              # top-digit bucket holding position pos
+    offset: int              # pos - keys in lower buckets (then: within the fixed prefix); 0 = cut at the start
+    mask: int = 0            # transformed-key digits fixed so far
+    value: int = 0
+    lt: np.ndarray | None = None   # per rank: keys of the bucket below the fixed prefix
+    eq: np.ndarray | None = None   # per rank: keys of the bucket equal to the fixed prefix
+    inside: bool = False     # the cut lies inside the bucket (its keys must be ordered locally)
+
+    @property
+    def refining(self) -> bool:
+        """still inside a group of keys sharing the fixed prefix"""
+        return self.offset > 0
+
+
+def make_targets(counts: np.ndarray, world: int, top_loc: int) -> list[Target]:
+    """counts[r][b] = keys of rank r in top-digit bucket b.  Targets
+    T_g = floor(g N / world), g = 1 .. world-1."""
+    counts = np.asarray(counts, dtype=np.int64)
+    tot = counts.sum(axis=0)
+    excl = np.concatenate([[0], np.cumsum(tot)])
+    n_all = int(excl[-1])
+    out = []
     for g in range(1, world):
-        target = total * g / world
-        lo = bounds[-1]
-        b = lo + int(np.argmin(np.abs(excl[lo:] - target)))
-        bounds.append(b)
-    bounds.append(BINS)
-    return bounds
+        pos = g * n_all // world
+        b = int(np.searchsorted(excl, pos, side="right")) - 1
+        b = min(max(b, 0), BINS - 1)
+        t = Target(pos, b, pos - int(excl[b]), mask=0xFF << top_loc, value=b << top_loc)
+        t.inside = t.offset > 0
+        t.lt = np.zeros(counts.shape[0], np.int64)
+        t.eq = counts[:, b].copy()
+        out.append(t)
+    return out
+
+
+def refine(targets: list[Target], hist: np.ndarray, loc: int):
+    """One refinement level.  hist[r][i][d] = keys of rank r in the bucket of
+    the i-th still-refining target matching its prefix, by the digit at bit
+    `loc`.  Fixes that digit for each of them."""
+    active = [t for t in targets if t.refining]
+    for i, t in enumerate(active):
+        h = np.asarray(hist[:, i, :], dtype=np.int64)
+        tot = h.sum(axis=0)
+        cum = np.cumsum(tot)
+        d = int(np.searchsorted(cum, t.offset, side="right"))   # first digit whose prefix sum exceeds offset
+        t.offset -= int(cum[d] - tot[d])
+        t.lt = t.lt + h[:, :d].sum(axis=1)
+        t.eq = h[:, d].copy()
+        t.mask |= 0xFF << loc
+        t.value |= d << loc
+
+
+def cut_points(counts: np.ndarray, targets: list[Target]) -> np.ndarray:
+    """cuts[r][g], g = 0 .. world: rank r sends positions [cuts[r][g],
+    cuts[r][g+1]) of its partitioned (and split-bucket sorted) keys to rank g.
+    Keys equal to a refined target's full key are split by (rank, position)."""
+    counts = np.asarray(counts, dtype=np.int64)
+    world = counts.shape[0]
+    off = np.concatenate([np.zeros((world, 1), np.int64), np.cumsum(counts, axis=1)], axis=1)  # off[r][b]
+    cuts = np.zeros((world, world + 1), np.int64)
+    cuts[:, world] = counts.sum(axis=1)
+    for g, t in enumerate(targets, start=1):
+        c = off[:, t.bucket].copy()
+        if t.inside:
+            # keys below the final prefix group, + rank r's keys of the group
+            # below the cut (the group split in (rank, position) order)
+            eq_before = np.concatenate([[0], np.cumsum(t.eq)[:-1]])
+            c += t.lt + np.clip(t.offset - eq_before, 0, t.eq)
+        cuts[:, g] = c
+    return cuts
 
 
 @dataclass
 class ExchangePlan:
-    bounds: list[int]
-    send: list[int]          # keys this rank sends to each destination
-    recv: list[int]          # keys this rank receives from each source
+    cuts: np.ndarray         # [world][world+1]
+    rank: int
+    send: list[int] = field(init=False)
+    recv: list[int] = field(init=False)
     n_out: int = field(init=False)
 
     def __post_init__(self):
+        c = self.cuts
+        self.send = [int(c[self.rank, g + 1] - c[self.rank, g]) for g in range(c.shape[0])]
+        self.recv = [int(c[src, self.rank + 1] - c[src, self.rank]) for src in range(c.shape[0])]
         self.n_out = int(sum(self.recv))
-
-
-def exchange_plan(all_counts, rank: int) -> ExchangePlan:
-    """all_counts[src][d] = keys of source rank src in bucket d."""
-    a = np.asarray(all_counts, dtype=np.int64)
-    world = a.shape[0]
-    bounds = assign_ranges(a.sum(axis=0), world)
-    send = [int(a[rank, bounds[g]:bounds[g + 1]].sum()) for g in range(world)]
-    recv = [int(a[src, bounds[rank]:bounds[rank + 1]].sum()) for src in range(world)]
-    return ExchangePlan(bounds, send, recv)
 
 
 # ----------------------------------------------------------------- local ops
@@ -101,9 +158,12 @@ class HipLocalOps:
 
     def __init__(self, config: RadixSort.Config):
         self.rs = RadixSort([], config)
+        # the finish: a rank's keys share ~256/world top digits, so the bucket
+        # path's 16-bit buckets would overflow its local sort (fallback + a
+        # wasted bucket histogram): plain LSD passes, asked for explicitly
         self.rs_lsd = RadixSort([], config, Options(path="lsd"))
         self._tmp = None
-        self.lsd_finish = False  # set by DistributedRadixSort for world > 1 (see sort)
+        self.lsd_finish = False  # set by DistributedRadixSort for world > 1
 
     def temp(self, n: int, like):
         import torch
@@ -122,16 +182,18 @@ class HipLocalOps:
         self.rs.partitionPass(keys, vals, n, self.temp(n, keys), pk, pv, bit, counts)
         return pk, pv, counts
 
-    def sort(self, keys, vals, n: int, start_bits: int, end_bits: int):
+    def histogram(self, keys, n: int, mask: int, value: int, bit: int):
+        """device int32[256]: digit histogram of the keys matching the prefix."""
+        import torch
+        h = torch.empty(BINS, dtype=torch.int32, device=keys.device)
+        self.rs.digitHistogram(keys, n, mask, value, bit, h)
+        return h
+
+    def sort(self, keys, vals, n: int, start_bits: int, end_bits: int, finish: bool = True):
         if n == 0:
             return
         tmp = self.temp(n, keys)
-        # A rank's keys share 256/world top digits, so the 3-HBM-pass path's
-        # 16-bit buckets would hold ~world * 2^14 keys each: always over the
-        # local sort's capacity, i.e. its fallback plus a wasted bucket
-        # histogram.  For world > 1 the finish asks for the plain LSD path
-        # (an explicit per-call option: DESIGN.md s4).
-        rs = self.rs_lsd if self.lsd_finish else self.rs
+        rs = self.rs_lsd if (finish and self.lsd_finish) else self.rs
         if vals is None:
             rs.sortKeys(keys, n, tmp, start_bits, end_bits)
         else:
@@ -161,6 +223,7 @@ class DistributedRadixSort:
             self.ops.lsd_finish = self.world > 1
         self.backend = dist.get_backend(group)
         self.last_plan: ExchangePlan | None = None
+        self.last_targets: list[Target] = []
 
     # keys/values travel as flat byte tensors
     @staticmethod
@@ -178,14 +241,16 @@ class DistributedRadixSort:
             return
         self.dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
 
-    def _all_counts(self, counts):
+    def _gather(self, t):
+        """all_gather of a small int tensor -> host numpy [world, *t.shape]
+        (a host synchronisation)."""
         import torch
-        c = counts.to(torch.int64)
+        c = t.to(torch.int64)
         if self.backend == "gloo" and c.device.type != "cpu":
             c = c.cpu()
         parts = [torch.empty_like(c) for _ in range(self.world)]
         self.dist.all_gather(parts, c, group=self.group)
-        return torch.stack(parts).cpu().numpy()         # the one host sync of the sort
+        return torch.stack(parts).cpu().numpy()
 
     def sort(self, keys, n: int | None = None, values=None, start_bits: int = 0, end_bits: int | None = None,
              timings: dict | None = None):
@@ -211,9 +276,32 @@ class DistributedRadixSort:
         k_in, v_in = kflat[:n * kb], (vflat[:n * vb] if vflat is not None else None)
         pk, pv, counts = self.ops.partition(k_in, v_in, n, locs[-1])
         clock.mark("partition")
-        plan = exchange_plan(self._all_counts(counts), self.rank)
-        self.last_plan = plan
+        all_counts = self._gather(counts)                       # [world][256]
         clock.mark("counts")
+        targets = make_targets(all_counts, self.world, locs[-1])
+        self.last_targets = targets
+        mine = all_counts[self.rank]
+        off = np.concatenate([[0], np.cumsum(mine)])
+        # refinement: one level per lower digit while a boundary lies inside a bucket
+        for loc in reversed(locs[:-1]):
+            active = [t for t in targets if t.refining]
+            if not active:
+                break
+            hs = []
+            for t in active:
+                lo, cnt = int(off[t.bucket]), int(mine[t.bucket])
+                hs.append(self.ops.histogram(pk[lo * kb:(lo + cnt) * kb], cnt, t.mask, t.value, loc))
+            refine(targets, self._gather(torch.stack(hs)), loc)
+        # buckets holding a refined boundary: stable local sort, so each cut is one position
+        if len(locs) > 1:
+            for b in sorted({t.bucket for t in targets if t.inside}):
+                lo, cnt = int(off[b]), int(mine[b])
+                if cnt > 1:
+                    self.ops.sort(pk[lo * kb:(lo + cnt) * kb], pv[lo * vb:(lo + cnt) * vb] if vb else None, cnt,
+                                  start_bits, end_bits, finish=False)
+        plan = ExchangePlan(cut_points(all_counts, targets), self.rank)
+        self.last_plan = plan
+        clock.mark("split")
         rk = torch.empty(plan.n_out * kb, dtype=torch.uint8, device=dev)
         self._a2a(rk, pk, [c * kb for c in plan.recv], [c * kb for c in plan.send])
         rv = None
