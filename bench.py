@@ -46,6 +46,7 @@ WORKLOADS = {
     "c3": (0, 4, 1 << 30, "uniform", "C3: sortPairs u32 key + u32 index payload (stable), N=2^30"),
     "c4": (2, 0, 1 << 28, "uniform", "C4: sortKeys f32 via fpKey transform, N=2^28 (bits & 0xFF7FFFFF)"),
     "c5": (1, 8, 1 << 30, "uniform", "C5: sortPairs u64 key + u64 index payload, 2^30 per GPU"),
+    "u64k": (1, 0, 1 << 30, "uniform", "sortKeys u64, N=2^30 uniform (64-bit keys without payload)"),
     # low-entropy inputs of C2's shape (not bench lines of BASELINE.json: robustness)
     "c2_sorted": (0, 0, 1 << 30, "sorted", "C2 shape, already-sorted input (stratified sorted uniform sample)"),
     "c2_reverse": (0, 0, 1 << 30, "reverse", "C2 shape, reverse-sorted input"),
@@ -465,7 +466,7 @@ def main():
             lm = prof["local_ms"] / prof["local_launches"]
             la = alg_bytes / (lm / 1e3) / 1e9
             # (u32 keys over the whole key above 2^29: 16-bit items; u32 pairs: items carry positions)
-            lk = ("thrs_local_pairs" if vb else
+            lk = ("thrs_local64" if kb == 8 else "thrs_local_pairs" if vb else
                   "thrs_local16" if (kt == 0 and n > (1 << 29))
                   else "thrs_local")
             roof["local"] = {"kernel": lk, "avg_launch_ms": round(lm, 4), "achieved": round(la, 1),

@@ -228,6 +228,39 @@ def test_hybrid_pairs_vs_oracle(gpu, desc, geom):
                 assert np.array_equal(v, ev), (name, n, s, e)
 
 
+@pytest.mark.parametrize("kt", [O.U64, O.F64])
+@pytest.mark.parametrize("vb", [0, 8])
+@pytest.mark.parametrize("desc", [False, True])
+def test_bucket64_vs_oracle(gpu, kt, vb, desc):
+    """8-byte keys (with or without 8-byte values) over the whole key take the
+    bucket path (forced here for every size; by default n in [2^28, 2^30 +
+    2^24]): two device passes on the top 16 bits, six in-LDS rounds per
+    bucket (thrs_local64), u64 keys rebuilt / f64 keys and values permuted by
+    carried positions; a bucket above 17408 keys takes the LSD fallback."""
+    torch = gpu
+    rs = make_sorter(kt, vb, desc, path="bucket")
+    mask48 = np.uint64(0xFFFF000000000000)
+    dists = {
+        "uniform": lambda k: k,
+        "low40": lambda k: k & np.uint64(0xFFFFFFFFFF),                  # one bucket -> fallback above 17408
+        "top_fixed": lambda k: (k & ~mask48) | np.uint64(0x3FF0000000000000),
+        "ties": lambda k: k & np.uint64(0xFFFF0000FF00FF00),
+        "const": lambda k: np.full_like(k, k[0]),
+        "signed_zero": lambda k: np.where(k & np.uint64(1), np.uint64(0x8000000000000000), np.uint64(0)),
+    }
+    j = 0
+    for name, f in dists.items():
+        for n in [1, 100, 17408, 17409, 70001, 300007, 1 << 20]:
+            j += 1
+            keys = f(O.randomize_np(kt, O.splitmix64_stream(4242 * j, n))).astype(np.uint64)
+            vals = np.arange(n, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15) if vb else None
+            k, v = gpu_sort(torch, rs, {"keys": keys, "values": vals}, kt, vb, 0, 64)
+            ek, ev = O.lsd_sort(kt, keys, vals, 0, 64, desc)
+            assert np.array_equal(k, ek), (name, n)
+            if vb:
+                assert np.array_equal(v, ev), (name, n)
+
+
 def test_concurrent_sorts_on_distinct_temps(gpu):
     """Per-call state lives in the caller's temp buffer: two sorts on two
     streams at once (the reference's module-global g_iterator would race)."""
@@ -309,7 +342,9 @@ def test_f32_raw_bits_with_nan_inf_full_size(gpu):
 
 @pytest.mark.large
 @pytest.mark.parametrize("kt,vb,n", [(O.U32, 4, 1 << 30),     # C3
-                                     (O.U64, 8, 1 << 28),     # C5's per-GPU local shape, reduced
+                                     (O.U64, 8, 1 << 30),     # C5's per-GPU local shape
+                                     (O.U64, 8, 1 << 28),
+                                     (O.F64, 8, 1 << 29),
                                      (O.F32, 8, 1 << 27),
                                      (O.U64, 16, 1 << 26)])
 def test_full_size_pairs_stability(gpu, kt, vb, n):

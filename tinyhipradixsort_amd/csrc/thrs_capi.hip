@@ -287,8 +287,11 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   VW* valOut = static_cast<VW*>(valOutBuf);
 
   const U orderMask = desc ? (U)~(U)0 : (U)0;
-  // 4-byte keys without values; u32 keys with 4-byte values over the whole key
-  constexpr bool kBucketType = sizeof(U) == 4 && (VB == 0 || (VB == 4 && KT == 0));
+  // 4-byte keys without values; u32 keys with 4-byte values over the whole
+  // key; 8-byte keys without values or with 8-byte values over the whole key
+  constexpr bool kBucket32 = sizeof(U) == 4 && (VB == 0 || (VB == 4 && KT == 0));
+  constexpr bool kBucket64 = sizeof(U) == 8 && (VB == 0 || VB == 8);
+  constexpr bool kBucketType = kBucket32 || kBucket64;
   const bool fullWindow = startBits == 0 && nPass * 8 >= (int)(8 * sizeof(U));
   // Size window of the default (uniform keys: n / 65536 keys per bucket;
   // docs/EXPERIMENTS.md row 29): the local sort costs about the same per chunk
@@ -299,14 +302,16 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   // Local geometries (thrs_hybrid.hpp LocG): LocSmall (9216-key chunks,
   // uniform buckets of 4-8K keys) for n <= 2^29, LocBig (18432) above.
   const uint64_t nn = n;
-  const bool sizeOk = nn >= (1ull << 28) && nn <= (1ull << 30) + (1ull << 26);
+  // (8-byte keys: one 17408-slot chunk per bucket, so up to 2^30 + 2^24: the
+  // largest uniform bucket stays ~3 sigma below the capacity)
+  const bool sizeOk = nn >= (1ull << 28) && nn <= (1ull << 30) + (sizeof(U) == 8 ? (1ull << 24) : (1ull << 26));
   const bool smallLocal = opt.localGeometry == THRS_LOCAL_SMALL ? true
                           : (opt.localGeometry == THRS_LOCAL_BIG || opt.localGeometry == THRS_LOCAL_BIG32)
                               ? false
                               : nn <= (1ull << 29);
   const bool bucket = kBucketType && !counts && nPass >= 3 &&
                       (opt.path == THRS_PATH_BUCKET || (opt.path == THRS_PATH_AUTO && sizeOk)) &&
-                      (VB == 0 || fullWindow);
+                      ((kBucket32 && VB == 0) || fullWindow);
   const int nLow = nPass - 2;
   // u32 keys over the whole key, large chunks: the local sort on 16-bit items
   // (thrs_hybrid.hpp thrs_local16) over single-bucket chunks
@@ -338,7 +343,10 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   if (bucket) {
     if (allow_lds(thrs_hist_joint<KT>, kJointLds) != hipSuccess || allow_lds(sk, lds) != hipSuccess)
       return THRS_ERROR_HIP;
-    if constexpr (kBucketType) {
+    if constexpr (kBucket64) {
+      if (allow_lds(atomicRank ? thrs_local64<KT, VB, true> : thrs_local64<KT, VB, false>, Loc64::LDS) != hipSuccess)
+        return THRS_ERROR_HIP;
+    } else if constexpr (kBucketType) {
       if (local16) {
         if constexpr (KT == 0 && VB == 0)
           if (allow_lds(atomicRank ? thrs_local16<true, Loc16> : thrs_local16<false, Loc16>, Loc16::LDS) !=
@@ -390,8 +398,8 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                          reinterpret_cast<uint32_t*>(hyb + kSegHistAOff));
       // chunks: whole buckets; neighbouring buckets below kLocCap/2 keys share one
       hipLaunchKernelGGL(thrs_plan, dim3(1), dim3(kPlanThreads), 0, stream, joint, n, base + nLow * kBins, chunkOff,
-                         chunkB0, meta, smallLocal ? LocSmall::CAP : LocBig::CAP,
-                         (VB || local16) ? -1 : (smallLocal ? kLocSmallLogT : kLocLogT),  // -1: single-bucket chunks
+                         chunkB0, meta, kBucket64 ? Loc64::CAP : smallLocal ? LocSmall::CAP : LocBig::CAP,
+                         (VB || local16 || kBucket64) ? -1 : (smallLocal ? kLocSmallLogT : kLocLogT),  // -1: single-bucket chunks
                          reinterpret_cast<uint32_t*>(hyb + kSegInfoOff), reinterpret_cast<uint32_t*>(hyb + kSegBaseOff),
                          (uint32_t)G::TILE, reinterpret_cast<const uint32_t*>(hyb + kSegHistAOff), (uint32_t)hgrid,
                          reinterpret_cast<uint32_t*>(hyb + kSegInfoAOff), reinterpret_cast<uint32_t*>(hyb + kSegBaseAOff));
@@ -468,8 +476,8 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
       }
       if (nLow & 1) {  // fallback result is in keyOut: the top-digit passes read K
         hipLaunchKernelGGL(thrs_copy_gated, dim3(2048), dim3(256), 0, stream,
-                           reinterpret_cast<const uint32_t*>(keyOut), reinterpret_cast<uint32_t*>(K), (uint64_t)n,
-                           fallback, 1u);
+                           reinterpret_cast<const uint32_t*>(keyOut), reinterpret_cast<uint32_t*>(K),
+                           (uint64_t)n * sizeof(U) / 4, fallback, 1u);
         if (VB)
           hipLaunchKernelGGL(thrs_copy_gated, dim3(2048), dim3(256), 0, stream,
                              reinterpret_cast<const uint32_t*>(valOut), reinterpret_cast<uint32_t*>(V),
@@ -526,7 +534,9 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
       auto launch_local = [&](auto geom) {
         using LG = decltype(geom);
         const size_t llds = LG::template lds<U>();
-        if constexpr (VB == 4) {
+        if constexpr (kBucket64) {
+          (void)llds;
+        } else if constexpr (VB == 4) {
           auto lk = atomicRank ? thrs_local_pairs<true, LG> : thrs_local_pairs<false, LG>;
           hipLaunchKernelGGL(lk, dim3((uint32_t)maxChunks), dim3(LG::THREADS), llds, stream,
                              reinterpret_cast<uint32_t*>(K), reinterpret_cast<uint32_t*>(V), (uint32_t)orderMask,
@@ -537,7 +547,12 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                              nLow, chunkOff, chunkB0, meta, g_lstamps);
         }
       };
-      if (local16) {
+      if constexpr (kBucket64) {
+        auto lk = atomicRank ? thrs_local64<KT, VB, true> : thrs_local64<KT, VB, false>;
+        hipLaunchKernelGGL(lk, dim3((uint32_t)maxChunks), dim3(Loc64::THREADS), Loc64::LDS, stream,
+                           reinterpret_cast<uint64_t*>(K), reinterpret_cast<uint64_t*>(V), (uint64_t)orderMask,
+                           chunkOff, chunkB0, meta);
+      } else if (local16) {
         if constexpr (KT == 0 && VB == 0) {
           auto lk = atomicRank ? thrs_local16<true, Loc16> : thrs_local16<false, Loc16>;
           hipLaunchKernelGGL(lk, dim3((uint32_t)maxChunks), dim3(Loc16::THREADS), Loc16::LDS, stream,

@@ -993,6 +993,153 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(4))
   }
 }
 
+// ------------------------------------------------ local sort, 64-bit keys
+// u64 / f64 keys over the whole key (startBits 0, 64 bits), optionally with
+// 8-byte values: the bucket path's two device passes group the keys by their
+// top 16 bits; each single-bucket chunk then takes SIX in-LDS rounds on the
+// low 48 bits.  Item = low48(image) << 16 | chunk position (positions <
+// 17408 < 2^16), so the rounds sort by item bits 16..63 (stable, the same
+// count / scan / lane-ordered rank / scatter / reload as loc_rounds), and the
+// carried position permutes what cannot be rebuilt from the item: the values,
+// and f64 keys (+0 and -0 share one image).  u64 keys are rebuilt from the
+// bucket id and the item.  One workgroup of 16 waves x 17 items = 17408
+// slots: 136 KiB of 8-byte stage + 16 KiB of per-wave counters, one per CU.
+struct Loc64 {
+  static constexpr int WAVES = 16, KPT = 17, THREADS = 64 * WAVES;
+  static constexpr uint32_t CAP = (uint32_t)THREADS * KPT;  // 17408
+  static constexpr size_t LDS = (size_t)CAP * 8 + (size_t)WAVES * kBins * 4;
+};
+static_assert(Loc64::CAP < 65536, "positions are carried in 16 bits");
+
+template <int KT, int VB, bool ATOMIC_RANK>
+__global__ __launch_bounds__(Loc64::THREADS) void thrs_local64(uint64_t* __restrict__ keys,
+                                                              uint64_t* __restrict__ vals, uint64_t orderMask,
+                                                              const uint32_t* __restrict__ chunkOff,
+                                                              const uint32_t* __restrict__ chunkB0,
+                                                              const uint32_t* __restrict__ meta) {
+  static_assert(KT == 1 || KT == 3, "64-bit keys");
+  static_assert(VB == 0 || VB == 8, "no values or 8-byte values");
+  constexpr int KPT = Loc64::KPT, W = Loc64::WAVES;
+  constexpr uint32_t CHUNK = 64 * KPT;
+  constexpr bool PERMUTE_KEYS = KT == 3;  // f64: keys travel by position (their -0 is not rebuilt)
+  if (meta[kMetaFallback] != 0) return;   // the plain LSD passes sorted everything
+  const uint32_t c = blockIdx.x;
+  if (c >= meta[kMetaChunks]) return;
+  const uint32_t start = chunkOff[c], size = chunkOff[c + 1] - start;
+  if (size == 0) return;
+  const uint64_t hiImg = (uint64_t)chunkB0[c] << 48;  // the bucket: the image's top 16 bits
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint64_t* stage = reinterpret_cast<uint64_t*>(smem);
+  uint32_t* s_cnt = reinterpret_cast<uint32_t*>(smem + (size_t)Loc64::CAP * 8);  // [W][256]
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  uint32_t* cnt = s_cnt + w * kBins;
+  const uint64_t* stw = stage + w * CHUNK + lane;
+  const uint32_t myOff = w * CHUNK + lane;
+  int32_t lim = (int32_t)size - (int32_t)myOff;
+  pin(reinterpret_cast<uint32_t&>(lim));
+  const int32_t limw = __builtin_amdgcn_readfirstlane((int32_t)size - (int32_t)(w * CHUNK));
+  const int nItems = limw <= 0 ? 0 : min(KPT, (limw + 63) >> 6);  // items j with j*64 < limw
+
+  // items: low 48 bits of the image and the position; padding (past the
+  // chunk) has every digit 255 and sorts last (stable: it sits at the end)
+  uint64_t it[KPT];
+  load_run<KPT>(it, keys + start, myOff, size, limw);
+#pragma unroll
+  for (int j = 0; j < KPT; ++j) {
+    const uint64_t img = KeyTraits<KT>::bits(it[j]) ^ orderMask;
+    it[j] = (j * 64 < lim) ? ((img << 16) | (uint64_t)(myOff + j * 64)) : ~0xFFFFull;
+  }
+  for (int r = 0; r < 6; ++r) {
+    const int shift = 16 + 8 * r;
+    auto digit_of = [&](int j) -> uint32_t { return (uint32_t)(it[j] >> shift) & 0xFFu; };
+#pragma unroll
+    for (int i = 0; i < kBins / 64; ++i) cnt[i * 64 + lane] = 0;
+#pragma unroll
+    for (int j = 0; j < KPT; ++j)
+      if (j < nItems) __hip_atomic_fetch_add(&cnt[digit_of(j)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    lds_barrier();
+    {  // digit totals over the waves -> block exclusive scan -> per-wave running offsets
+      uint32_t* s_wt = reinterpret_cast<uint32_t*>(smem);  // stage words: free until the scatter
+      uint32_t cw[W], tot = 0, inc = 0;
+      if (tid < kBins) {
+#pragma unroll
+        for (int ww = 0; ww < W; ++ww) {
+          cw[ww] = s_cnt[ww * kBins + tid];
+          tot += cw[ww];
+        }
+        inc = wave_incl_scan(tot, lane);
+        if (lane == 63) s_wt[w] = inc;
+      }
+      lds_barrier();
+      if (tid < kBins) {
+        const uint32_t w0 = s_wt[0], w1 = s_wt[1], w2 = s_wt[2];
+        uint32_t run = inc - tot + (w > 0 ? w0 : 0u) + (w > 1 ? w1 : 0u) + (w > 2 ? w2 : 0u);
+#pragma unroll
+        for (int ww = 0; ww < W; ++ww) {
+          s_cnt[ww * kBins + tid] = run;
+          run += cw[ww];
+        }
+      }
+    }
+    lds_barrier();
+    constexpr int RB = 9;
+#pragma unroll
+    for (int j0 = 0; j0 < KPT; j0 += RB) {
+      uint32_t sl[RB];
+#pragma unroll
+      for (int jj = 0; jj < RB; ++jj) {
+        const int j = j0 + jj;
+        if (j < KPT && j < nItems) sl[jj] = wave_rank<ATOMIC_RANK>(cnt, digit_of(j), lane, false);
+      }
+#pragma unroll
+      for (int jj = 0; jj < RB; ++jj)
+        if (j0 + jj < KPT && j0 + jj < nItems) stage[sl[jj]] = it[j0 + jj];
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    lds_barrier();
+    if (r < 5) {
+#pragma unroll
+      for (int j = 0; j < KPT; ++j)
+        if (j < nItems) it[j] = stw[j * 64];
+    }
+  }
+  // sorted items: this lane's output slots myOff + 64j; every stage read
+  // first (in bounds for all lanes), then the lane-conditional stores
+#pragma unroll
+  for (int j = 0; j < KPT; ++j) it[j] = stw[j * 64];
+  uint64_t* kdst = keys + start + myOff;
+  if constexpr (!PERMUTE_KEYS) {
+#pragma unroll
+    for (int j = 0; j < KPT; ++j)
+      if (j * 64 < lim) kdst[j * 64] = (hiImg | (it[j] >> 16)) ^ orderMask;  // u64: image == key ^ orderMask
+  }
+  if constexpr (PERMUTE_KEYS || VB == 8) {
+    // carried positions; then each permuted array goes through the stage
+    uint32_t pos[(KPT + 1) / 2];
+#pragma unroll
+    for (int j = 0; j < (KPT + 1) / 2; ++j) pos[j] = 0;
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) pos[j / 2] |= (uint32_t)(it[j] & 0xFFFFu) << (16 * (j & 1));
+    auto permute = [&](uint64_t* arr) {
+      uint64_t x[KPT];
+      load_run<KPT>(x, arr + start, myOff, size, limw);
+      lds_barrier();  // every stage read of the previous step is done
+#pragma unroll
+      for (int j = 0; j < KPT; ++j)
+        if (j < nItems) stage[myOff + j * 64] = x[j];
+      lds_barrier();
+#pragma unroll
+      for (int j = 0; j < KPT; ++j) x[j] = stage[(pos[j / 2] >> (16 * (j & 1))) & 0xFFFFu];
+#pragma unroll
+      for (int j = 0; j < KPT; ++j)
+        if (j * 64 < lim) arr[start + myOff + j * 64] = x[j];
+    };
+    if constexpr (PERMUTE_KEYS) permute(keys);
+    if constexpr (VB == 8) permute(vals);
+  }
+}
+
 // Copy on the fallback path only (odd number of low passes: their result is
 // in the temporary buffer; the two top-digit passes read the caller's).
 __global__ void thrs_copy_gated(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, uint64_t words,
