@@ -41,8 +41,8 @@ clean:
 # Tuning variants of libthrs.so for scripts/sweep.py: VARIANTS="name:-DFLAG=V+-DFLAG2=W ..."
 VARIANTS ?= stamps:-DTHRS_STAMPS
 variants:
-	@mkdir -p build/variants
+	@mkdir -p exp/variants
 	@for v in $(VARIANTS); do name=$${v%%:*}; flags=$$(echo $${v#*:} | tr '+' ' '); \
 	  echo "variant $$name: $$flags"; \
-	  $(HIPCC) $(HIPFLAGS) $$flags -shared -o build/variants/libthrs_$$name.so $(PKG)/csrc/thrs_capi.hip & done; wait
+	  $(HIPCC) $(HIPFLAGS) $$flags -shared -o exp/variants/libthrs_$$name.so $(PKG)/csrc/thrs_capi.hip & done; wait
 .PHONY: variants

@@ -71,6 +71,7 @@ def parse():
                    help="time the reference's own kernels (oracle/_ref) on the same inputs (N=1 only)")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--quiet", action="store_true")
+    p.add_argument("--lib", default=None, help="experiments: a variant build of libthrs.so (make variants)")
     p.add_argument("--force-dist", action="store_true",
                    help="run the bucket-exchange path even at world size 1 (RCCL smoke test)")
     return p.parse_args()
@@ -274,6 +275,8 @@ def main():
 
     import tinyhipradixsort_amd as T
     from tinyhipradixsort_amd import testutil as TU
+    if args.lib:
+        T.LIB_PATH = os.path.abspath(args.lib)
 
     wl = args.workload or "c2"
     kt, vb, n_default, dist_name, desc = WORKLOADS[wl]

@@ -9,7 +9,7 @@ TAG=${1:-r01}; WL=${2:-c2}
 OUT=gpurun_out/prof_${TAG}_${WL}
 mkdir -p $OUT
 # 1) the bench command itself (its thrs_pass average must agree with bench.py's roofline)
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/bench -o run -- python3 bench.py --workload $WL --steps 5 --warmup 1 --cpu-baseline off > $OUT/bench.json 2> $OUT/bench.log || { echo "bench trace failed"; tail -5 $OUT/bench.log; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/bench -o run -- python3 bench.py --workload $WL --steps 5 --warmup 1 --cpu-baseline off --vendor off --ref-gpu off > $OUT/bench.json 2> $OUT/bench.log || { echo "bench trace failed"; tail -5 $OUT/bench.log; exit 1; }
 cat $OUT/bench.json
 # 2) calibration copies + sorts: trace, then one --pmc pass per counter group
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 scripts/profile_run.py --workload $WL > $OUT/trace.log 2>&1 || { echo "trace failed"; tail -5 $OUT/trace.log; exit 1; }

@@ -499,7 +499,7 @@ template <> struct PassCfg<4, 0> {
   static constexpr int WAVES = CFG[0], KPT = CFG[1], ROUNDS = CFG[2], WPE = CFG[3];
 };
 #ifndef THRS_K4V4_CFG
-#define THRS_K4V4_CFG 16, 16, 4, 4
+#define THRS_K4V4_CFG 16, 16, 2, 4
 #endif
 #ifndef THRS_K4V8_CFG
 #define THRS_K4V8_CFG 16, 16, 8, 4
@@ -514,7 +514,7 @@ template <> struct PassCfg<4, 0> {
 #define THRS_K8V4_CFG 16, 16, 8, 4
 #endif
 #ifndef THRS_K8V8_CFG
-#define THRS_K8V8_CFG 8, 16, 2, 4
+#define THRS_K8V8_CFG 8, 8, 1, 4
 #endif
 #ifndef THRS_K8V16_CFG
 #define THRS_K8V16_CFG 16, 8, 8, 4
@@ -767,7 +767,12 @@ __device__ __forceinline__ void pass_tile(
   uint32_t* s_cnt = reinterpret_cast<uint32_t*>(smem + STAGE * (sizeof(U) + VB));  // [WAVES][256]
   uint32_t* s_gofs = s_cnt + WAVES * kBins;
   uint32_t* s_misc = s_gofs + kBins;
-  const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // tid is re-derived per tile (pinned): in the persistent kernels the
+  // addresses computed from it would otherwise be hoisted out of the tile
+  // loop and spilled to scratch (this kernel is at its VGPR limit)
+  uint32_t tid0 = threadIdx.x;
+  pin(tid0);
+  const uint32_t tid = tid0, lane = tid & 63, w = tid >> 6;
 #ifdef THRS_STAMPS
   uint64_t* s_stamp = reinterpret_cast<uint64_t*>(s_misc + 16);  // flushed once per tile (a global
                                                                   // store mid-tile would perturb timing)
