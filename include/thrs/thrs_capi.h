@@ -63,6 +63,7 @@ enum { THRS_LOCAL_AUTO = 0, THRS_LOCAL_BIG = 1, THRS_LOCAL_SMALL = 2, THRS_LOCAL
 enum { THRS_SEG_AUTO = 0, THRS_SEG_TOP_ONLY = 1, THRS_SEG_NONE = 2 };
 enum { THRS_CLAIMS_AUTO = 0, THRS_CLAIMS_XCD_BLOCKS = 1, THRS_CLAIMS_TICKET = 2 };
 enum { THRS_RANK_AUTO = 0, THRS_RANK_ATOMIC = 1, THRS_RANK_BALLOT = 2 };
+enum { THRS_PLANES_AUTO = 0, THRS_PLANES_ON = 1, THRS_PLANES_OFF = 2 };
 typedef struct thrs_options {
   int32_t path;          /* THRS_PATH_*: LSD = one device pass per digit; BUCKET = the
                             3-HBM-pass path wherever the key/value types and window
@@ -75,7 +76,12 @@ typedef struct thrs_options {
   int32_t rank;          /* THRS_RANK_*: in-tile rank by lane-ordered LDS atomics
                             (AUTO: where the per-device probe confirms the order) or
                             by the 8-ballot match                                    */
-  int32_t reserved[3];   /* zero */
+  int32_t planes;        /* THRS_PLANES_*: u32 keys-only bucket path with 16-bit items:
+                            the top-digit passes carry the keys as a u16 + a u8
+                            plane (12 instead of 16 bytes per key over the two
+                            passes, 6 instead of 8 in the local sort).  AUTO = ON
+                            where it applies; OFF = full keys                      */
+  int32_t reserved[2];   /* zero */
 } thrs_options;
 
 /* == RadixSort::TemporaryBufferDef (tinyhipradixsort.hpp:806-832).

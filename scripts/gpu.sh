@@ -53,7 +53,7 @@ for step in "$@"; do
       # per-kernel durations of a short bench run (no counters)
       wl=$arg
       timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/stats_$wl -o run -- \
-        python3 bench.py --workload $wl --steps 3 --warmup 1 --cpu-baseline off --vendor off \
+        python3 bench.py --workload $wl --steps 3 --warmup 1 --cpu-baseline off --vendor off --ref-gpu off \
         > gpurun_out/stats_$wl.json 2> gpurun_out/stats_$wl.err || { echo "STATS $wl FAILED"; tail -20 gpurun_out/stats_$wl.err; exit 1; }
       cat gpurun_out/stats_$wl.json
       python3 - "$wl" <<'PY'

@@ -110,7 +110,8 @@ class _CConfig(ctypes.Structure):
 
 class _COptions(ctypes.Structure):
     _fields_ = [("path", ctypes.c_int32), ("localGeometry", ctypes.c_int32), ("segmented", ctypes.c_int32),
-                ("tileClaims", ctypes.c_int32), ("rank", ctypes.c_int32), ("reserved", ctypes.c_int32 * 3)]
+                ("tileClaims", ctypes.c_int32), ("rank", ctypes.c_int32), ("planes", ctypes.c_int32),
+                ("reserved", ctypes.c_int32 * 2)]
 
 
 @dataclass
@@ -123,10 +124,11 @@ class Options:
     segmented: str = "auto"       # auto | top_only | none
     tileClaims: str = "auto"      # auto | xcd_blocks | ticket
     rank: str = "auto"            # auto | atomic | ballot
+    planes: str = "auto"          # auto | on | off
 
     _ENUMS = {"path": ("auto", "lsd", "bucket"), "localGeometry": ("auto", "big", "small", "big32"),
               "segmented": ("auto", "top_only", "none"), "tileClaims": ("auto", "xcd_blocks", "ticket"),
-              "rank": ("auto", "atomic", "ballot")}
+              "rank": ("auto", "atomic", "ballot"), "planes": ("auto", "on", "off")}
 
     def _c(self) -> "_COptions":
         o = _COptions()

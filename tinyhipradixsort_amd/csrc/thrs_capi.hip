@@ -73,7 +73,8 @@ struct Plan {
   uint64_t setBytes;      // one look-back table set = status + ga + gp
   uint64_t claimBytes;    // per pass: XCD-block claim state (tickets, block counter, 8 block tables)
   uint64_t hybridOff;     // 3-pass path (thrs_hybrid.hpp): bucket histogram, chunk table, meta
-  uint64_t scratchBytes;  // header + 2 sets (ping-pong between passes) + 8 claim areas + hybrid area
+  uint64_t hiPlaneOff;    // u32 keys without values: the bucket path's u8 plane (n bytes)
+  uint64_t scratchBytes;  // header + 2 sets (ping-pong between passes) + 8 claim areas + hybrid area [+ u8 plane]
 };
 
 // hybrid area: u32 joint[65536] | segHistA[8][256] | chunkOff[65537] |
@@ -110,6 +111,11 @@ Plan make_plan(int keyType, int valueBytesOrZero, uint32_t n) {
   p.claimBytes = round_up((16 + 8 * nXb) * 4, kAlign);
   p.hybridOff = kHeaderBytes + 2 * p.setBytes + 8 * p.claimBytes;
   p.scratchBytes = p.hybridOff + kHybridBytes;
+  // the u8 plane of the planes codecs (thrs_kernels.hpp kCodecSplit): the u16
+  // planes fill keyOut, which is all a sortKeys caller must allocate
+  // (getTemporaryBufferBytesForSortKeys = pSumBuffer + keyOutBuffer)
+  p.hiPlaneOff = p.scratchBytes;
+  if (keyType == THRS_KEY_U32 && valueBytesOrZero == 0) p.scratchBytes += round_up(n, kAlign);
   return p;
 }
 
@@ -319,6 +325,14 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                        opt.localGeometry != THRS_LOCAL_BIG32;
   const bool segTop = opt.segmented != THRS_SEG_NONE;
   const bool segA = opt.segmented == THRS_SEG_AUTO;
+  // local16 with both top-digit passes segmented: the passes carry the keys
+  // as planes (thrs_kernels.hpp kCodecSplit / kCodecPlanes): keyOut (4n bytes)
+  // = lo u16[n] | lo2 u16[n], the u8 plane hi[n] at the end of the scratch
+  const bool planes = local16 && segA && opt.planes != THRS_PLANES_OFF &&
+                      plan.scratchBytes - plan.hiPlaneOff >= (uint64_t)n;
+  uint16_t* loP = static_cast<uint16_t*>(keyOutBuf);
+  uint16_t* lo2P = loP + n;
+  uint8_t* hiP = reinterpret_cast<uint8_t*>(scratch + plan.hiPlaneOff);
   const bool atomicRank = opt.rank == THRS_RANK_ATOMIC ? true
                           : opt.rank == THRS_RANK_BALLOT ? false
                                                          : probe_rank_mode(stream) != 0;
@@ -336,12 +350,19 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   auto kernel = useXb ? (atomicRank ? thrs_pass_xb<KT, VB, ST, true> : thrs_pass_xb<KT, VB, ST, false>)
                       : (atomicRank ? thrs_pass<KT, VB, ST, true> : thrs_pass<KT, VB, ST, false>);
   auto sk = atomicRank ? thrs_pass_seg<KT, VB, ST, true> : thrs_pass_seg<KT, VB, ST, false>;
+  // plane codecs (u32 keys-only instantiations only; `planes` is false elsewhere)
+  auto skSplit = atomicRank ? thrs_pass_seg<KT, VB, ST, true, (KT == 0 && VB == 0) ? kCodecSplit : kCodecKeys>
+                            : thrs_pass_seg<KT, VB, ST, false, (KT == 0 && VB == 0) ? kCodecSplit : kCodecKeys>;
+  auto skPlanes = atomicRank ? thrs_pass_seg<KT, VB, ST, true, (KT == 0 && VB == 0) ? kCodecPlanes : kCodecKeys>
+                             : thrs_pass_seg<KT, VB, ST, false, (KT == 0 && VB == 0) ? kCodecPlanes : kCodecKeys>;
   const int histPasses = bucket ? nLow : nPass;
   const size_t histLds = (size_t)histPasses * kBins * hist_copies<(int)sizeof(U)>() * 4;
   if (allow_lds(thrs_hist<KT>, histLds) != hipSuccess || allow_lds(kernel, lds) != hipSuccess)
     return THRS_ERROR_HIP;
   if (bucket) {
     if (allow_lds(thrs_hist_joint<KT>, kJointLds) != hipSuccess || allow_lds(sk, lds) != hipSuccess)
+      return THRS_ERROR_HIP;
+    if (planes && (allow_lds(skSplit, lds) != hipSuccess || allow_lds(skPlanes, lds) != hipSuccess))
       return THRS_ERROR_HIP;
     if constexpr (kBucket64) {
       if (allow_lds(atomicRank ? thrs_local64<KT, VB, true> : thrs_local64<KT, VB, false>, Loc64::LDS) != hipSuccess)
@@ -427,7 +448,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     GroupTables<ST> g = grp[p & 1];
     g.gaNext = more ? grp[(p + 1) & 1].ga : nullptr;
     g.gpNext = more ? grp[(p + 1) & 1].gp : nullptr;
-    ProfScope prof(stream, gate && gateMask == kGateFallback ? 3 : 1);  // fallback-only passes are timed apart
+    ProfScope prof(stream, gate && (gateMask == kGateFallback || gateMask == kGateMode1) ? 3 : 1);  // fallback-only passes are timed apart
     hipLaunchKernelGGL(kernel, dim3(grid), dim3(G::THREADS), lds, stream, kin, kout, vin, vout, n, orderMask,
                        startBits + 8 * p, base + p * kBins, status[p & 1], next,
                        useXb ? reinterpret_cast<uint32_t*>(claim + p * plan.claimBytes) : counters + p, err, g,
@@ -494,12 +515,14 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     // top-digit pass either (both are identities, and skipping both keeps the
     // result in K).
     auto launch_seg = [&](int p, U* kin, U* kout, VW* vin, VW* vout, uint64_t infoOff, uint64_t baseOff,
-                          const uint32_t* gate, uint32_t gateMask) {
-      ProfScope prof(stream, 1);
-      hipLaunchKernelGGL(sk, dim3((uint32_t)segPerCU * cu_count()), dim3(G::THREADS), lds, stream, kin, kout, vin,
-                         vout, orderMask, startBits + 8 * p, reinterpret_cast<uint32_t*>(hyb + infoOff),
-                         reinterpret_cast<const uint32_t*>(hyb + baseOff), status[p & 1], err, grp[p & 1], gate,
-                         gateMask);
+                          const uint32_t* gate, uint32_t gateMask, int codec = kCodecKeys) {
+      ProfScope prof(stream, gateMask == kGateMode1 ? 3 : 1);  // fallback-only launches are timed apart
+      auto kern = codec == kCodecSplit ? skSplit : codec == kCodecPlanes ? skPlanes : sk;
+      // kCodecPlanes: image-space input (orderMask 0), digit at bits 16-23 of k'
+      hipLaunchKernelGGL(kern, dim3((uint32_t)segPerCU * cu_count()), dim3(G::THREADS), lds, stream, kin, kout, vin,
+                         vout, codec == kCodecPlanes ? (U)0 : orderMask, codec == kCodecPlanes ? 16 : startBits + 8 * p,
+                         reinterpret_cast<uint32_t*>(hyb + infoOff), reinterpret_cast<const uint32_t*>(hyb + baseOff),
+                         status[p & 1], err, grp[p & 1], gate, gateMask, hiP);
     };
     const uint64_t sw = plan.wideStatus ? 8 : 4;
     const int setB = (nLow + 1) & 1;
@@ -507,7 +530,11 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
       // The table set is clean either way: zeroed up front, or rows [0,
       // nTiles) cleared by the last fallback pass.  Neither clears rows for
       // the top-digit pass: zero that set.
-      launch_seg(nLow, K, keyOut, V, valOut, kSegInfoAOff, kSegBaseAOff, mode, kGateMode0);
+      if (planes)
+        launch_seg(nLow, K, reinterpret_cast<U*>(loP), V, valOut, kSegInfoAOff, kSegBaseAOff, mode, kGateMode0,
+                   kCodecSplit);
+      else
+        launch_seg(nLow, K, keyOut, V, valOut, kSegInfoAOff, kSegBaseAOff, mode, kGateMode0);
       launch_pass(nLow, K, keyOut, V, valOut, mode, kGateMode1);
       if (hipMemsetAsync(status[setB], 0, plan.setBytes, stream) != hipSuccess) return THRS_ERROR_HIP;
     } else {
@@ -522,7 +549,11 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                          stream) != hipSuccess)
         return THRS_ERROR_HIP;
     }
-    if (segTop)
+    if (planes) {  // mode 0: planes -> lo2; mode 1 (fallback): keys
+      launch_seg(nLow + 1, reinterpret_cast<U*>(loP), reinterpret_cast<U*>(lo2P), valOut, V, kSegInfoOff, kSegBaseOff,
+                 mode, kGateMode0, kCodecPlanes);
+      launch_seg(nLow + 1, keyOut, K, valOut, V, kSegInfoOff, kSegBaseOff, mode, kGateMode1);
+    } else if (segTop)
       launch_seg(nLow + 1, keyOut, K, valOut, V, kSegInfoOff, kSegBaseOff, mode, kGateMode0 | kGateMode1);
     else
       launch_pass(nLow + 1, keyOut, K, valOut, V, mode, kGateMode0 | kGateMode1);
@@ -556,7 +587,8 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
         if constexpr (KT == 0 && VB == 0) {
           auto lk = atomicRank ? thrs_local16<true, Loc16> : thrs_local16<false, Loc16>;
           hipLaunchKernelGGL(lk, dim3((uint32_t)maxChunks), dim3(Loc16::THREADS), Loc16::LDS, stream,
-                             reinterpret_cast<uint32_t*>(K), (uint32_t)orderMask, chunkOff, chunkB0, meta);
+                             reinterpret_cast<uint32_t*>(K), (uint32_t)orderMask, chunkOff, chunkB0, meta,
+                             planes ? static_cast<const uint16_t*>(lo2P) : nullptr);
         }
       } else if (smallLocal) {
         launch_local(LocSmall{});
@@ -593,7 +625,7 @@ bool valid_options(const thrs_options& o) {
   return o.path >= THRS_PATH_AUTO && o.path <= THRS_PATH_BUCKET && o.localGeometry >= THRS_LOCAL_AUTO &&
          o.localGeometry <= THRS_LOCAL_BIG32 && o.segmented >= THRS_SEG_AUTO && o.segmented <= THRS_SEG_NONE &&
          o.tileClaims >= THRS_CLAIMS_AUTO && o.tileClaims <= THRS_CLAIMS_TICKET && o.rank >= THRS_RANK_AUTO &&
-         o.rank <= THRS_RANK_BALLOT;
+         o.rank <= THRS_RANK_BALLOT && o.planes >= THRS_PLANES_AUTO && o.planes <= THRS_PLANES_OFF;
 }
 
 // Scratch is sized for the larger of the keys-only and pairs tile plans so

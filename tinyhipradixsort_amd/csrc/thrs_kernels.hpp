@@ -471,6 +471,9 @@ template <typename ST> struct GroupTables {
 #ifndef THRS_RELOAD_KEYS
 #define THRS_RELOAD_KEYS 0
 #endif
+#ifndef THRS_RANK_PIPE
+#define THRS_RANK_PIPE 2  // pass rank: LDS atomics in flight per wave
+#endif
 #ifndef THRS_WO_BATCH
 #define THRS_WO_BATCH 8
 #endif
@@ -708,12 +711,29 @@ struct GroupWalk {
 // which is the order the stable rank walks.  Keys past n read as 0.
 // keyStart / valid: the tile's first key and key count (tile * TILE and
 // min(TILE, n - tile * TILE) except in segmented passes).
-template <int KT, int VB>
+// Key codecs of the pass kernels.  The bucket path for u32 keys without
+// values (thrs_hybrid.hpp, thrs_local16) carries only what the next step
+// reads, in two planes instead of the 4-byte keys:
+//   kCodecKeys    keys in, keys out
+//   kCodecSplit   keys in; out: the image's low 16 bits to the u16 plane
+//                 (keysOut) and its top byte to the u8 plane (hiPlane) -- the
+//                 second digit (bits 16-23), which this pass sorts by, is
+//                 implied by the output position
+//   kCodecPlanes  in: the two planes, as k' = top byte << 16 | low 16 bits (the
+//                 pass's digit at shift 16, orderMask 0); out: the low 16 bits
+//                 to a u16 plane -- the local sort rebuilds the top 16 bits
+//                 from its chunk's bucket
+// 7 + 5 bytes per key instead of 8 + 8 for the two top-digit passes, 6
+// instead of 8 for the local sort.
+enum { kCodecKeys = 0, kCodecSplit = 1, kCodecPlanes = 2 };
+
+template <int KT, int VB, int CODEC = kCodecKeys>
 __device__ __forceinline__ void load_tile(const typename KeyTraits<KT>::U* __restrict__ keysIn,
                                           const typename ValueWord<VB>::T* __restrict__ valsIn, uint64_t keyStart,
                                           uint32_t valid,
                                           typename KeyTraits<KT>::U (&k)[PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::KPT],
-                                          typename ValueWord<VB>::T (&v)[VB ? PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::KPT : 1]) {
+                                          typename ValueWord<VB>::T (&v)[VB ? PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::KPT : 1],
+                                          const uint8_t* __restrict__ hiIn = nullptr) {
   using U = typename KeyTraits<KT>::U;
   using VW = typename ValueWord<VB>::T;
   using G = PassGeom<sizeof(U), VB>;
@@ -723,6 +743,19 @@ __device__ __forceinline__ void load_tile(const typename KeyTraits<KT>::U* __res
   const uint64_t chunkBase = keyStart + w * CHUNK;
   int32_t lim = (int32_t)valid - (int32_t)(w * CHUNK + lane);  // item j is real iff j*64 < lim
   pin(reinterpret_cast<uint32_t&>(lim));
+  if constexpr (CODEC == kCodecPlanes) {
+    static_assert(sizeof(U) == 4 && VB == 0, "planes: u32 keys without values");
+    const uint16_t* lo = reinterpret_cast<const uint16_t*>(keysIn);
+    auto ld = [&](uint64_t i) -> U { return (U)(((uint32_t)hiIn[i] << 16) | (uint32_t)lo[i]); };
+    if (valid == T) {
+#pragma unroll
+      for (int j = 0; j < KPT; ++j) k[j] = ld(chunkBase + j * 64 + lane);
+    } else {
+#pragma unroll
+      for (int j = 0; j < KPT; ++j) k[j] = (j * 64 < lim) ? ld(chunkBase + j * 64 + lane) : (U)0;
+    }
+    return;
+  }
   if (valid == T) {
 #pragma unroll
     for (int j = 0; j < KPT; ++j) k[j] = keysIn[chunkBase + j * 64 + lane];
@@ -745,7 +778,7 @@ struct NoMid {
   __device__ __forceinline__ void operator()() const {}
 };
 
-template <int KT, int VB, typename ST, bool ATOMIC_RANK, typename Mid>
+template <int KT, int VB, typename ST, bool ATOMIC_RANK, typename Mid, int CODEC = kCodecKeys>
 __device__ __forceinline__ void pass_tile(
     const typename KeyTraits<KT>::U* __restrict__ keysIn, typename KeyTraits<KT>::U* __restrict__ keysOut,
     const typename ValueWord<VB>::T* __restrict__ valsIn, typename ValueWord<VB>::T* __restrict__ valsOut,
@@ -753,10 +786,12 @@ __device__ __forceinline__ void pass_tile(
     ST* __restrict__ status, ST* __restrict__ statusNext, uint32_t* __restrict__ errFlag, uint32_t tile,
     uint32_t chainStart, const GroupTables<ST>& grp, unsigned char* smem, uint64_t* __restrict__ stamps,
     typename KeyTraits<KT>::U (&k)[PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::KPT],
-    typename ValueWord<VB>::T (&v)[VB ? PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::KPT : 1], Mid mid) {
+    typename ValueWord<VB>::T (&v)[VB ? PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::KPT : 1], Mid mid,
+    uint8_t* __restrict__ hiOut = nullptr) {
   using U = typename KeyTraits<KT>::U;
   using VW = typename ValueWord<VB>::T;
   using G = PassGeom<sizeof(U), VB>;
+  static_assert(CODEC == kCodecKeys || (sizeof(U) == 4 && VB == 0 && !THRS_RELOAD_KEYS), "codecs: u32 keys only");
   constexpr int WAVES = G::WAVES, KPT = G::KPT, ROUNDS = G::ROUNDS, THREADS = G::THREADS;
   constexpr uint32_t T = G::TILE, STAGE = G::STAGE, CHUNK = 64 * KPT;
   constexpr int STAGE_SHIFT = __builtin_ctz(STAGE);
@@ -912,14 +947,34 @@ __device__ __forceinline__ void pass_tile(
 #pragma unroll
   for (int j = 0; j < (KPT + 1) / 2; ++j) sl[j] = 0;
   const uint32_t ubase = (uint32_t)__builtin_amdgcn_readfirstlane((int)cnt[d0]);  // scalar
+  // lane-ordered rank atomics kept RP in flight: item j+RP's atomic is issued
+  // before item j's result is used (a wave's LDS operations execute in issue
+  // order, so the ranks are those of the one-at-a-time loop); one at a time,
+  // every item waited a full LDS round trip
+  constexpr int RP = THRS_RANK_PIPE;
+  auto rank_atomic = [&](int j) -> uint32_t {
+    return __hip_atomic_fetch_add(allU ? sink : &cnt[digit_of(k[j], j)], 1u, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+  };
+  uint32_t rq[RP];
+  if constexpr (ATOMIC_RANK) {
+#pragma unroll
+    for (int j = 0; j < RP && j < KPT; ++j) {
+      pin(k[j]);
+      rq[j] = rank_atomic(j);
+    }
+  }
 #pragma unroll
   for (int j = 0; j < KPT; ++j) {
-    pin(k[j]);  // keep item j's digit/address math inside iteration j (register pressure)
     uint32_t slot;
     if constexpr (ATOMIC_RANK) {
-      slot = __hip_atomic_fetch_add(allU ? sink : &cnt[digit_of(k[j], j)], 1u, __ATOMIC_RELAXED,
-                                    __HIP_MEMORY_SCOPE_WORKGROUP);
+      slot = rq[j % RP];
+      if (j + RP < KPT) {
+        pin(k[j + RP]);  // keep item j+RP's digit/address math here (register pressure)
+        rq[j % RP] = rank_atomic(j + RP);
+      }
     } else {
+      pin(k[j]);  // keep item j's digit/address math inside iteration j (register pressure)
       slot = wave_rank<false>(cnt, digit_of(k[j], j), lane, false);
     }
     slot = allU ? ubase + 64u * j + lane : slot;
@@ -1040,6 +1095,41 @@ __device__ __forceinline__ void pass_tile(
       }
       lds_barrier();
     }
+    // write one stage slot (i) to its global position
+    auto put = [&](U key, uint32_t i, uint32_t off) __attribute__((always_inline)) {
+      const uint32_t dst = off + (uint32_t)r * STAGE + i;
+      if constexpr (CODEC == kCodecSplit) {
+        const uint32_t img = (uint32_t)(KeyTraits<KT>::bits(key) ^ orderMask);
+        reinterpret_cast<uint16_t*>(keysOut)[dst] = (uint16_t)img;
+        hiOut[dst] = (uint8_t)(img >> 24);
+      } else if constexpr (CODEC == kCodecPlanes) {
+        reinterpret_cast<uint16_t*>(keysOut)[dst] = (uint16_t)key;
+      } else {
+        keysOut[dst] = key;
+      }
+      if constexpr (VB != 0) valsOut[dst] = stage_v[i];
+    };
+    if (full) {
+      // whole tile: no lane conditions, so each batch's stage reads,
+      // then its offset reads, are issued back to back (a read under a lane
+      // condition is waited for before the next one issues)
+      constexpr int NS = (int)(STAGE / THREADS), WB = THRS_WO_BATCH;
+#pragma unroll
+      for (int j0 = 0; j0 < NS; j0 += WB) {
+        U key[WB];
+        uint32_t off[WB];
+#pragma unroll
+        for (int b = 0; b < WB; ++b)
+          if (j0 + b < NS) key[b] = stage_k[(j0 + b) * THREADS + tid];
+#pragma unroll
+        for (int b = 0; b < WB; ++b)
+          if (j0 + b < NS) off[b] = s_gofs[(uint32_t)((KeyTraits<KT>::bits(key[b]) ^ orderMask) >> shift) & 0xFFu];
+#pragma unroll
+        for (int b = 0; b < WB; ++b)
+          if (j0 + b < NS) put(key[b], (j0 + b) * THREADS + tid, off[b]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else
 #pragma unroll
     for (int j = 0; j < (int)(STAGE / THREADS); ++j) {
       const uint32_t i = j * THREADS + tid;
@@ -1047,9 +1137,7 @@ __device__ __forceinline__ void pass_tile(
       if (full || slot < valid) {
         const U key = stage_k[i];
         const uint32_t dd = (uint32_t)((KeyTraits<KT>::bits(key) ^ orderMask) >> shift) & 0xFFu;
-        const uint32_t dst = s_gofs[dd] + slot;
-        keysOut[dst] = key;
-        if constexpr (VB != 0) valsOut[dst] = stage_v[i];
+        put(key, i, s_gofs[dd]);
       }
       // bound the batch the scheduler hoists (LDS reads + 64-bit addresses):
       // in the persistent kernel the next tile's keys are live here
@@ -1260,15 +1348,18 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
 // Deadlock-free: a walk waits only on earlier tiles of its segment, which
 // were claimed earlier (tickets are monotone) by running workgroups.
 // segInfo: segPos[9] (key positions), segTiles[9] (first tile id); tickets[8] at word 64
+// CODEC (kCodec*): keys, or the u32 bucket path's planes (hiPlane: the u8
+// plane written by kCodecSplit / read by kCodecPlanes; keysIn / keysOut are
+// then u16 planes).
 constexpr int kSegs = 8;
-template <int KT, int VB, typename ST, bool ATOMIC_RANK>
+template <int KT, int VB, typename ST, bool ATOMIC_RANK, int CODEC = kCodecKeys>
 __global__ __launch_bounds__((PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::THREADS))
 __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::WPE))) void thrs_pass_seg(
     const typename KeyTraits<KT>::U* __restrict__ keysIn, typename KeyTraits<KT>::U* __restrict__ keysOut,
     const typename ValueWord<VB>::T* __restrict__ valsIn, typename ValueWord<VB>::T* __restrict__ valsOut,
     typename KeyTraits<KT>::U orderMask, int shift, uint32_t* __restrict__ segInfo,
     const uint32_t* __restrict__ segBase, ST* __restrict__ status, uint32_t* __restrict__ errFlag,
-    GroupTables<ST> grp, const uint32_t* __restrict__ gate, uint32_t gateMask) {
+    GroupTables<ST> grp, const uint32_t* __restrict__ gate, uint32_t gateMask, uint8_t* __restrict__ hiPlane) {
   using U = typename KeyTraits<KT>::U;
   using VW = typename ValueWord<VB>::T;
   using G = PassGeom<sizeof(U), VB>;
@@ -1318,9 +1409,10 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
     g.gaNext = nullptr;
     g.gpNext = nullptr;
     const uint32_t myBase = segBase[seg * kBins + (tid & 255u)];
-    load_tile<KT, VB>(keysIn, valsIn, keyStart, valid, k, v);
-    pass_tile<KT, VB, ST, ATOMIC_RANK>(keysIn, keysOut, valsIn, valsOut, keyStart, valid, orderMask, shift, myBase,
-                                       status, nullptr, errFlag, chain + t, chain, g, smem, nullptr, k, v, NoMid{});
+    load_tile<KT, VB, CODEC>(keysIn, valsIn, keyStart, valid, k, v, hiPlane);
+    pass_tile<KT, VB, ST, ATOMIC_RANK, NoMid, CODEC>(keysIn, keysOut, valsIn, valsOut, keyStart, valid, orderMask,
+                                                     shift, myBase, status, nullptr, errFlag, chain + t, chain, g, smem,
+                                                     nullptr, k, v, NoMid{}, hiPlane);
     lds_barrier();  // stage, s_gofs and s_misc are reused by the next tile
   }
 }
