@@ -57,6 +57,9 @@ constexpr uint32_t kGateMode0 = 1u << 0, kGateMode1 = 1u << 1, kGateMode2 = 1u <
 #ifndef THRS_HJ_UN
 #define THRS_HJ_UN 4  // 16-byte loads in flight per lane
 #endif
+#ifndef THRS_HJ_BATCHCARRY
+#define THRS_HJ_BATCHCARRY 0  // 1: one guard-bit test per 16 adds (measured slower, EXPERIMENTS row 50)
+#endif
 #ifndef THRS_HJ_PF
 #define THRS_HJ_PF 1  // bucket histogram: next iteration's loads in flight during the adds
 #endif
@@ -196,8 +199,20 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
         } else if (mode == kMixed) {
 #pragma unroll
           for (int e = 0; e < E; ++e) o[e] = add(b[e], 1u);
+#if THRS_HJ_BATCHCARRY
+          // a carry (field crossing 0x8000) flips its guard bit: one test for
+          // all E adds, the exact per-add check only when some lane carried
+          uint32_t flips = 0;
+#pragma unroll
+          for (int e = 0; e < E; ++e) flips |= (o[e] ^ (o[e] + (1u << ((b[e] & 1u) << 4)))) & 0x80008000u;
+          if (__ballot(flips != 0)) {
+#pragma unroll
+            for (int e = 0; e < E; ++e) check(b[e], o[e], 1u);
+          }
+#else
 #pragma unroll
           for (int e = 0; e < E; ++e) check(b[e], o[e], 1u);
+#endif
         } else {
 #pragma unroll
           for (int e = 0; e < E; ++e) {
@@ -645,9 +660,19 @@ __device__ __forceinline__ int loc_rounds(typename KeyTraits<KT>::U (&k)[LG::KPT
     // (no wave aggregation here: these kernels sit at their VGPR limit, and
     // the inputs that make a local round's digits wave-uniform -- constant
     // low bytes -- are rare; sorted input is not among them)
+    // whole waves (nItems == KPT) run without per-item tests: a scalar branch
+    // around an LDS atomic or read makes the compiler wait for every earlier
+    // one (thrs_local16)
+    const bool wfull = nItems == KPT;
+    if (wfull) {
 #pragma unroll
-    for (int j = 0; j < KPT; ++j)
-      if (j < nItems) __hip_atomic_fetch_add(&cnt[digit_of(k[j])], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      for (int j = 0; j < KPT; ++j)
+        __hip_atomic_fetch_add(&cnt[digit_of(k[j])], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else {
+#pragma unroll
+      for (int j = 0; j < KPT; ++j)
+        if (j < nItems) __hip_atomic_fetch_add(&cnt[digit_of(k[j])], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
     lds_barrier();
     {  // threads d < 256: digit d's total over the waves -> block exclusive scan
        // (wave totals through stage words: the stage is free between the
@@ -684,25 +709,35 @@ __device__ __forceinline__ int loc_rounds(typename KeyTraits<KT>::U (&k)[LG::KPT
 #define THRS_LOC_RB 12
 #endif
     constexpr int RB = THRS_LOC_RB;
+    auto rank_scatter = [&](auto fullc) __attribute__((always_inline)) {
+      constexpr bool FULL = decltype(fullc)::value;
 #pragma unroll
-    for (int j0 = 0; j0 < KPT; j0 += RB) {
-      uint32_t sl[RB];
+      for (int j0 = 0; j0 < KPT; j0 += RB) {
+        uint32_t sl[RB];
 #pragma unroll
-      for (int jj = 0; jj < RB; ++jj) {
-        const int j = j0 + jj;
-        if (j < KPT && j < nItems) sl[jj] = wave_rank<ATOMIC_RANK>(cnt, digit_of(k[j]), lane, false);
+        for (int jj = 0; jj < RB; ++jj) {
+          const int j = j0 + jj;
+          if (j < KPT && (FULL || j < nItems)) sl[jj] = wave_rank<ATOMIC_RANK>(cnt, digit_of(k[j]), lane, false);
+        }
+#pragma unroll
+        for (int jj = 0; jj < RB; ++jj)
+          if (j0 + jj < KPT && (FULL || j0 + jj < nItems)) stage[sl[jj]] = k[j0 + jj];
+        __builtin_amdgcn_sched_barrier(0);
       }
-#pragma unroll
-      for (int jj = 0; jj < RB; ++jj)
-        if (j0 + jj < KPT && j0 + jj < nItems) stage[sl[jj]] = k[j0 + jj];
-      __builtin_amdgcn_sched_barrier(0);
-    }
+    };
+    if (wfull) rank_scatter(std::true_type{});
+    else rank_scatter(std::false_type{});
     lds_barrier();
     loc_stamp(st, 2 + (r & 1));
     if (r + 1 < roundsRun) {
+      if (limw >= (int32_t)CHUNK) {
 #pragma unroll
-      for (int j = 0; j < KPT; ++j)
-        if (j * 64 < limw) k[j] = stw[j * 64];
+        for (int j = 0; j < KPT; ++j) k[j] = stw[j * 64];
+      } else {
+#pragma unroll
+        for (int j = 0; j < KPT; ++j)
+          if (j * 64 < limw) k[j] = stw[j * 64];
+      }
     }
   }
   return roundsRun;
@@ -869,9 +904,20 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(6))
     auto digit_of = [&](int j) -> uint32_t { return (it[j >> 1] >> ((j & 1) * 16 + shift)) & 0xFFu; };
 #pragma unroll
     for (int i = 0; i < kBins / 64; ++i) cnt[i * 64 + lane] = 0;
+    // A wave whose KPT items all lie in the chunk (every wave but the chunk's
+    // last) runs the loops below without per-item tests: a scalar branch
+    // around an LDS atomic makes the compiler wait for every earlier one, so
+    // the batched rank atomics would be issued one round trip apart.
+    const bool wfull = nItems == KPT;
+    if (wfull) {
 #pragma unroll
-    for (int j = 0; j < KPT; ++j)
-      if (j < nItems) __hip_atomic_fetch_add(&cnt[digit_of(j)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      for (int j = 0; j < KPT; ++j)
+        __hip_atomic_fetch_add(&cnt[digit_of(j)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else {
+#pragma unroll
+      for (int j = 0; j < KPT; ++j)
+        if (j < nItems) __hip_atomic_fetch_add(&cnt[digit_of(j)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
     lds_barrier();
     {  // digit totals over the waves -> block exclusive scan -> per-wave running offsets
       uint32_t* s_wt = reinterpret_cast<uint32_t*>(smem);  // stage words: free until the scatter
@@ -898,26 +944,40 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(6))
     }
     lds_barrier();
     constexpr int RB = THRS_LOC_RB;
+    auto rank_scatter = [&](auto fullc) __attribute__((always_inline)) {
+      constexpr bool FULL = decltype(fullc)::value;
 #pragma unroll
-    for (int j0 = 0; j0 < KPT; j0 += RB) {
-      uint32_t sl[RB];
+      for (int j0 = 0; j0 < KPT; j0 += RB) {
+        uint32_t sl[RB];
 #pragma unroll
-      for (int jj = 0; jj < RB; ++jj) {
-        const int j = j0 + jj;
-        if (j < KPT && j < nItems) sl[jj] = wave_rank<ATOMIC_RANK>(cnt, digit_of(j), lane, false);
+        for (int jj = 0; jj < RB; ++jj) {
+          const int j = j0 + jj;
+          if (j < KPT && (FULL || j < nItems)) sl[jj] = wave_rank<ATOMIC_RANK>(cnt, digit_of(j), lane, false);
+        }
+#pragma unroll
+        for (int jj = 0; jj < RB; ++jj)
+          if (j0 + jj < KPT && (FULL || j0 + jj < nItems)) stage[LG::at(sl[jj])] = (uint16_t)item(j0 + jj);
+        __builtin_amdgcn_sched_barrier(0);
       }
-#pragma unroll
-      for (int jj = 0; jj < RB; ++jj)
-        if (j0 + jj < KPT && j0 + jj < nItems) stage[LG::at(sl[jj])] = (uint16_t)item(j0 + jj);
-      __builtin_amdgcn_sched_barrier(0);
-    }
+    };
+    if (wfull) rank_scatter(std::true_type{});
+    else rank_scatter(std::false_type{});
     lds_barrier();
     if (r == 0) {
+      if (limw >= (int32_t)CHUNK) {  // the wave's whole run is in the chunk: plain reads
 #pragma unroll
-      for (int j = 0; j < KPT; j += 2) {
-        const uint32_t a = (j * 64 < limw) ? (uint32_t)stw[j * LG::ROW] : 0xFFFFu;
-        const uint32_t b = (j + 1 < KPT && (j + 1) * 64 < limw) ? (uint32_t)stw[(j + 1) * LG::ROW] : 0xFFFFu;
-        it[j >> 1] = a | (b << 16);
+        for (int j = 0; j < KPT; j += 2) {
+          const uint32_t a = stw[j * LG::ROW];
+          const uint32_t b = (j + 1 < KPT) ? (uint32_t)stw[(j + 1) * LG::ROW] : 0xFFFFu;
+          it[j >> 1] = a | (b << 16);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < KPT; j += 2) {
+          const uint32_t a = (j * 64 < limw) ? (uint32_t)stw[j * LG::ROW] : 0xFFFFu;
+          const uint32_t b = (j + 1 < KPT && (j + 1) * 64 < limw) ? (uint32_t)stw[(j + 1) * LG::ROW] : 0xFFFFu;
+          it[j >> 1] = a | (b << 16);
+        }
       }
     }
   }
@@ -1093,9 +1153,16 @@ __global__ __launch_bounds__(Loc64::THREADS) void thrs_local64(uint64_t* __restr
     auto digit_of = [&](int j) -> uint32_t { return (uint32_t)(it[j] >> shift) & 0xFFu; };
 #pragma unroll
     for (int i = 0; i < kBins / 64; ++i) cnt[i * 64 + lane] = 0;
+    const bool wfull = nItems == KPT;  // whole wave: no per-item tests (see loc_rounds)
+    if (wfull) {
 #pragma unroll
-    for (int j = 0; j < KPT; ++j)
-      if (j < nItems) __hip_atomic_fetch_add(&cnt[digit_of(j)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      for (int j = 0; j < KPT; ++j)
+        __hip_atomic_fetch_add(&cnt[digit_of(j)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else {
+#pragma unroll
+      for (int j = 0; j < KPT; ++j)
+        if (j < nItems) __hip_atomic_fetch_add(&cnt[digit_of(j)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
     lds_barrier();
     {  // digit totals over the waves -> block exclusive scan -> per-wave running offsets
       uint32_t* s_wt = reinterpret_cast<uint32_t*>(smem);  // stage words: free until the scatter
@@ -1122,24 +1189,34 @@ __global__ __launch_bounds__(Loc64::THREADS) void thrs_local64(uint64_t* __restr
     }
     lds_barrier();
     constexpr int RB = 9;
+    auto rank_scatter = [&](auto fullc) __attribute__((always_inline)) {
+      constexpr bool FULL = decltype(fullc)::value;
 #pragma unroll
-    for (int j0 = 0; j0 < KPT; j0 += RB) {
-      uint32_t sl[RB];
+      for (int j0 = 0; j0 < KPT; j0 += RB) {
+        uint32_t sl[RB];
 #pragma unroll
-      for (int jj = 0; jj < RB; ++jj) {
-        const int j = j0 + jj;
-        if (j < KPT && j < nItems) sl[jj] = wave_rank<ATOMIC_RANK>(cnt, digit_of(j), lane, false);
+        for (int jj = 0; jj < RB; ++jj) {
+          const int j = j0 + jj;
+          if (j < KPT && (FULL || j < nItems)) sl[jj] = wave_rank<ATOMIC_RANK>(cnt, digit_of(j), lane, false);
+        }
+#pragma unroll
+        for (int jj = 0; jj < RB; ++jj)
+          if (j0 + jj < KPT && (FULL || j0 + jj < nItems)) stage[sl[jj]] = it[j0 + jj];
+        __builtin_amdgcn_sched_barrier(0);
       }
-#pragma unroll
-      for (int jj = 0; jj < RB; ++jj)
-        if (j0 + jj < KPT && j0 + jj < nItems) stage[sl[jj]] = it[j0 + jj];
-      __builtin_amdgcn_sched_barrier(0);
-    }
+    };
+    if (wfull) rank_scatter(std::true_type{});
+    else rank_scatter(std::false_type{});
     lds_barrier();
     if (r < 5) {
+      if (wfull) {
 #pragma unroll
-      for (int j = 0; j < KPT; ++j)
-        if (j < nItems) it[j] = stw[j * 64];
+        for (int j = 0; j < KPT; ++j) it[j] = stw[j * 64];
+      } else {
+#pragma unroll
+        for (int j = 0; j < KPT; ++j)
+          if (j < nItems) it[j] = stw[j * 64];
+      }
     }
   }
   // sorted items: this lane's output slots myOff + 64j; every stage read

@@ -25,6 +25,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace thrs_dev {
 
 constexpr int kRadixBits = 8;
@@ -129,6 +131,9 @@ __device__ __forceinline__ void match_digit(uint32_t d, uint32_t& mlo, uint32_t&
 //   kMixed       random input: one atomic per lane and item, no extra test.
 // Every lane of the wave is active in all of these.
 enum : uint32_t { kMixed = 0, kSomeUniform = 1, kAllUniform = 2 };
+#ifndef THRS_WAVE_MODE_EARLY
+#define THRS_WAVE_MODE_EARLY 0  // 1: test the first / last item before the others
+#endif
 
 __device__ __forceinline__ bool wave_uniform(uint32_t d) {
   const uint32_t d0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)d);
@@ -138,6 +143,20 @@ __device__ __forceinline__ bool wave_uniform(uint32_t d) {
 template <int N, typename F>
 __device__ __forceinline__ uint32_t wave_mode(F digit, int nItems, uint32_t& d0) {
   d0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)digit(0));
+#if THRS_WAVE_MODE_EARLY
+  // first and last item decide first: neither uniform (random input) is
+  // kMixed without looking at the others
+  bool some = wave_uniform(digit(0));
+#pragma unroll
+  for (int j = 1; j < N; ++j)
+    if (j == nItems - 1) some = some || wave_uniform(digit(j));
+  if (!some) return kMixed;
+  uint32_t diff = 0;
+#pragma unroll
+  for (int j = 0; j < N; ++j)
+    if (j < nItems) diff |= digit(j) ^ d0;
+  return __ballot(diff != 0) == 0 ? kAllUniform : kSomeUniform;
+#else
   uint32_t diff = 0;
 #pragma unroll
   for (int j = 0; j < N; ++j)
@@ -148,6 +167,7 @@ __device__ __forceinline__ uint32_t wave_mode(F digit, int nItems, uint32_t& d0)
   for (int j = 1; j < N; ++j)
     if (j == nItems - 1) some = some || wave_uniform(digit(j));
   return some ? kSomeUniform : kMixed;
+#endif
 }
 
 // true iff digit(j) is the same for every j < N in every lane; d0 = that digit
@@ -474,6 +494,9 @@ template <typename ST> struct GroupTables {
 #ifndef THRS_RANK_PIPE
 #define THRS_RANK_PIPE 2  // pass rank: LDS atomics in flight per wave
 #endif
+#ifndef THRS_WO_FULL_PAIRS
+#define THRS_WO_FULL_PAIRS 0  // 1: whole-tile batched write-out for pairs too (slower: EXPERIMENTS row 51)
+#endif
 #ifndef THRS_WO_BATCH
 #define THRS_WO_BATCH 8
 #endif
@@ -542,8 +565,8 @@ template <int KB, int VB> struct PassGeom {
   static constexpr int THREADS = 64 * WAVES;
   static constexpr uint32_t TILE = (uint32_t)THREADS * KPT;
   static constexpr uint32_t STAGE = TILE / ROUNDS;
-  // stage | s_cnt[WAVES][256] | s_gofs[256] | s_misc[16] | stamps | s_sink[WAVES][64]
-  static constexpr uint32_t LDS_BYTES = STAGE * (KB + VB) + (WAVES + 1) * kBins * 4 + 16 * 4 + kStampLds + WAVES * 64 * 4;
+  // stage | s_cnt[WAVES][256] | s_gofs[256] | s_misc[16] | stamps
+  static constexpr uint32_t LDS_BYTES = STAGE * (KB + VB) + (WAVES + 1) * kBins * 4 + 16 * 4 + kStampLds;
   static_assert(TILE <= 65536, "slots are kept as 16-bit halves");
   static_assert(kGroup == 0 || (uint64_t)kGroup * TILE < kArrival, "group counts must fit below the arrival bits");
   static_assert((STAGE & (STAGE - 1)) == 0 && STAGE % THREADS == 0, "stage must be a power of two");
@@ -842,30 +865,28 @@ __device__ __forceinline__ void pass_tile(
 
   // ---- B: per-wave histogram (order-free LDS atomics) -> tile counts.
   // A wave whose every item has one digit (sorted / constant input: one LDS
-  // atomic per key would be a 64-way same-address conflict) points its
-  // per-key atomics at a private sink word per lane instead (conflict-free)
-  // and adds 64*KPT to the digit once; slots are then base + 64j + lane.
-  // Branch-free selects: this kernel is at the VGPR limit.
+  // atomic per key would be a 64-way same-address conflict) adds 64*KPT to
+  // the digit once instead; its slots are then base + 64j + lane.
   uint32_t* cnt = s_cnt + w * kBins;
-  uint32_t* sink = s_misc + 16 + kStampLds / 4 + w * 64 + lane;
   // hint: items 0 and KPT-1 carry one digit d0 in every lane (sorted input);
   // the count loop verifies the others, and a wrong hint recounts (rare).
   const uint32_t d0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)digit_of(k[0], 0));
   const bool hint = full && __ballot(digit_of(k[0], 0) != d0 || digit_of(k[KPT - 1], KPT - 1) != d0) == 0;
-  uint32_t diff = 0;
+  // (wave-uniform branches: random input runs only the plain loops)
+  bool allU = false;
+  if (hint) {
+    uint32_t diff = 0;
 #pragma unroll
-  for (int j = 0; j < KPT; ++j) {
-    const uint32_t dj = digit_of(k[j], j);
-    diff |= dj ^ d0;
-    __hip_atomic_fetch_add(hint ? sink : &cnt[dj], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    for (int j = 0; j < KPT; ++j) diff |= digit_of(k[j], j) ^ d0;
+    allU = __ballot(diff != 0) == 0;
   }
-  const bool allU = hint && __ballot(diff != 0) == 0;
-  if (hint && !allU) {  // some item differs: count for real
+  if (allU) {
+    if (lane == 0) __hip_atomic_fetch_add(&cnt[d0], 64u * KPT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  } else {
 #pragma unroll
     for (int j = 0; j < KPT; ++j)
       __hip_atomic_fetch_add(&cnt[digit_of(k[j], j)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
-  if (allU && lane == 0) __hip_atomic_fetch_add(&cnt[d0], 64u * KPT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   lds_barrier();
   THRS_STAMP(2);
 
@@ -942,7 +963,7 @@ __device__ __forceinline__ void pass_tile(
   // lanes of the item (wave_rank: one ds_add_rtn_u32 per key, or one per
   // wave when its digit is uniform; the ballot match without ATOMIC_RANK).
   // all-uniform wave: item j of lane l takes slot base + 64j + l, base = the
-  // wave's running offset of d0 (a broadcast read); its atomics hit the sink
+  // wave's running offset of d0 (a broadcast read), no atomics
   uint32_t sl[(KPT + 1) / 2];  // final slots, two 16-bit halves per register
 #pragma unroll
   for (int j = 0; j < (KPT + 1) / 2; ++j) sl[j] = 0;
@@ -953,31 +974,9 @@ __device__ __forceinline__ void pass_tile(
   // every item waited a full LDS round trip
   constexpr int RP = THRS_RANK_PIPE;
   auto rank_atomic = [&](int j) -> uint32_t {
-    return __hip_atomic_fetch_add(allU ? sink : &cnt[digit_of(k[j], j)], 1u, __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+    return __hip_atomic_fetch_add(&cnt[digit_of(k[j], j)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   };
-  uint32_t rq[RP];
-  if constexpr (ATOMIC_RANK) {
-#pragma unroll
-    for (int j = 0; j < RP && j < KPT; ++j) {
-      pin(k[j]);
-      rq[j] = rank_atomic(j);
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < KPT; ++j) {
-    uint32_t slot;
-    if constexpr (ATOMIC_RANK) {
-      slot = rq[j % RP];
-      if (j + RP < KPT) {
-        pin(k[j + RP]);  // keep item j+RP's digit/address math here (register pressure)
-        rq[j % RP] = rank_atomic(j + RP);
-      }
-    } else {
-      pin(k[j]);  // keep item j's digit/address math inside iteration j (register pressure)
-      slot = wave_rank<false>(cnt, digit_of(k[j], j), lane, false);
-    }
-    slot = allU ? ubase + 64u * j + lane : slot;
+  auto place = [&](int j, uint32_t slot) __attribute__((always_inline)) {
     if constexpr (ROUNDS == 1) {
       // one LDS round: place the key in sorted order now (frees its register
       // before the walk; the post-walk barrier orders it for phase E)
@@ -987,7 +986,38 @@ __device__ __forceinline__ void pass_tile(
       sl[j / 2] |= slot << (16 * (j & 1));
       pin(sl[j / 2]);  // materialise the slot now (else it is sunk to phase E, keeping masks alive)
     }
-    __builtin_amdgcn_sched_barrier(0);
+  };
+  if (allU) {
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) {
+      place(j, ubase + 64u * j + lane);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  } else {
+    uint32_t rq[RP];
+    if constexpr (ATOMIC_RANK) {
+#pragma unroll
+      for (int j = 0; j < RP && j < KPT; ++j) {
+        pin(k[j]);
+        rq[j] = rank_atomic(j);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) {
+      uint32_t slot;
+      if constexpr (ATOMIC_RANK) {
+        slot = rq[j % RP];
+        if (j + RP < KPT) {
+          pin(k[j + RP]);  // keep item j+RP's digit/address math here (register pressure)
+          rq[j % RP] = rank_atomic(j + RP);
+        }
+      } else {
+        pin(k[j]);  // keep item j's digit/address math inside iteration j (register pressure)
+        slot = wave_rank<false>(cnt, digit_of(k[j], j), lane, false);
+      }
+      place(j, slot);
+      __builtin_amdgcn_sched_barrier(0);
+    }
   }
   auto slot_of = [&](int j) -> uint32_t { return (sl[j / 2] >> (16 * (j & 1))) & 0xFFFFu; };
   THRS_STAMP(4);
@@ -1095,8 +1125,8 @@ __device__ __forceinline__ void pass_tile(
       }
       lds_barrier();
     }
-    // write one stage slot (i) to its global position
-    auto put = [&](U key, uint32_t i, uint32_t off) __attribute__((always_inline)) {
+    // write one stage slot (i) to its global position (vv: its value, read by the caller)
+    auto put = [&](U key, uint32_t i, uint32_t off, const VW& vv) __attribute__((always_inline)) {
       const uint32_t dst = off + (uint32_t)r * STAGE + i;
       if constexpr (CODEC == kCodecSplit) {
         const uint32_t img = (uint32_t)(KeyTraits<KT>::bits(key) ^ orderMask);
@@ -1107,9 +1137,9 @@ __device__ __forceinline__ void pass_tile(
       } else {
         keysOut[dst] = key;
       }
-      if constexpr (VB != 0) valsOut[dst] = stage_v[i];
+      if constexpr (VB != 0) valsOut[dst] = vv;
     };
-    if (full) {
+    if ((VB == 0 || THRS_WO_FULL_PAIRS) && full) {
       // whole tile: no lane conditions, so each batch's stage reads,
       // then its offset reads, are issued back to back (a read under a lane
       // condition is waited for before the next one issues)
@@ -1118,15 +1148,19 @@ __device__ __forceinline__ void pass_tile(
       for (int j0 = 0; j0 < NS; j0 += WB) {
         U key[WB];
         uint32_t off[WB];
+        VW val[VB ? WB : 1];
 #pragma unroll
         for (int b = 0; b < WB; ++b)
-          if (j0 + b < NS) key[b] = stage_k[(j0 + b) * THREADS + tid];
+          if (j0 + b < NS) {
+            key[b] = stage_k[(j0 + b) * THREADS + tid];
+            if constexpr (VB != 0) val[b] = stage_v[(j0 + b) * THREADS + tid];
+          }
 #pragma unroll
         for (int b = 0; b < WB; ++b)
           if (j0 + b < NS) off[b] = s_gofs[(uint32_t)((KeyTraits<KT>::bits(key[b]) ^ orderMask) >> shift) & 0xFFu];
 #pragma unroll
         for (int b = 0; b < WB; ++b)
-          if (j0 + b < NS) put(key[b], (j0 + b) * THREADS + tid, off[b]);
+          if (j0 + b < NS) put(key[b], (j0 + b) * THREADS + tid, off[b], val[VB ? b : 0]);
         __builtin_amdgcn_sched_barrier(0);
       }
     } else
@@ -1137,7 +1171,9 @@ __device__ __forceinline__ void pass_tile(
       if (full || slot < valid) {
         const U key = stage_k[i];
         const uint32_t dd = (uint32_t)((KeyTraits<KT>::bits(key) ^ orderMask) >> shift) & 0xFFu;
-        put(key, i, s_gofs[dd]);
+        VW vv{};
+        if constexpr (VB != 0) vv = stage_v[i];
+        put(key, i, s_gofs[dd], vv);
       }
       // bound the batch the scheduler hoists (LDS reads + 64-bit addresses):
       // in the persistent kernel the next tile's keys are live here
