@@ -403,9 +403,15 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   // header (histograms, tile counters, error word) + first status table; the
   // bucket path with an odd number of (skippable) low passes starts on set 1
   // too, and zeroes its bucket histogram
-  const uint64_t sets = (bucket && (nLow & 1)) ? 2 : 1;
-  if (hipMemsetAsync(scratch, 0, kHeaderBytes + sets * plan.setBytes, stream) != hipSuccess) return THRS_ERROR_HIP;
-  if (bucket && hipMemsetAsync(joint, 0, kJointZero, stream) != hipSuccess) return THRS_ERROR_HIP;
+  // Bucket path: ONE memset from the header through the bucket histogram --
+  // both table sets (the top-digit passes use set nLow&1 and the other one,
+  // and no launch before them dirties the other unless it also cleans it:
+  // fallback passes clear their successor's rows), all 8 claim areas, joint.
+  if (bucket) {
+    if (hipMemsetAsync(scratch, 0, plan.hybridOff + kJointZero, stream) != hipSuccess) return THRS_ERROR_HIP;
+  } else if (hipMemsetAsync(scratch, 0, kHeaderBytes + plan.setBytes, stream) != hipSuccess) {
+    return THRS_ERROR_HIP;
+  }
   char* claim = scratch + kHeaderBytes + 2 * plan.setBytes;  // 8 per-pass claim areas
 
   {  // histograms of every pass in one read of the keys
@@ -437,7 +443,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
       return THRS_ERROR_HIP;
   }
 
-  if (useXb && hipMemsetAsync(claim, 0, (size_t)nPass * plan.claimBytes, stream) != hipSuccess)
+  if (useXb && !bucket && hipMemsetAsync(claim, 0, (size_t)nPass * plan.claimBytes, stream) != hipSuccess)
     return THRS_ERROR_HIP;
 
   // pass p: digit at startBits + 8p, tables of set p&1; gate != nullptr runs
@@ -527,16 +533,15 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     const uint64_t sw = plan.wideStatus ? 8 : 4;
     const int setB = (nLow + 1) & 1;
     if (segA) {
-      // The table set is clean either way: zeroed up front, or rows [0,
-      // nTiles) cleared by the last fallback pass.  Neither clears rows for
-      // the top-digit pass: zero that set.
+      // Both table sets are clean: zeroed up front, and on the fallback each
+      // low pass clears its successor's rows; the segmented passes' extra
+      // tile ids (rows past nTiles) are touched by nothing else.
       if (planes)
         launch_seg(nLow, K, reinterpret_cast<U*>(loP), V, valOut, kSegInfoAOff, kSegBaseAOff, mode, kGateMode0,
                    kCodecSplit);
       else
         launch_seg(nLow, K, keyOut, V, valOut, kSegInfoAOff, kSegBaseAOff, mode, kGateMode0);
       launch_pass(nLow, K, keyOut, V, valOut, mode, kGateMode1);
-      if (hipMemsetAsync(status[setB], 0, plan.setBytes, stream) != hipSuccess) return THRS_ERROR_HIP;
     } else {
       launch_pass(nLow, K, keyOut, V, valOut, mode, kGateMode0 | kGateMode1);
       // the segmented pass's tile ids reach past nTiles (per-segment
@@ -561,7 +566,10 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
       ProfScope prof(stream, 2);
       // never more workgroups than chunks can exist: <= 256 (one per top digit)
       // + 2 per non-empty bucket, and <= the number of buckets
-      const uint64_t maxChunks = std::min<uint64_t>(kBuckets, 256 + 2 * (uint64_t)n);
+      // (single-bucket chunks -- pairs, local16, 8-byte keys: thrs_plan makes
+      // every bucket a chunk, empty or not)
+      const bool singleChunks = VB || local16 || kBucket64;
+      const uint64_t maxChunks = singleChunks ? kBuckets : std::min<uint64_t>(kBuckets, 256 + 2 * (uint64_t)n);
       auto launch_local = [&](auto geom) {
         using LG = decltype(geom);
         const size_t llds = LG::template lds<U>();

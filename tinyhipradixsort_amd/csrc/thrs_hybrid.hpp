@@ -294,6 +294,8 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
 // than T keys.  All buckets of a multi-bucket chunk start inside one T-window
 // and hold <= T keys, so a chunk holds < 2T <= cap keys unless it is a single
 // bucket; a single bucket above cap sets the fallback flag.  T = 2^logT.
+// logT < 0 (single mode: u32 keys-only at n > 2^29, pairs, 8-byte keys):
+// chunk c is bucket c, empty or not, so no sweep counts the chunks.
 constexpr int kPlanThreads = 1024;
 __device__ __forceinline__ uint32_t block_excl_scan1024(uint32_t v, uint32_t* s_w, uint32_t* total) {
   const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -342,7 +344,7 @@ __global__ __launch_bounds__(kPlanThreads) void thrs_plan(const uint32_t* __rest
   const int lt = single ? 0 : logT;
   const uint32_t T = 1u << lt;
   auto opens = [&](uint32_t b, uint32_t off, uint32_t sz, uint32_t prevSz) -> bool {
-    if (single) return (b & 255u) == 0 || sz != 0 || prevSz != 0;
+    if (single) return true;  // chunk c = bucket c (empty chunks exit at once)
     return (b & 255u) == 0 || (off >> lt) != ((off - prevSz) >> lt) || sz > T || prevSz > T;
   };
 
@@ -482,13 +484,17 @@ __global__ __launch_bounds__(kPlanThreads) void thrs_plan(const uint32_t* __rest
     }
     return nOpen;
   };
-  const uint32_t myOpen = sweep(false, 0);
-  if (lane == 0) s_wopen[w] = myOpen;
-  __syncthreads();
-  uint32_t cbase = 0, nChunks = 0;
-  for (int ww = 0; ww < WAVES; ++ww) {
-    cbase += ((uint32_t)ww < w) ? s_wopen[ww] : 0u;
-    nChunks += s_wopen[ww];
+  uint32_t cbase = w * (64 * STEPS), nChunks = kBuckets;  // single: every bucket is a chunk
+  if (!single) {
+    const uint32_t myOpen = sweep(false, 0);
+    if (lane == 0) s_wopen[w] = myOpen;
+    __syncthreads();
+    cbase = 0;
+    nChunks = 0;
+    for (int ww = 0; ww < WAVES; ++ww) {
+      cbase += ((uint32_t)ww < w) ? s_wopen[ww] : 0u;
+      nChunks += s_wopen[ww];
+    }
   }
   sweep(true, cbase);
   if (tid == kPlanThreads - 1) {
