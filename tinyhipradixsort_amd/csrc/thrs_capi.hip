@@ -347,8 +347,8 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
 
   // ---- kernels and their LDS opt-ins, before anything is enqueued
   const size_t lds = G::LDS_BYTES;
-  auto kernel = useXb ? (atomicRank ? thrs_pass_xb<KT, VB, ST, true> : thrs_pass_xb<KT, VB, ST, false>)
-                      : (atomicRank ? thrs_pass<KT, VB, ST, true> : thrs_pass<KT, VB, ST, false>);
+  auto kernelXb = atomicRank ? thrs_pass_xb<KT, VB, ST, true> : thrs_pass_xb<KT, VB, ST, false>;
+  auto kernel = useXb ? kernelXb : (atomicRank ? thrs_pass<KT, VB, ST, true> : thrs_pass<KT, VB, ST, false>);
   auto sk = atomicRank ? thrs_pass_seg<KT, VB, ST, true> : thrs_pass_seg<KT, VB, ST, false>;
   // plane codecs (u32 keys-only instantiations only; `planes` is false elsewhere)
   auto skSplit = atomicRank ? thrs_pass_seg<KT, VB, ST, true, (KT == 0 && VB == 0) ? kCodecSplit : kCodecKeys>
@@ -357,7 +357,8 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                              : thrs_pass_seg<KT, VB, ST, false, (KT == 0 && VB == 0) ? kCodecPlanes : kCodecKeys>;
   const int histPasses = bucket ? nLow : nPass;
   const size_t histLds = (size_t)histPasses * kBins * hist_copies<(int)sizeof(U)>() * 4;
-  if (allow_lds(thrs_hist<KT>, histLds) != hipSuccess || allow_lds(kernel, lds) != hipSuccess)
+  if (allow_lds(thrs_hist<KT>, histLds) != hipSuccess || allow_lds(kernel, lds) != hipSuccess ||
+      allow_lds(kernelXb, lds) != hipSuccess)
     return THRS_ERROR_HIP;
   if (bucket) {
     if (allow_lds(thrs_hist_joint<KT>, kJointLds) != hipSuccess || allow_lds(sk, lds) != hipSuccess)
@@ -388,13 +389,17 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
       }
     }
   }
-  uint32_t grid = (uint32_t)plan.nTiles;
-  if (useXb) {
+  // persistent grid of the XCD-block kernel; the bucket path's gated
+  // (fallback-only) passes use it too: a launch of nTiles workgroups that all
+  // exit at once still costs ~0.1 ms at 2^18 tiles (C5 shape)
+  uint32_t gridXb = (uint32_t)plan.nTiles;
+  if (useXb || bucket) {
     int perCU = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, kernel, G::THREADS, lds) != hipSuccess || perCU < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, kernelXb, G::THREADS, lds) != hipSuccess || perCU < 1)
       perCU = 1;
-    grid = (uint32_t)std::min<uint64_t>(plan.nTiles, (uint64_t)perCU * cu_count());
+    gridXb = (uint32_t)std::min<uint64_t>(plan.nTiles, (uint64_t)perCU * cu_count());
   }
+  const uint32_t grid = useXb ? gridXb : (uint32_t)plan.nTiles;
   int segPerCU = 0;
   if (bucket &&
       (hipOccupancyMaxActiveBlocksPerMultiprocessor(&segPerCU, sk, G::THREADS, lds) != hipSuccess || segPerCU < 1))
@@ -455,9 +460,10 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     g.gaNext = more ? grp[(p + 1) & 1].ga : nullptr;
     g.gpNext = more ? grp[(p + 1) & 1].gp : nullptr;
     ProfScope prof(stream, gate && (gateMask == kGateFallback || gateMask == kGateMode1) ? 3 : 1);  // fallback-only passes are timed apart
-    hipLaunchKernelGGL(kernel, dim3(grid), dim3(G::THREADS), lds, stream, kin, kout, vin, vout, n, orderMask,
-                       startBits + 8 * p, base + p * kBins, status[p & 1], next,
-                       useXb ? reinterpret_cast<uint32_t*>(claim + p * plan.claimBytes) : counters + p, err, g,
+    const bool xb = useXb || (bucket && gate);  // (bucket path: every claim area is zeroed up front)
+    hipLaunchKernelGGL(xb ? kernelXb : kernel, dim3(xb ? gridXb : grid), dim3(G::THREADS), lds, stream, kin, kout, vin,
+                       vout, n, orderMask, startBits + 8 * p, base + p * kBins, status[p & 1], next,
+                       xb ? reinterpret_cast<uint32_t*>(claim + p * plan.claimBytes) : counters + p, err, g,
                        g_stamps ? g_stamps + (uint64_t)p * plan.nTiles * kStampSlots : nullptr, gate, gateMask);
   };
   auto publish_error = [&]() -> int {
