@@ -163,7 +163,8 @@ def test_cpp_port_with_path_forced(gpu, path):
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
 
 
-@pytest.mark.parametrize("geom,seg", [("big", "1"), ("small", "1"), ("big", "0"), ("big", "top"), ("big32", "1")])
+@pytest.mark.parametrize("geom,seg", [("big", "1"), ("small", "1"), ("big", "0"), ("big", "top"), ("big32", "1"),
+                                      ("big", "1-noplanes")])
 @pytest.mark.parametrize("kt", [O.U32, O.F32])
 @pytest.mark.parametrize("desc", [False, True])
 def test_hybrid_paths_vs_oracle(gpu, kt, desc, geom, seg):
@@ -175,9 +176,12 @@ def test_hybrid_paths_vs_oracle(gpu, kt, desc, geom, seg):
     torch = gpu
     # the two top-digit passes XCD-segmented (default), neither, or the top one
     # only; local-sort geometry: 18432- or 9216-key chunks; u32 keys over the
-    # whole key sort 16-bit items in the big geometry unless "big32"
+    # whole key sort 16-bit items in the big geometry unless "big32"; u32 keys
+    # there travel as u16/u8 planes through the top-digit passes unless
+    # "noplanes" (thrs_options.planes)
     rs = make_sorter(kt, 0, desc, path="bucket",
-                     segmented={"1": "auto", "0": "none", "top": "top_only"}[seg], localGeometry=geom)
+                     segmented={"1": "auto", "0": "none", "top": "top_only"}[seg.split("-")[0]], localGeometry=geom,
+                     planes="off" if seg.endswith("noplanes") else "auto")
     dists = {
         "uniform": lambda k: k,
         "low20": lambda k: k & np.array(0xFFFFF, k.dtype),        # 16 buckets -> fallback above 295k keys
