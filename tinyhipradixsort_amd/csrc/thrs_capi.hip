@@ -77,15 +77,17 @@ struct Plan {
   uint64_t scratchBytes;  // header + 2 sets (ping-pong between passes) + 8 claim areas + hybrid area [+ u8 plane]
 };
 
-// hybrid area: u32 joint[65536] | segHistA[8][256] | chunkOff[65537] |
-// chunkB0[65537] | meta[4] | segment tables of the two top-digit passes
+// hybrid area: u32 joint[65536] | segHistA[8][256] | rowHist[256] | meta[64]
+// (all zeroed up front) | chunkOff[65537] | chunkB0[65537] | segment tables
+// of the two top-digit passes
 constexpr uint64_t kJointBytes = kBuckets * 4;
-constexpr uint64_t kSegHistAOff = kJointBytes;         // zeroed with joint
-constexpr uint64_t kJointZero = kJointBytes + kSegs * 256 * 4;
+constexpr uint64_t kSegHistAOff = kJointBytes;                    // per position segment: second-digit counts
+constexpr uint64_t kRowHistOff = kSegHistAOff + kSegs * 256 * 4;  // top-digit counts (thrs_hist_joint)
+constexpr uint64_t kMetaOff = kRowHistOff + 256 * 4;              // zero: thrs_plan_rows raises its flags atomically
+constexpr uint64_t kJointZero = kMetaOff + 256;
 constexpr uint64_t kChunkOffOff = kJointZero;
 constexpr uint64_t kChunkB0Off = kChunkOffOff + round_up_c((kBuckets + 1) * 4, 256);
-constexpr uint64_t kMetaOff = kChunkB0Off + round_up_c((kBuckets + 1) * 4, 256);
-constexpr uint64_t kSegInfoOff = kMetaOff + 256;      // segPos[9] | segTiles[9] ... tickets[8] at +256 B (thrs_pass_seg)
+constexpr uint64_t kSegInfoOff = kChunkB0Off + round_up_c((kBuckets + 1) * 4, 256);  // segPos[9] | segTiles[9] ... tickets[8] at +256 B (thrs_pass_seg)
 constexpr uint64_t kSegBaseOff = kSegInfoOff + 512;   // u32 [8][256] per-segment top-digit bases
 constexpr uint64_t kSegInfoAOff = kSegBaseOff + kSegs * 256 * 4;  // the same two for the second-digit pass
 constexpr uint64_t kSegBaseAOff = kSegInfoAOff + 512;
@@ -348,6 +350,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   // ---- kernels and their LDS opt-ins, before anything is enqueued
   const size_t lds = G::LDS_BYTES;
   auto kernelXb = atomicRank ? thrs_pass_xb<KT, VB, ST, true> : thrs_pass_xb<KT, VB, ST, false>;
+  auto kernelPersist = atomicRank ? thrs_pass_persist<KT, VB, ST, true> : thrs_pass_persist<KT, VB, ST, false>;
   auto kernel = useXb ? kernelXb : (atomicRank ? thrs_pass<KT, VB, ST, true> : thrs_pass<KT, VB, ST, false>);
   auto sk = atomicRank ? thrs_pass_seg<KT, VB, ST, true> : thrs_pass_seg<KT, VB, ST, false>;
   // plane codecs (u32 keys-only instantiations only; `planes` is false elsewhere)
@@ -358,7 +361,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   const int histPasses = bucket ? nLow : nPass;
   const size_t histLds = (size_t)histPasses * kBins * hist_copies<(int)sizeof(U)>() * 4;
   if (allow_lds(thrs_hist<KT>, histLds) != hipSuccess || allow_lds(kernel, lds) != hipSuccess ||
-      allow_lds(kernelXb, lds) != hipSuccess)
+      allow_lds(kernelXb, lds) != hipSuccess || allow_lds(kernelPersist, lds) != hipSuccess)
     return THRS_ERROR_HIP;
   if (bucket) {
     if (allow_lds(thrs_hist_joint<KT>, kJointLds) != hipSuccess || allow_lds(sk, lds) != hipSuccess)
@@ -389,16 +392,17 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
       }
     }
   }
-  // persistent grid of the XCD-block kernel; the bucket path's gated
-  // (fallback-only) passes use it too: a launch of nTiles workgroups that all
-  // exit at once still costs ~0.1 ms at 2^18 tiles (C5 shape)
-  uint32_t gridXb = (uint32_t)plan.nTiles;
-  if (useXb || bucket) {
+  // persistent grids (occupancy x CUs): the XCD-block kernel, and the bucket
+  // path's fallback-only passes (thrs_pass_persist): a launch of nTiles
+  // workgroups that all exit at once still costs ~0.1 ms at 2^18 tiles
+  auto persistent_grid = [&](auto kern) -> uint32_t {
     int perCU = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, kernelXb, G::THREADS, lds) != hipSuccess || perCU < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, kern, G::THREADS, lds) != hipSuccess || perCU < 1)
       perCU = 1;
-    gridXb = (uint32_t)std::min<uint64_t>(plan.nTiles, (uint64_t)perCU * cu_count());
-  }
+    return (uint32_t)std::min<uint64_t>(plan.nTiles, (uint64_t)perCU * cu_count());
+  };
+  const uint32_t gridXb = useXb ? persistent_grid(kernelXb) : (uint32_t)plan.nTiles;
+  const uint32_t gridPersist = bucket ? persistent_grid(kernelPersist) : (uint32_t)plan.nTiles;
   const uint32_t grid = useXb ? gridXb : (uint32_t)plan.nTiles;
   int segPerCU = 0;
   if (bucket &&
@@ -427,14 +431,27 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     if (bucket) {
       hipLaunchKernelGGL(thrs_hist_joint<KT>, dim3(hgrid), dim3(kHistThreads), kJointLds, stream,
                          static_cast<const U*>(keys), n, orderMask, startBits + 8 * nLow, vec, joint,
-                         reinterpret_cast<uint32_t*>(hyb + kSegHistAOff));
-      // chunks: whole buckets; neighbouring buckets below kLocCap/2 keys share one
-      hipLaunchKernelGGL(thrs_plan, dim3(1), dim3(kPlanThreads), 0, stream, joint, n, base + nLow * kBins, chunkOff,
-                         chunkB0, meta, kBucket64 ? Loc64::CAP : smallLocal ? LocSmall::CAP : LocBig::CAP,
-                         (VB || local16 || kBucket64) ? -1 : (smallLocal ? kLocSmallLogT : kLocLogT),  // -1: single-bucket chunks
-                         reinterpret_cast<uint32_t*>(hyb + kSegInfoOff), reinterpret_cast<uint32_t*>(hyb + kSegBaseOff),
-                         (uint32_t)G::TILE, reinterpret_cast<const uint32_t*>(hyb + kSegHistAOff), (uint32_t)hgrid,
-                         reinterpret_cast<uint32_t*>(hyb + kSegInfoAOff), reinterpret_cast<uint32_t*>(hyb + kSegBaseAOff));
+                         reinterpret_cast<uint32_t*>(hyb + kSegHistAOff), reinterpret_cast<uint32_t*>(hyb + kRowHistOff));
+      const uint32_t cap = kBucket64 ? Loc64::CAP : smallLocal ? LocSmall::CAP : LocBig::CAP;
+#ifndef THRS_PLAN_ROWS
+#define THRS_PLAN_ROWS 1
+#endif
+      if (THRS_PLAN_ROWS && (VB || local16 || kBucket64)) {
+        // single-bucket chunks: one workgroup per top digit
+        hipLaunchKernelGGL(thrs_plan_rows, dim3(kBins), dim3(kPlanRowThreads), 0, stream, joint,
+                           reinterpret_cast<const uint32_t*>(hyb + kRowHistOff),
+                           reinterpret_cast<const uint32_t*>(hyb + kSegHistAOff), n, cap, base + nLow * kBins,
+                           chunkOff, chunkB0, meta, reinterpret_cast<uint32_t*>(hyb + kSegInfoOff),
+                           reinterpret_cast<uint32_t*>(hyb + kSegBaseOff), (uint32_t)G::TILE, (uint32_t)hgrid,
+                           reinterpret_cast<uint32_t*>(hyb + kSegInfoAOff), reinterpret_cast<uint32_t*>(hyb + kSegBaseAOff));
+      } else {
+        // chunks: whole buckets; neighbouring buckets below kLocCap/2 keys share one
+        hipLaunchKernelGGL(thrs_plan, dim3(1), dim3(kPlanThreads), 0, stream, joint, n, base + nLow * kBins, chunkOff,
+                           chunkB0, meta, cap, (VB || local16 || kBucket64) ? -1 : smallLocal ? kLocSmallLogT : kLocLogT,
+                           reinterpret_cast<uint32_t*>(hyb + kSegInfoOff), reinterpret_cast<uint32_t*>(hyb + kSegBaseOff),
+                           (uint32_t)G::TILE, reinterpret_cast<const uint32_t*>(hyb + kSegHistAOff), (uint32_t)hgrid,
+                           reinterpret_cast<uint32_t*>(hyb + kSegInfoAOff), reinterpret_cast<uint32_t*>(hyb + kSegBaseAOff));
+      }
       // the low digits' histograms + bases: needed only on the fallback path
       hipLaunchKernelGGL(thrs_hist<KT>, dim3(hgrid), dim3(kHistThreads), histLds, stream, static_cast<const U*>(keys),
                          n, orderMask, startBits, nLow, vec, hist, meta + kMetaFallback);
@@ -460,10 +477,13 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     g.gaNext = more ? grp[(p + 1) & 1].ga : nullptr;
     g.gpNext = more ? grp[(p + 1) & 1].gp : nullptr;
     ProfScope prof(stream, gate && (gateMask == kGateFallback || gateMask == kGateMode1) ? 3 : 1);  // fallback-only passes are timed apart
-    const bool xb = useXb || (bucket && gate);  // (bucket path: every claim area is zeroed up front)
-    hipLaunchKernelGGL(xb ? kernelXb : kernel, dim3(xb ? gridXb : grid), dim3(G::THREADS), lds, stream, kin, kout, vin,
-                       vout, n, orderMask, startBits + 8 * p, base + p * kBins, status[p & 1], next,
-                       xb ? reinterpret_cast<uint32_t*>(claim + p * plan.claimBytes) : counters + p, err, g,
+    // fallback-only launches (most exit at once): persistent ticket kernel,
+    // unless the XCD-block kernel runs anyway
+    const bool fallbackOnly = gate && (gateMask == kGateFallback || gateMask == kGateMode1);
+    const bool persist = bucket && fallbackOnly && !useXb;
+    hipLaunchKernelGGL(persist ? kernelPersist : kernel, dim3(persist ? gridPersist : grid), dim3(G::THREADS), lds,
+                       stream, kin, kout, vin, vout, n, orderMask, startBits + 8 * p, base + p * kBins, status[p & 1],
+                       next, useXb ? reinterpret_cast<uint32_t*>(claim + p * plan.claimBytes) : counters + p, err, g,
                        g_stamps ? g_stamps + (uint64_t)p * plan.nTiles * kStampSlots : nullptr, gate, gateMask);
   };
   auto publish_error = [&]() -> int {

@@ -90,7 +90,8 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
                                                                 uint32_t n, typename KeyTraits<KT>::U orderMask,
                                                                 int bucketShift, int vec,
                                                                 uint32_t* __restrict__ joint,
-                                                                uint32_t* __restrict__ segHist /* [8][256] */) {
+                                                                uint32_t* __restrict__ segHist /* [8][256] */,
+                                                                uint32_t* __restrict__ rowHist /* [256] */) {
   using U = typename KeyTraits<KT>::U;
   extern __shared__ __attribute__((aligned(16))) uint32_t s_joint[];
   uint32_t* s_d2 = s_joint + kJointWords;
@@ -129,6 +130,7 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
       } else {
         atomicAdd(&joint[b], 0x8000u);
         atomicAdd(&segH[b & 255u], 0x8000u);
+        atomicAdd(&rowHist[b >> 8], 0x8000u);
       }
     }
   };
@@ -263,6 +265,7 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
     if (first) {
       atomicAdd(&joint[b], mult * 0x8000u);
       atomicAdd(&segH[b & 255u], mult * 0x8000u);
+      atomicAdd(&rowHist[b >> 8], mult * 0x8000u);
     }
   }
   for (uint32_t i = tid; i < kBuckets; i += kHistThreads) {
@@ -281,8 +284,118 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
     }
     __hip_atomic_fetch_add(&s_d2[d], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
+  // the range's top-digit counts (row sums: thread 4r+q sums words [128r +
+  // 32q, +32), two fields each, every field < 0x8000 after the last epoch)
+  {
+    const uint32_t r = tid >> 2, q = tid & 3u;
+    uint32_t c = 0;
+#pragma unroll 8
+    for (uint32_t i = 0; i < 32; ++i) {
+      const uint32_t x = s_joint[128 * r + 32 * q + i];
+      c += (x & 0xFFFFu) + (x >> 16);
+    }
+    c += __shfl_xor(c, 1);
+    c += __shfl_xor(c, 2);
+    if (q == 0 && c) atomicAdd(&rowHist[r], c);
+  }
   __syncthreads();
   if (tid < kBins && s_d2[tid]) atomicAdd(&segH[tid], s_d2[tid]);
+}
+
+// ------------------------------------------------------------- plan, rows
+// Single-bucket chunks (pairs, thrs_local16, 8-byte keys): chunk c is bucket
+// c, so the plan needs no chunk-counting sweep and splits by top digit: one
+// workgroup per row r (the 256 buckets of top digit r).  The top-digit totals
+// come from thrs_hist_joint (rowHist), the second digit's from the position
+// segments' counts (segHistA), so no workgroup waits on another.
+//   chunkOff[256r + t] = base(r) + (keys of row r's buckets before t)
+//   segBase[s][r]      = base(r) + (keys of row r in columns < 32s)
+//   fallback / mode    raised atomically (meta is zeroed with the histogram)
+// Workgroup 0 also writes the second digit's bases, both passes' segment
+// tables and the chunk count.
+constexpr int kPlanRowThreads = 256;
+__global__ __launch_bounds__(kPlanRowThreads) void thrs_plan_rows(
+    const uint32_t* __restrict__ joint, const uint32_t* __restrict__ rowHist, const uint32_t* __restrict__ segHistA,
+    uint32_t n, uint32_t cap, uint32_t* __restrict__ baseTop /* [2][256]: second, top */,
+    uint32_t* __restrict__ chunkOff, uint32_t* __restrict__ chunkB0, uint32_t* __restrict__ meta,
+    uint32_t* __restrict__ segInfo, uint32_t* __restrict__ segBase, uint32_t tileKeys, uint32_t histGrid,
+    uint32_t* __restrict__ segInfoA, uint32_t* __restrict__ segBaseA) {
+  __shared__ uint32_t s_w[2][4], s_base, s_b2[kBins];
+  const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6, r = blockIdx.x;
+  // 256-thread exclusive scan (4 waves)
+  auto scan256 = [&](uint32_t v, int slot, uint32_t* total) -> uint32_t {
+    const uint32_t inc = wave_incl_scan(v, lane);
+    if (lane == 63) s_w[slot][w] = inc;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t x = s_w[slot][i];
+      pre += (i < (int)w) ? x : 0u;
+      tot += x;
+    }
+    if (total) *total = tot;
+    return pre + inc - v;
+  };
+  // base(r): exclusive scan of the top-digit totals
+  const uint32_t rowTot = rowHist[t];
+  const uint32_t rowEx = scan256(rowTot, 0, nullptr);
+  if (t == r) s_base = rowEx;
+  const uint32_t x = joint[kBins * r + t];
+  const uint32_t pre = scan256(x, 1, nullptr);  // (its barrier also publishes s_base)
+  const uint32_t base = s_base;
+  chunkOff[kBins * r + t] = base + pre;
+  chunkB0[kBins * r + t] = kBins * r + t;
+  if ((t & 31u) == 0) segBase[(t >> 5) * kBins + r] = base + pre;  // segment s = columns [32s, 32s+32)
+  if (t == 0) baseTop[kBins + r] = base;
+  if (x > cap) {  // a bucket above the chunk capacity: fallback; all n keys in one bucket: mode 2
+    atomicOr(&meta[kMetaFallback], 1u);
+    atomicMax(&meta[kMetaMode], x == n ? 2u : 1u);
+  }
+  if (r != 0) return;
+  // second digit: totals over the position segments -> bases, segment bases
+  uint32_t tot2 = 0;
+#pragma unroll
+  for (int sg = 0; sg < kSegs; ++sg) tot2 += segHistA[sg * kBins + t];
+  __syncthreads();  // s_w reuse
+  const uint32_t b2 = scan256(tot2, 0, nullptr);
+  baseTop[t] = b2;
+  s_b2[t] = b2;
+  uint32_t sa = b2;
+#pragma unroll
+  for (int sg = 0; sg < kSegs; ++sg) {
+    segBaseA[sg * kBins + t] = sa;
+    sa += segHistA[sg * kBins + t];
+  }
+  __syncthreads();
+  // segment positions, first tile ids (multiples of kGroup), tickets: thread 0
+  // for the top-digit pass (second-digit ranges), thread 64 for the
+  // second-digit pass (position ranges) -- as thrs_plan
+  if (t == 0 || t == 64) {
+    const bool top = t == 0;
+    uint32_t* info = top ? segInfo : segInfoA;
+    auto pos_of = [&](int sg) -> uint32_t {
+      if (sg >= kSegs) return n;
+      return top ? s_b2[32 * sg] : hj_seg_pos(n, histGrid, (uint32_t)sg);
+    };
+    uint32_t tiles = 0;
+    for (int sg = 0; sg <= kSegs; ++sg) {
+      const uint32_t pos = pos_of(sg);
+      info[sg] = pos;
+      info[kSegs + 1 + sg] = tiles;
+      if (sg < kSegs) {
+        const uint32_t len = pos_of(sg + 1) - pos;
+        const uint32_t nT = (len + tileKeys - 1) / tileKeys;
+        tiles += (nT + kGroup - 1) / kGroup * kGroup;
+        info[64 + sg] = 0;  // ticket (own cache line)
+      }
+    }
+  }
+  if (t == 128) {
+    chunkOff[kBuckets] = n;
+    chunkB0[kBuckets] = kBuckets;
+    meta[kMetaChunks] = kBuckets;
+  }
 }
 
 // ------------------------------------------------------------------- plan

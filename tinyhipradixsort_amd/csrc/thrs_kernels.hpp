@@ -1255,6 +1255,47 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
                                      statusNext, errFlag, tile, 0, grp, smem, stamps, k, v, NoMid{});
 }
 
+// Persistent form with plain ticket claims: the bucket path's fallback-only
+// passes (gated: they exit at once unless the fallback flag is set), where
+// one workgroup per tile would cost ~0.1 ms of empty dispatch at 2^18 tiles.
+// Tiles are claimed in ticket order, so every earlier tile is held by a
+// running workgroup (deadlock-free exactly as thrs_pass).
+template <int KT, int VB, typename ST, bool ATOMIC_RANK>
+__global__ __launch_bounds__((PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::THREADS))
+__attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::WPE))) void thrs_pass_persist(
+    const typename KeyTraits<KT>::U* __restrict__ keysIn, typename KeyTraits<KT>::U* __restrict__ keysOut,
+    const typename ValueWord<VB>::T* __restrict__ valsIn, typename ValueWord<VB>::T* __restrict__ valsOut,
+    uint32_t n, typename KeyTraits<KT>::U orderMask, int shift, const uint32_t* __restrict__ digitBase,
+    ST* __restrict__ status, ST* __restrict__ statusNext, uint32_t* __restrict__ tileCounter,
+    uint32_t* __restrict__ errFlag, GroupTables<ST> grp, uint64_t* __restrict__ stamps,
+    const uint32_t* __restrict__ gate, uint32_t gateMask) {
+  if (gate && !((gateMask >> *gate) & 1u)) return;  // not needed on this launch path (thrs_plan decides)
+  using U = typename KeyTraits<KT>::U;
+  using VW = typename ValueWord<VB>::T;
+  using G = PassGeom<sizeof(U), VB>;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint32_t* s_cnt = reinterpret_cast<uint32_t*>(smem + G::STAGE * (sizeof(U) + VB));
+  uint32_t* s_misc = s_cnt + (G::WAVES + 1) * kBins;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t nTiles = (uint32_t)(((uint64_t)n + G::TILE - 1) / G::TILE);
+  const uint32_t myBase = digitBase[tid & 255u];
+  (void)stamps;
+  U k[G::KPT];
+  VW v[VB ? G::KPT : 1];
+  for (;;) {
+    if (tid == 0) s_misc[0] = atomicAdd(tileCounter, 1u);
+    for (uint32_t i = tid; i < (uint32_t)(G::WAVES * kBins); i += G::THREADS) s_cnt[i] = 0;
+    lds_barrier();
+    const uint32_t tile = s_misc[0];
+    if (tile >= nTiles) break;
+    load_tile<KT, VB>(keysIn, valsIn, (uint64_t)tile * G::TILE, tile_valid<G::TILE>(n, tile), k, v);
+    pass_tile<KT, VB, ST, ATOMIC_RANK>(keysIn, keysOut, valsIn, valsOut, (uint64_t)tile * G::TILE,
+                                       tile_valid<G::TILE>(n, tile), orderMask, shift, myBase, status,
+                                       statusNext, errFlag, tile, 0, grp, smem, nullptr, k, v, NoMid{});
+    lds_barrier();  // stage, s_gofs and s_misc[0] are reused by the next tile
+  }
+}
+
 // ============================================================ XCD-block claims
 // Tiles are claimed in BLOCKS of kXcdBlock consecutive tiles, one open block
 // per XCD, so neighbouring tiles -- whose digit runs share the 128-B lines at
