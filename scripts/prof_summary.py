@@ -20,7 +20,7 @@ import sys
 from collections import defaultdict
 
 FAMILIES = ["thrs_pass_seg", "thrs_pass_xb", "thrs_pass", "thrs_hist_joint", "thrs_hist", "thrs_scan", "thrs_plan",
-            "thrs_local16", "thrs_local64", "thrs_local_pairs", "thrs_local", "thrs_copy_gated", "thrs_digit_hist",
+            "thrs_local_count16", "thrs_local16", "thrs_local64", "thrs_local_pairs", "thrs_local", "thrs_copy_gated", "thrs_digit_hist",
             "thrs_err_publish", "k_fill_dist",
             "k_copy_u128", "k_copy_u32", "k_fill", "k_iota", "k_sorted", "k_fingerprint", "thrs_probe"]
 # dominant global access width per family, for counter calibration

@@ -62,6 +62,13 @@ inline uint64_t tile_keys(int kb, int vb) {
   }
 }
 
+#ifndef THRS_COUNT16_DEFAULT
+// u32 keys-only local sort over 16-bit items: 1 = counting (thrs_local_count16)
+// unless RANK16 is asked; 0 = two LSD rounds (thrs_local16) unless COUNT16 is
+// asked.  Counting measured slower (docs/EXPERIMENTS.md row 56: 2.63 vs 1.78 ms)
+#define THRS_COUNT16_DEFAULT 0
+#endif
+
 struct Plan {
   int kb, vb;         // key / value bytes (vb = 0 for sortKeys)
   uint64_t tileKeys;  // keys per tile of the pass kernel
@@ -325,6 +332,9 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   // (thrs_hybrid.hpp thrs_local16) over single-bucket chunks
   const bool local16 = bucket && KT == 0 && VB == 0 && fullWindow && !smallLocal &&
                        opt.localGeometry != THRS_LOCAL_BIG32;
+  // ... sorted by counting (thrs_local_count16) or by two LSD rounds (thrs_local16)
+  const bool count16 = local16 && (opt.localGeometry == THRS_LOCAL_COUNT16 ||
+                                   (opt.localGeometry != THRS_LOCAL_RANK16 && THRS_COUNT16_DEFAULT));
   const bool segTop = opt.segmented != THRS_SEG_NONE;
   const bool segA = opt.segmented == THRS_SEG_AUTO;
   // local16 with both top-digit passes segmented: the passes carry the keys
@@ -373,10 +383,13 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
         return THRS_ERROR_HIP;
     } else if constexpr (kBucketType) {
       if (local16) {
-        if constexpr (KT == 0 && VB == 0)
+        if constexpr (KT == 0 && VB == 0) {
           if (allow_lds(atomicRank ? thrs_local16<true, Loc16> : thrs_local16<false, Loc16>, Loc16::LDS) !=
-              hipSuccess)
+                  hipSuccess ||
+              allow_lds(thrs_local_count16<true>, LocCount::LDS) != hipSuccess ||
+              allow_lds(thrs_local_count16<false>, LocCount::LDS) != hipSuccess)
             return THRS_ERROR_HIP;
+        }
       } else if constexpr (VB == 4) {
         if (allow_lds(atomicRank ? thrs_local_pairs<true, LocBig> : thrs_local_pairs<false, LocBig>,
                       LocBig::lds<U>()) != hipSuccess ||
@@ -619,10 +632,20 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                            chunkOff, chunkB0, meta);
       } else if (local16) {
         if constexpr (KT == 0 && VB == 0) {
-          auto lk = atomicRank ? thrs_local16<true, Loc16> : thrs_local16<false, Loc16>;
-          hipLaunchKernelGGL(lk, dim3((uint32_t)maxChunks), dim3(Loc16::THREADS), Loc16::LDS, stream,
-                             reinterpret_cast<uint32_t*>(K), (uint32_t)orderMask, chunkOff, chunkB0, meta,
-                             planes ? static_cast<const uint16_t*>(lo2P) : nullptr);
+          if (count16) {
+            // persistent: one 128-KiB workgroup per CU walks the chunks
+            const uint32_t cgrid = (uint32_t)std::min<uint64_t>(maxChunks, (uint64_t)cu_count());
+            // planes off / mode 2: the items are the keys themselves (in place)
+            auto lk = planes ? thrs_local_count16<true> : thrs_local_count16<false>;
+            hipLaunchKernelGGL(lk, dim3(cgrid), dim3(LocCount::THREADS), LocCount::LDS, stream,
+                               reinterpret_cast<uint32_t*>(K), n, (uint32_t)orderMask, chunkOff, chunkB0, meta,
+                               static_cast<const uint16_t*>(lo2P), joint);
+          } else {
+            auto lk = atomicRank ? thrs_local16<true, Loc16> : thrs_local16<false, Loc16>;
+            hipLaunchKernelGGL(lk, dim3((uint32_t)maxChunks), dim3(Loc16::THREADS), Loc16::LDS, stream,
+                               reinterpret_cast<uint32_t*>(K), (uint32_t)orderMask, chunkOff, chunkB0, meta,
+                               planes ? static_cast<const uint16_t*>(lo2P) : nullptr);
+          }
         }
       } else if (smallLocal) {
         launch_local(LocSmall{});
@@ -657,7 +680,7 @@ int run_vb(int vb, void* keys, void* vals, uint32_t n, void* tmp, void* ko, void
 
 bool valid_options(const thrs_options& o) {
   return o.path >= THRS_PATH_AUTO && o.path <= THRS_PATH_BUCKET && o.localGeometry >= THRS_LOCAL_AUTO &&
-         o.localGeometry <= THRS_LOCAL_BIG32 && o.segmented >= THRS_SEG_AUTO && o.segmented <= THRS_SEG_NONE &&
+         o.localGeometry <= THRS_LOCAL_RANK16 && o.segmented >= THRS_SEG_AUTO && o.segmented <= THRS_SEG_NONE &&
          o.tileClaims >= THRS_CLAIMS_AUTO && o.tileClaims <= THRS_CLAIMS_TICKET && o.rank >= THRS_RANK_AUTO &&
          o.rank <= THRS_RANK_BALLOT && o.planes >= THRS_PLANES_AUTO && o.planes <= THRS_PLANES_OFF;
 }

@@ -1110,6 +1110,210 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(6))
     if (j * 64 < lim) src[j * 64] = (hiBits | o[j]) ^ orderMask;
 }
 
+// ------------------------------------------- local sort, counting (keys only)
+// The same chunks as thrs_local16 (u32 keys without values over the whole key,
+// single-bucket chunks), sorted by COUNTING instead of two LSD rounds: without
+// values, equal 16-bit items are indistinguishable, so a chunk's sorted order
+// is fully described by how often each of the 65536 item values occurs.
+// Per chunk (one 1024-thread workgroup per CU, persistent):
+//   1. count   one no-return LDS add per key into 65536 16-bit counters (two
+//              per word, 128 KiB; a chunk holds <= 18432 keys, so no field
+//              overflows); a wave whose 64 items are equal adds 64 once
+//   2. scan    thread t owns counter words [32t, 32t + 32) (values 64t ..
+//              64t + 63): a running sum in registers, one block scan of the
+//              thread totals; every word is zeroed as it is read.  Words are
+//              rotated within their 32-word row (cnt_at) so that the 64 lanes
+//              reading "their j-th word" hit distinct banks
+//   3. marks   for each present value v with output offset o: stage[o] = v
+//              (the stage is the first 36 KiB of the zeroed counters)
+//   4. fill    an inclusive MAX scan over the stage fills the runs of equal
+//              items (values ascend with the position, unmarked slots are 0);
+//              the keys are rebuilt from the bucket and written coalesced
+// LDS work is ~4 counter words per key instead of two rounds of count / scan
+// / rank / scatter; the next chunk's items are loaded during this one (its
+// offsets one chunk earlier still).  Every global load and store is
+// unconditional (clamped loads; a lane past the chunk stores the chunk's last
+// key again, which the max scan carries there, or -- empty chunk -- writes
+// the sink), so the compiler's vmcnt waits count exactly and the prefetch
+// stays in flight.
+struct LocCount {
+  static constexpr int THREADS = 1024, WAVES = 16, ITEMS = 18;
+  static constexpr uint32_t CAP = (uint32_t)THREADS * ITEMS;     // 18432
+  static constexpr uint32_t WORDS = kBuckets / 2;                // counters: two 16-bit fields per word
+  static constexpr int ROWW = (int)(WORDS / THREADS);            // 32 words per thread
+  static constexpr uint32_t WAVE_SLOTS = CAP / WAVES;            // 1152 stage slots per wave in step 4
+  static constexpr size_t LDS = (size_t)WORDS * 4;               // 128 KiB
+  __device__ static uint32_t cnt_at(uint32_t word) {             // rotate within the 32-word row
+    return (word & ~31u) | ((word + (word >> 5)) & 31u);
+  }
+};
+static_assert(LocCount::CAP == Loc16::CAP, "same chunk capacity as thrs_local16 (thrs_plan's cap)");
+static_assert(LocCount::CAP / 2 <= LocCount::WORDS, "the stage fits in the counter words");
+static_assert(LocCount::ROWW == 32, "cnt_at rotates 32-word rows");
+
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, kDppRowShr | 1, 0xf, 0xf, false));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, kDppRowShr | 2, 0xf, 0xf, false));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, kDppRowShr | 4, 0xf, 0xf, false));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, kDppRowShr | 8, 0xf, 0xf, false));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, kDppRowBcast15, 0xa, 0xf, false));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, kDppRowBcast31, 0xc, 0xf, false));
+  return x;
+}
+
+// PLANE: items from the u16 plane `lo` (the key-planes codecs), else the low
+// 16 bits of the keys' images in place.  sink: >= 64 * ITEMS words of scratch
+// nobody reads (the bucket histogram, consumed by thrs_plan before this launch).
+template <bool PLANE>
+__global__ __launch_bounds__(LocCount::THREADS) void thrs_local_count16(
+    uint32_t* __restrict__ keys, uint32_t n, uint32_t orderMask, const uint32_t* __restrict__ chunkOff,
+    const uint32_t* __restrict__ chunkB0, const uint32_t* __restrict__ meta, const uint16_t* __restrict__ lo,
+    uint32_t* __restrict__ sink) {
+  using LC = LocCount;
+  constexpr int IT = LC::ITEMS, RW = LC::ROWW;
+  constexpr uint32_t NONE = 0xFFFFFFFFu;
+  if (meta[kMetaFallback] != 0) return;
+  const uint32_t nChunks = meta[kMetaChunks];
+  if (blockIdx.x >= nChunks) return;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(smem);
+  uint16_t* stage = reinterpret_cast<uint16_t*>(smem);
+  __shared__ uint32_t s_wsum[LC::WAVES], s_wmax[LC::WAVES];
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t G = gridDim.x;
+
+  for (uint32_t i = tid; i < LC::WORDS / 4; i += LC::THREADS)
+    reinterpret_cast<uint4*>(cnt)[i] = make_uint4(0, 0, 0, 0);
+
+  // item k of thread tid = chunk position 1024k + tid (64 consecutive per wave)
+  // (indices built from loop-variant bases: per-item constants hoisted out of
+  // the chunk loop would pin 18 registers each)
+  // Raw loads only: whether item k exists is decided where it is used.
+  // Addresses are a scalar chunk base plus a 32-bit byte offset (one VGPR).
+  auto load_items = [&](uint32_t (&nx)[IT], uint32_t st, uint32_t sz) __attribute__((always_inline)) {
+    const uint32_t last = sz ? sz - 1 : 0u;
+    const size_t b = sz ? st : 0u;  // an empty chunk may start at n: read key 0 instead
+    const char* base = PLANE ? reinterpret_cast<const char*>(lo + b) : reinterpret_cast<const char*>(keys + b);
+    uint32_t r0 = tid;
+    pin(r0);
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+      const uint32_t off = min(r0 + (uint32_t)k * LC::THREADS, last) * (PLANE ? 2u : 4u);
+      if constexpr (PLANE) nx[k] = *reinterpret_cast<const uint16_t*>(base + off);
+      else nx[k] = *reinterpret_cast<const uint32_t*>(base + off);
+    }
+  };
+  // Two register sets, A and B, in turn: chunk i is counted from one while
+  // chunk i+1 loads into the other (a single set would be copied at the loop
+  // latch, which waits for the loads -- and the stores issued after them).
+  uint32_t A[IT], B[IT];
+  uint32_t c = blockIdx.x;
+  uint32_t nStart = chunkOff[c], nSize = chunkOff[c + 1] - nStart, nHi = chunkB0[c];
+  load_items(A, nStart, nSize);
+  uint32_t c2 = min(c + G, nChunks - 1);
+  uint32_t mStart = chunkOff[c2], mEnd = chunkOff[c2 + 1], mHi = chunkB0[c2];
+
+  auto body = [&](uint32_t (&it)[IT], uint32_t (&nx)[IT]) __attribute__((always_inline)) {
+    const uint32_t start = nStart, size = nSize, hiBits = nHi << 16;
+    // the next chunk's items in flight during this one (clamped: always a
+    // valid load); the one after that: its offsets
+    nStart = mStart;
+    nSize = mEnd - mStart;
+    nHi = mHi;
+    load_items(nx, nStart, nSize);
+    c2 = min(c + 2 * G, nChunks - 1);
+    mStart = chunkOff[c2];
+    mEnd = chunkOff[c2 + 1];
+    mHi = chunkB0[c2];
+
+    if (size != 0) {
+      // 1. count
+      uint32_t rc = tid;
+      pin(rc);
+#pragma unroll
+      for (int k = 0; k < IT; ++k) {
+        const uint32_t v = rc + (uint32_t)k * LC::THREADS < size ? (PLANE ? it[k] : (it[k] ^ orderMask) & 0xFFFFu) : NONE;
+        const bool uni = __all(__builtin_amdgcn_readfirstlane(v) == v);
+        const uint32_t add = uni ? (lane == 0 ? 64u : 0u) : 1u;
+        if (v != NONE && add != 0)
+          __hip_atomic_fetch_add(&cnt[LC::cnt_at(v >> 1)], add << ((v & 1u) * 16), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      lds_barrier();
+      // 2. scan: this thread's 32 words in value order, zeroed as read
+      uint32_t cw[RW], run = 0;
+      uint32_t rt = tid;
+      pin(rt);  // opaque per chunk: the 32 word addresses are not hoisted out of the chunk loop
+#pragma unroll
+      for (int j = 0; j < RW; ++j) {
+        const uint32_t a = rt * RW + ((uint32_t)j + rt) % RW;  // cnt_at(32 tid + j)
+        cw[j] = cnt[a];
+        cnt[a] = 0;
+      }
+#pragma unroll
+      for (int j = 0; j < RW; ++j) run += (cw[j] & 0xFFFFu) + (cw[j] >> 16);
+      for (int j = 0; j < RW; ++j) pin(cw[j]);  // else the fields are split into 64 registers (spills)
+      const uint32_t inc = wave_incl_scan(run, lane);
+      if (lane == 63) s_wsum[w] = inc;
+      lds_barrier();
+      uint32_t o = inc - run;
+#pragma unroll
+      for (int ww = 0; ww < LC::WAVES - 1; ++ww) o += ww < (int)w ? s_wsum[ww] : 0u;
+      // 3. marks
+#pragma unroll
+      for (int j = 0; j < RW; ++j) {
+        const uint32_t a = cw[j] & 0xFFFFu, b = cw[j] >> 16, v0 = 2 * (rt * RW + j);
+        if (a) stage[o] = (uint16_t)v0;
+        o += a;
+        if (b) stage[o] = (uint16_t)(v0 + 1);
+        o += b;
+      }
+      lds_barrier();
+      // 4a. read this wave's stage slots, their max, zero them for the next chunk
+      const uint16_t* sw = stage + w * LC::WAVE_SLOTS + lane;
+      uint32_t y[IT], m = 0;
+#pragma unroll
+      for (int k = 0; k < IT; ++k) {
+        y[k] = sw[64 * k];
+        m = max(m, y[k]);
+      }
+      m = lane63(wave_incl_max(m));
+      if (lane == 0) s_wmax[w] = m;
+      uint32_t* zw = cnt + w * (LC::WAVE_SLOTS / 2) + lane;
+#pragma unroll
+      for (int j = 0; j < (int)(LC::WAVE_SLOTS / 128); ++j) zw[64 * j] = 0;
+      lds_barrier();
+      // 4b. max scan and write-out (every store unconditional, see above)
+      uint32_t carry = 0;
+#pragma unroll
+      for (int ww = 0; ww < LC::WAVES - 1; ++ww) carry = max(carry, ww < (int)w ? s_wmax[ww] : 0u);
+      char* const dbase = reinterpret_cast<char*>(keys + start);
+      uint32_t d0 = w * LC::WAVE_SLOTS + lane;
+      pin(d0);
+#pragma unroll
+      for (int k = 0; k < IT; ++k) {
+        const uint32_t x = max(wave_incl_max(y[k]), carry);
+        carry = lane63(x);
+        *reinterpret_cast<uint32_t*>(dbase + min(d0 + 64u * k, size - 1) * 4u) = (hiBits | x) ^ orderMask;
+      }
+    } else {
+      // empty chunk: as many (dummy) stores as a full one, so the vmcnt
+      // waits on the prefetched items are the same on both paths
+#pragma unroll
+      for (int k = 0; k < IT; ++k) sink[64 * k + lane] = k;
+    }
+  };
+  for (;;) {
+    body(A, B);
+    c += G;
+    if (c >= nChunks) break;
+    body(B, A);
+    c += G;
+    if (c >= nChunks) break;
+  }
+}
+
 // ------------------------------------------------------ local sort, pairs
 // sortPairs with u32 keys and 4-byte values over the whole key (startBits 0,
 // 32 bits): chunks are single buckets (thrs_plan single mode), so a key is
