@@ -425,6 +425,24 @@ def main():
         bad = TU.count_unsorted(kt, ko, n_out, 0, kb * 8)
         if bad:
             raise SystemExit(f"bench: rank {rank} output is not sorted ({bad} inversions)")
+        # across ranks: every key arrived somewhere, and rank r's last key <=
+        # rank r+1's first (unsigned key types compare as stored)
+        tot = torch.tensor([n_out], dtype=torch.int64, device="cuda")
+        dist.all_reduce(tot)
+        if int(tot.item()) != n * world:
+            raise SystemExit(f"bench: {int(tot.item())} keys after the exchange, expected {n * world}")
+        if kt in (T.KeyType.U32, T.KeyType.U64):
+            kdt = torch.int32 if kb == 4 else torch.int64
+            kv = ko.view(kdt)[:n_out].to(torch.int64)
+            ends = torch.tensor([[n_out, kv[0].item(), kv[-1].item()] if n_out else [0, 0, 0]], dtype=torch.int64,
+                                device="cuda")
+            allends = [torch.empty_like(ends) for _ in range(world)]
+            dist.all_gather(allends, ends)
+            mask = (1 << (8 * kb)) - 1
+            seq = [(int(e[0, 1]) & mask, int(e[0, 2]) & mask) for e in allends if int(e[0, 0]) > 0]
+            for (_a0, a1), (b0, _b1) in zip(seq, seq[1:]):
+                if a1 > b0:
+                    raise SystemExit("bench: ranks' key ranges overlap after the exchange")
         recycled = False
         vendor = ref_gpu = None
         elapsed = t1 - t0
