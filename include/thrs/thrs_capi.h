@@ -60,7 +60,7 @@ typedef struct thrs_config {
  * never fit the local sort).  Nothing is read from the environment. */
 enum { THRS_PATH_AUTO = 0, THRS_PATH_LSD = 1, THRS_PATH_BUCKET = 2 };
 enum { THRS_LOCAL_AUTO = 0, THRS_LOCAL_BIG = 1, THRS_LOCAL_SMALL = 2, THRS_LOCAL_BIG32 = 3, THRS_LOCAL_COUNT16 = 4,
-       THRS_LOCAL_RANK16 = 5 };
+       THRS_LOCAL_RANK16 = 5, THRS_LOCAL_WIDE16 = 6 };
 enum { THRS_SEG_AUTO = 0, THRS_SEG_TOP_ONLY = 1, THRS_SEG_NONE = 2 };
 enum { THRS_CLAIMS_AUTO = 0, THRS_CLAIMS_XCD_BLOCKS = 1, THRS_CLAIMS_TICKET = 2 };
 enum { THRS_RANK_AUTO = 0, THRS_RANK_ATOMIC = 1, THRS_RANK_BALLOT = 2 };
@@ -73,7 +73,8 @@ typedef struct thrs_options {
                             9216-key chunks; BIG32 = no 16-bit items (u32 keys);
                             u32 keys-only over the whole key, 18432-key chunks:
                             COUNT16 = counting sort of the 16-bit items, RANK16 =
-                            two LSD rounds on them                                  */
+                            two LSD rounds on them; WIDE16 = the same rounds in
+                            36864-key chunks (AUTO above 2^30 + 2^26, to 2^31 + 2^27) */
   int32_t segmented;     /* THRS_SEG_*: XCD-segmented top-digit passes (AUTO: both)   */
   int32_t tileClaims;    /* THRS_CLAIMS_*: XCD-block tile claims in the digit passes
                             (AUTO: 4-byte keys without values, n >= 2^29)            */

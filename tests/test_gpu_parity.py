@@ -165,7 +165,7 @@ def test_cpp_port_with_path_forced(gpu, path):
 
 @pytest.mark.parametrize("geom,seg", [("big", "1"), ("small", "1"), ("big", "0"), ("big", "top"), ("big32", "1"),
                                       ("big", "1-noplanes"), ("count16", "1"), ("count16", "1-noplanes"),
-                                      ("count16", "0")])
+                                      ("count16", "0"), ("wide16", "1"), ("wide16", "1-noplanes")])
 @pytest.mark.parametrize("kt", [O.U32, O.F32])
 @pytest.mark.parametrize("desc", [False, True])
 def test_hybrid_paths_vs_oracle(gpu, kt, desc, geom, seg):
@@ -178,7 +178,8 @@ def test_hybrid_paths_vs_oracle(gpu, kt, desc, geom, seg):
     # the two top-digit passes XCD-segmented (default), neither, or the top one
     # only; local-sort geometry: 18432- or 9216-key chunks; u32 keys over the
     # whole key sort 16-bit items in the big geometry unless "big32" -- by two
-    # LSD rounds (default, "rank16") or by counting ("count16"); u32 keys
+    # LSD rounds (default, "rank16") or by counting ("count16"), or in 36864-key
+    # chunks ("wide16", the default above 2^30 + 2^26); u32 keys
     # there travel as u16/u8 planes through the top-digit passes unless
     # "noplanes" (thrs_options.planes)
     rs = make_sorter(kt, 0, desc, path="bucket",

@@ -120,13 +120,13 @@ class Options:
     reference counterpart.  Every choice gives the same bit-exact result; the
     defaults are the library's own choice.  Values are the names below."""
     path: str = "auto"            # auto | lsd | bucket
-    localGeometry: str = "auto"   # auto | big | small | big32 | count16 | rank16
+    localGeometry: str = "auto"   # auto | big | small | big32 | count16 | rank16 | wide16
     segmented: str = "auto"       # auto | top_only | none
     tileClaims: str = "auto"      # auto | xcd_blocks | ticket
     rank: str = "auto"            # auto | atomic | ballot
     planes: str = "auto"          # auto | on | off
 
-    _ENUMS = {"path": ("auto", "lsd", "bucket"), "localGeometry": ("auto", "big", "small", "big32", "count16", "rank16"),
+    _ENUMS = {"path": ("auto", "lsd", "bucket"), "localGeometry": ("auto", "big", "small", "big32", "count16", "rank16", "wide16"),
               "segmented": ("auto", "top_only", "none"), "tileClaims": ("auto", "xcd_blocks", "ticket"),
               "rank": ("auto", "atomic", "ballot"), "planes": ("auto", "on", "off")}
 

@@ -62,6 +62,9 @@ inline uint64_t tile_keys(int kb, int vb) {
   }
 }
 
+#ifndef THRS_WIDE16_AUTO
+#define THRS_WIDE16_AUTO 1  // AUTO takes the bucket path (wide 16-bit local sort) for u32 keys-only up to 2^31 + 2^27
+#endif
 #ifndef THRS_COUNT16_DEFAULT
 // u32 keys-only local sort over 16-bit items: 1 = counting (thrs_local_count16)
 // unless RANK16 is asked; 0 = two LSD rounds (thrs_local16) unless COUNT16 is
@@ -320,12 +323,16 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   // (8-byte keys: one 17408-slot chunk per bucket, so up to 2^30 + 2^24: the
   // largest uniform bucket stays ~3 sigma below the capacity)
   const bool sizeOk = nn >= (1ull << 28) && nn <= (1ull << 30) + (sizeof(U) == 8 ? (1ull << 24) : (1ull << 26));
+  // u32 keys without values over the whole key: up to 2^31 + 2^27 with the
+  // wide 16-bit local sort (Loc16Wide: 36864-key chunks)
+  const bool wideOk = THRS_WIDE16_AUTO && KT == 0 && VB == 0 && fullWindow && nn > (1ull << 30) + (1ull << 26) &&
+                      nn <= (1ull << 31) + (1ull << 27);
   const bool smallLocal = opt.localGeometry == THRS_LOCAL_SMALL ? true
-                          : (opt.localGeometry == THRS_LOCAL_BIG || opt.localGeometry == THRS_LOCAL_BIG32)
+                          : opt.localGeometry != THRS_LOCAL_AUTO  // BIG, BIG32 and the 16-bit kernels
                               ? false
                               : nn <= (1ull << 29);
   const bool bucket = kBucketType && !counts && nPass >= 3 &&
-                      (opt.path == THRS_PATH_BUCKET || (opt.path == THRS_PATH_AUTO && sizeOk)) &&
+                      (opt.path == THRS_PATH_BUCKET || (opt.path == THRS_PATH_AUTO && (sizeOk || wideOk))) &&
                       ((kBucket32 && VB == 0) || fullWindow);
   const int nLow = nPass - 2;
   // u32 keys over the whole key, large chunks: the local sort on 16-bit items
@@ -333,8 +340,12 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   const bool local16 = bucket && KT == 0 && VB == 0 && fullWindow && !smallLocal &&
                        opt.localGeometry != THRS_LOCAL_BIG32;
   // ... sorted by counting (thrs_local_count16) or by two LSD rounds (thrs_local16)
-  const bool count16 = local16 && (opt.localGeometry == THRS_LOCAL_COUNT16 ||
-                                   (opt.localGeometry != THRS_LOCAL_RANK16 && THRS_COUNT16_DEFAULT));
+  // ... in 36864-key chunks (explicitly, or by default above 2^30 + 2^26)
+  const bool wide16 = local16 && (opt.localGeometry == THRS_LOCAL_WIDE16 ||
+                                  (opt.localGeometry == THRS_LOCAL_AUTO && nn > (1ull << 30) + (1ull << 26)));
+  const bool count16 = local16 && !wide16 &&
+                       (opt.localGeometry == THRS_LOCAL_COUNT16 ||
+                        (opt.localGeometry != THRS_LOCAL_RANK16 && THRS_COUNT16_DEFAULT));
   const bool segTop = opt.segmented != THRS_SEG_NONE;
   const bool segA = opt.segmented == THRS_SEG_AUTO;
   // local16 with both top-digit passes segmented: the passes carry the keys
@@ -386,6 +397,8 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
         if constexpr (KT == 0 && VB == 0) {
           if (allow_lds(atomicRank ? thrs_local16<true, Loc16> : thrs_local16<false, Loc16>, Loc16::LDS) !=
                   hipSuccess ||
+              allow_lds(atomicRank ? thrs_local16<true, Loc16Wide> : thrs_local16<false, Loc16Wide>,
+                        Loc16Wide::LDS) != hipSuccess ||
               allow_lds(thrs_local_count16<true>, LocCount::LDS) != hipSuccess ||
               allow_lds(thrs_local_count16<false>, LocCount::LDS) != hipSuccess)
             return THRS_ERROR_HIP;
@@ -445,7 +458,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
       hipLaunchKernelGGL(thrs_hist_joint<KT>, dim3(hgrid), dim3(kHistThreads), kJointLds, stream,
                          static_cast<const U*>(keys), n, orderMask, startBits + 8 * nLow, vec, joint,
                          reinterpret_cast<uint32_t*>(hyb + kSegHistAOff), reinterpret_cast<uint32_t*>(hyb + kRowHistOff));
-      const uint32_t cap = kBucket64 ? Loc64::CAP : smallLocal ? LocSmall::CAP : LocBig::CAP;
+      const uint32_t cap = kBucket64 ? Loc64::CAP : smallLocal ? LocSmall::CAP : wide16 ? Loc16Wide::CAP : LocBig::CAP;
 #ifndef THRS_PLAN_ROWS
 #define THRS_PLAN_ROWS 1
 #endif
@@ -640,6 +653,11 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
             hipLaunchKernelGGL(lk, dim3(cgrid), dim3(LocCount::THREADS), LocCount::LDS, stream,
                                reinterpret_cast<uint32_t*>(K), n, (uint32_t)orderMask, chunkOff, chunkB0, meta,
                                static_cast<const uint16_t*>(lo2P), joint);
+          } else if (wide16) {
+            auto lk = atomicRank ? thrs_local16<true, Loc16Wide> : thrs_local16<false, Loc16Wide>;
+            hipLaunchKernelGGL(lk, dim3((uint32_t)maxChunks), dim3(Loc16Wide::THREADS), Loc16Wide::LDS, stream,
+                               reinterpret_cast<uint32_t*>(K), (uint32_t)orderMask, chunkOff, chunkB0, meta,
+                               planes ? static_cast<const uint16_t*>(lo2P) : nullptr);
           } else {
             auto lk = atomicRank ? thrs_local16<true, Loc16> : thrs_local16<false, Loc16>;
             hipLaunchKernelGGL(lk, dim3((uint32_t)maxChunks), dim3(Loc16::THREADS), Loc16::LDS, stream,
@@ -680,7 +698,7 @@ int run_vb(int vb, void* keys, void* vals, uint32_t n, void* tmp, void* ko, void
 
 bool valid_options(const thrs_options& o) {
   return o.path >= THRS_PATH_AUTO && o.path <= THRS_PATH_BUCKET && o.localGeometry >= THRS_LOCAL_AUTO &&
-         o.localGeometry <= THRS_LOCAL_RANK16 && o.segmented >= THRS_SEG_AUTO && o.segmented <= THRS_SEG_NONE &&
+         o.localGeometry <= THRS_LOCAL_WIDE16 && o.segmented >= THRS_SEG_AUTO && o.segmented <= THRS_SEG_NONE &&
          o.tileClaims >= THRS_CLAIMS_AUTO && o.tileClaims <= THRS_CLAIMS_TICKET && o.rank >= THRS_RANK_AUTO &&
          o.rank <= THRS_RANK_BALLOT && o.planes >= THRS_PLANES_AUTO && o.planes <= THRS_PLANES_OFF;
 }

@@ -962,6 +962,10 @@ template <int W, int K> struct Loc16G {
 };
 using Loc16 = Loc16G<8, 36>;
 static_assert(Loc16::CAP == LocBig::CAP, "same chunk capacity as the 32-bit geometry (thrs_plan's cap)");
+// 36864-key chunks (one 1024-thread workgroup per CU, 92 KiB of LDS): u32
+// keys-only sorts above 2^30 + 2^26, whose uniform buckets (n / 65536 keys,
+// up to ~34K at 2^31 + 2^27) outgrow Loc16's 18432 slots
+using Loc16Wide = Loc16G<16, 36>;
 
 template <bool ATOMIC_RANK, typename LG>
 __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(6))) void thrs_local16(uint32_t* __restrict__ keys, uint32_t orderMask,
@@ -1185,6 +1189,7 @@ __global__ __launch_bounds__(LocCount::THREADS) void thrs_local_count16(
 
   for (uint32_t i = tid; i < LC::WORDS / 4; i += LC::THREADS)
     reinterpret_cast<uint4*>(cnt)[i] = make_uint4(0, 0, 0, 0);
+  lds_barrier();  // every counter zero before the first chunk's adds
 
   // item k of thread tid = chunk position 1024k + tid (64 consecutive per wave)
   // (indices built from loop-variant bases: per-item constants hoisted out of
