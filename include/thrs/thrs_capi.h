@@ -74,7 +74,7 @@ typedef struct thrs_options {
                             u32 keys-only over the whole key, 18432-key chunks:
                             COUNT16 = counting sort of the 16-bit items, RANK16 =
                             two LSD rounds on them; WIDE16 = the same rounds in
-                            36864-key chunks (AUTO above 2^30 + 2^26, to 2^31 + 2^27) */
+                            34816-key chunks (AUTO above 2^30 + 2^26, to 2^31 + 2^25) */
   int32_t segmented;     /* THRS_SEG_*: XCD-segmented top-digit passes (AUTO: both)   */
   int32_t tileClaims;    /* THRS_CLAIMS_*: XCD-block tile claims in the digit passes
                             (AUTO: 4-byte keys without values, n >= 2^29)            */

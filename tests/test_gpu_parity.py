@@ -178,7 +178,7 @@ def test_hybrid_paths_vs_oracle(gpu, kt, desc, geom, seg):
     # the two top-digit passes XCD-segmented (default), neither, or the top one
     # only; local-sort geometry: 18432- or 9216-key chunks; u32 keys over the
     # whole key sort 16-bit items in the big geometry unless "big32" -- by two
-    # LSD rounds (default, "rank16") or by counting ("count16"), or in 36864-key
+    # LSD rounds (default, "rank16") or by counting ("count16"), or in 34816-key
     # chunks ("wide16", the default above 2^30 + 2^26); u32 keys
     # there travel as u16/u8 planes through the top-digit passes unless
     # "noplanes" (thrs_options.planes)

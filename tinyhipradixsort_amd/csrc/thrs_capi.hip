@@ -63,7 +63,7 @@ inline uint64_t tile_keys(int kb, int vb) {
 }
 
 #ifndef THRS_WIDE16_AUTO
-#define THRS_WIDE16_AUTO 1  // AUTO takes the bucket path (wide 16-bit local sort) for u32 keys-only up to 2^31 + 2^27
+#define THRS_WIDE16_AUTO 1  // AUTO takes the bucket path (wide 16-bit local sort) for u32 keys-only up to 2^31 + 2^25
 #endif
 #ifndef THRS_COUNT16_DEFAULT
 // u32 keys-only local sort over 16-bit items: 1 = counting (thrs_local_count16)
@@ -323,10 +323,10 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   // (8-byte keys: one 17408-slot chunk per bucket, so up to 2^30 + 2^24: the
   // largest uniform bucket stays ~3 sigma below the capacity)
   const bool sizeOk = nn >= (1ull << 28) && nn <= (1ull << 30) + (sizeof(U) == 8 ? (1ull << 24) : (1ull << 26));
-  // u32 keys without values over the whole key: up to 2^31 + 2^27 with the
-  // wide 16-bit local sort (Loc16Wide: 36864-key chunks)
+  // u32 keys without values over the whole key: up to 2^31 + 2^25 with the
+  // wide 16-bit local sort (Loc16Wide: 34816-key chunks)
   const bool wideOk = THRS_WIDE16_AUTO && KT == 0 && VB == 0 && fullWindow && nn > (1ull << 30) + (1ull << 26) &&
-                      nn <= (1ull << 31) + (1ull << 27);
+                      nn <= (1ull << 31) + (1ull << 25);
   const bool smallLocal = opt.localGeometry == THRS_LOCAL_SMALL ? true
                           : opt.localGeometry != THRS_LOCAL_AUTO  // BIG, BIG32 and the 16-bit kernels
                               ? false
@@ -340,7 +340,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   const bool local16 = bucket && KT == 0 && VB == 0 && fullWindow && !smallLocal &&
                        opt.localGeometry != THRS_LOCAL_BIG32;
   // ... sorted by counting (thrs_local_count16) or by two LSD rounds (thrs_local16)
-  // ... in 36864-key chunks (explicitly, or by default above 2^30 + 2^26)
+  // ... in 34816-key chunks (explicitly, or by default above 2^30 + 2^26)
   const bool wide16 = local16 && (opt.localGeometry == THRS_LOCAL_WIDE16 ||
                                   (opt.localGeometry == THRS_LOCAL_AUTO && nn > (1ull << 30) + (1ull << 26)));
   const bool count16 = local16 && !wide16 &&

@@ -952,8 +952,8 @@ __global__ __launch_bounds__(LG::THREADS) void thrs_local(typename KeyTraits<KT>
 // at (s / 64) * 66 + s % 64.  Structured inputs scatter with regular strides
 // (sorted keys: a wave's 64 slots ~288 apart, all on 2 of the 32 store banks);
 // the pad spreads them.  A wave's 64 consecutive slots stay contiguous.
-template <int W, int K> struct Loc16G {
-  static constexpr int WAVES = W, KPT = K, THREADS = 64 * W, NP = (K + 1) / 2;
+template <int W, int K, int WPE_ = 6, int LB_ = K> struct Loc16G {
+  static constexpr int WAVES = W, KPT = K, THREADS = 64 * W, NP = (K + 1) / 2, WPE = WPE_, LB = LB_;
   static constexpr uint32_t CAP = (uint32_t)THREADS * K;
   static constexpr uint32_t ROW = 66;                                // u16 slots per 64 items
   static constexpr size_t STAGE_BYTES = (size_t)(CAP / 64) * ROW * 2;
@@ -962,13 +962,21 @@ template <int W, int K> struct Loc16G {
 };
 using Loc16 = Loc16G<8, 36>;
 static_assert(Loc16::CAP == LocBig::CAP, "same chunk capacity as the 32-bit geometry (thrs_plan's cap)");
-// 36864-key chunks (one 1024-thread workgroup per CU, 92 KiB of LDS): u32
-// keys-only sorts above 2^30 + 2^26, whose uniform buckets (n / 65536 keys,
-// up to ~34K at 2^31 + 2^27) outgrow Loc16's 18432 slots
-using Loc16Wide = Loc16G<16, 36>;
+// Wide chunks for u32 keys-only sorts above 2^30 + 2^26, whose uniform
+// buckets (n / 65536 keys) outgrow Loc16's 18432 slots: 34816 keys (8 waves x
+// 68 items, 79.8 KiB of LDS: two workgroups per CU, which overlap their
+// rounds; up to ~2^31 + 2^25, where the largest of 65536 uniform buckets is
+// ~4.5 sigma below the capacity)
+#ifndef THRS_WIDE_K
+#define THRS_WIDE_K 68
+#endif
+#ifndef THRS_WIDE_W
+#define THRS_WIDE_W 8
+#endif
+using Loc16Wide = Loc16G<THRS_WIDE_W, THRS_WIDE_K, 4, THRS_WIDE_K / 2>;
 
 template <bool ATOMIC_RANK, typename LG>
-__global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(6))) void thrs_local16(uint32_t* __restrict__ keys, uint32_t orderMask,
+__global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(LG::WPE))) void thrs_local16(uint32_t* __restrict__ keys, uint32_t orderMask,
                                                             const uint32_t* __restrict__ chunkOff,
                                                             const uint32_t* __restrict__ chunkB0,
                                                             const uint32_t* __restrict__ meta,
@@ -1001,23 +1009,35 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(6))
   // u16 plane lo (kCodecPlanes) -- unless both were skipped (mode 2: one
   // bucket holds every key), which leaves the keys in place
   uint32_t it[NP];
+  // (in batches of LB items: a wide geometry's raw loads would not fit the
+  // register budget at once)
+  constexpr int LB = LG::LB;
+  static_assert(KPT % LB == 0 && LB % 2 == 0, "load batches hold whole item pairs");
   if (lo && meta[kMetaMode] == 0) {
-    uint16_t raw[KPT];
-    load_run<KPT>(raw, lo + start, w * CHUNK + lane, size, limw);
 #pragma unroll
-    for (int j = 0; j < KPT; j += 2) {
-      const uint32_t a = (j * 64 < lim) ? (uint32_t)raw[j] : 0xFFFFu;
-      const uint32_t b = (j + 1 < KPT && (j + 1) * 64 < lim) ? (uint32_t)raw[j + 1] : 0xFFFFu;
-      it[j >> 1] = a | (b << 16);
+    for (int h = 0; h < KPT; h += LB) {
+      uint16_t raw[LB];
+      load_run<LB>(raw, lo + start, w * CHUNK + h * 64 + lane, size, limw - h * 64);
+#pragma unroll
+      for (int jj = 0; jj < LB; jj += 2) {
+        const int j = h + jj;
+        const uint32_t a = (j * 64 < lim) ? (uint32_t)raw[jj] : 0xFFFFu;
+        const uint32_t b = (j + 1 < KPT && (j + 1) * 64 < lim) ? (uint32_t)raw[jj + 1] : 0xFFFFu;
+        it[j >> 1] = a | (b << 16);
+      }
     }
   } else {
-    uint32_t raw[KPT];
-    load_run<KPT>(raw, keys + start, w * CHUNK + lane, size, limw);
 #pragma unroll
-    for (int j = 0; j < KPT; j += 2) {
-      const uint32_t a = (j * 64 < lim) ? ((raw[j] ^ orderMask) & 0xFFFFu) : 0xFFFFu;
-      const uint32_t b = (j + 1 < KPT && (j + 1) * 64 < lim) ? ((raw[j + 1] ^ orderMask) & 0xFFFFu) : 0xFFFFu;
-      it[j >> 1] = a | (b << 16);
+    for (int h = 0; h < KPT; h += LB) {
+      uint32_t raw[LB];
+      load_run<LB>(raw, keys + start, w * CHUNK + h * 64 + lane, size, limw - h * 64);
+#pragma unroll
+      for (int jj = 0; jj < LB; jj += 2) {
+        const int j = h + jj;
+        const uint32_t a = (j * 64 < lim) ? ((raw[jj] ^ orderMask) & 0xFFFFu) : 0xFFFFu;
+        const uint32_t b = (j + 1 < KPT && (j + 1) * 64 < lim) ? ((raw[jj + 1] ^ orderMask) & 0xFFFFu) : 0xFFFFu;
+        it[j >> 1] = a | (b << 16);
+      }
     }
   }
   auto item = [&](int j) -> uint32_t { return (it[j >> 1] >> ((j & 1) * 16)) & 0xFFFFu; };
@@ -1106,12 +1126,15 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(6))
   }
   // every stage read first (in bounds for all lanes), then the lane-conditional
   // stores: a read inside the condition would be waited for one at a time
-  uint32_t o[KPT];
 #pragma unroll
-  for (int j = 0; j < KPT; ++j) o[j] = stw[j * LG::ROW];
+  for (int h = 0; h < KPT; h += LB) {
+    uint32_t o[LB];
 #pragma unroll
-  for (int j = 0; j < KPT; ++j)
-    if (j * 64 < lim) src[j * 64] = (hiBits | o[j]) ^ orderMask;
+    for (int jj = 0; jj < LB; ++jj) o[jj] = stw[(h + jj) * LG::ROW];
+#pragma unroll
+    for (int jj = 0; jj < LB; ++jj)
+      if ((h + jj) * 64 < lim) src[(h + jj) * 64] = (hiBits | o[jj]) ^ orderMask;
+  }
 }
 
 // ------------------------------------------- local sort, counting (keys only)
