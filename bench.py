@@ -47,6 +47,7 @@ WORKLOADS = {
     "c4": (2, 0, 1 << 28, "uniform", "C4: sortKeys f32 via fpKey transform, N=2^28 (bits & 0xFF7FFFFF)"),
     "c5": (1, 8, 1 << 30, "uniform", "C5: sortPairs u64 key + u64 index payload, 2^30 per GPU"),
     "u64k": (1, 0, 1 << 30, "uniform", "sortKeys u64, N=2^30 uniform (64-bit keys without payload)"),
+    "u32large": (0, 0, (1 << 31) + 100, "uniform", "u32Large: sortKeys u32, N=2^31+100 uniform (unittest.cpp:688-717)"),
     # low-entropy inputs of C2's shape (not bench lines of BASELINE.json: robustness)
     "c2_sorted": (0, 0, 1 << 30, "sorted", "C2 shape, already-sorted input (stratified sorted uniform sample)"),
     "c2_reverse": (0, 0, 1 << 30, "reverse", "C2 shape, reverse-sorted input"),
@@ -369,7 +370,8 @@ def main():
         if args.vendor == "auto" and world == 1:
             del keys_in0
             vendor = vendor_bench(T, TU, kt, kb, vb, n, keys, vals, gen, stream)
-        if args.ref_gpu == "auto" and world == 1 and dist_kind == "uniform":
+        # (the reference's kernels index with 32-bit ints: up to 2^30 keys here)
+        if args.ref_gpu == "auto" and world == 1 and dist_kind == "uniform" and n <= (1 << 30):
             ref_gpu = reference_gpu_bench(TU, kt, kb, vb, n, keys, vals, gen, stream)
         recycled = False
         elapsed = t1 - t0
