@@ -134,6 +134,19 @@ def test_rank_probe_and_ballot_fallback(gpu):
     assert r.returncode == 0, r.stdout[-3000:]
 
 
+def test_rank_order_partial_waves(gpu):
+    """The atomic rank is only ever issued by fully active waves (padding
+    items are ranked too), which is what thrs_probe_lds_order certifies.  This
+    records whether the lane order also holds under partial exec masks, so a
+    future partial-wave use is not relying on an unmeasured property."""
+    from tinyhipradixsort_amd import testutil as TU
+    import tinyhipradixsort_amd as T
+    bad = TU.probe_lds_order_partial(64)
+    print("partial-mask lane-order violations:", bad)
+    if T.lib().thrs_rank_mode() == 1:
+        assert bad == 0, f"{bad} lanes out of order under partial exec masks"
+
+
 def test_cpp_port_of_reference_unittest(gpu):
     """The reference's UTEST matrix, ported to C++ against the drop-in header."""
     exe = os.path.join(ROOT, "tests", "cpp", "unittest_thrs")

@@ -183,6 +183,42 @@ __global__ void k_copy_u128(uint4* __restrict__ dst, const uint4* __restrict__ s
     dst[i] = src[i];
 }
 
+// The rank's lane-order property under PARTIAL exec masks (thrs_probe_lds_order
+// checks fully active waves only, which is all the product kernels issue:
+// their rank loops run whole waves, padding items included).  Same digit
+// patterns, with 4 lane subsets active: odd lanes, lanes < 40, a random mask,
+// lanes not divisible by 3.  *bad counts disagreeing active lanes.
+__global__ __launch_bounds__(256) void k_probe_partial(uint32_t* bad, int iters) {
+  __shared__ uint32_t cnt[4][kBins];
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t b = 0;
+  uint64_t x = (blockIdx.x * 256ull + threadIdx.x + 1) * 0x9E3779B97F4A7C15ull;
+  for (int it = 0; it < iters; ++it) {
+    for (uint32_t i = lane; i < (uint32_t)kBins; i += 64) cnt[w][i] = (uint32_t)it;
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    x ^= x >> 31;
+    x *= 0xBF58476D1CE4E5B9ull;
+    x ^= x >> 29;
+    uint32_t d = (uint32_t)(x >> 24) & 0xFFu;
+    const int mode = it & 3, pm = (it >> 2) & 3;
+    if (mode == 1) d &= 0x3u;
+    if (mode == 2) d = 0x5Au;
+    if (mode == 3) d &= 0x1Fu;
+    const bool act = pm == 0 ? (lane & 1u) != 0 : pm == 1 ? lane < 40u : pm == 2 ? ((x >> 40) & 1u) != 0 : (lane % 3u) != 0;
+    if (act) {
+      uint32_t mlo, mhi;
+      match_digit(d, mlo, mhi);
+      const uint64_t ex = __ballot(1);  // inactive lanes read as digit 0 in the ballots: mask them out
+      mlo &= (uint32_t)ex;
+      mhi &= (uint32_t)(ex >> 32);
+      const uint32_t want = (uint32_t)it + __builtin_amdgcn_mbcnt_hi(mhi, __builtin_amdgcn_mbcnt_lo(mlo, 0u));
+      const uint32_t got = __hip_atomic_fetch_add(&cnt[w][d], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      b += got != want;
+    }
+  }
+  if (b) atomicAdd(bad, b);
+}
+
 inline int grid_for(uint64_t n) {
   uint64_t g = (n + 255) / 256;
   if (g > 8192) g = 8192;
@@ -257,6 +293,18 @@ THRS_API int thrsu_check_pairs(int keyType, int desc, int valueBytes, const void
                        vals, n, startBits, endBits, d);
   (void)hipMemcpyAsync(result5, d, 40, hipMemcpyDeviceToHost, stream);
   int rc = ok(hipStreamSynchronize(stream));
+  (void)hipFree(d);
+  return rc;
+}
+
+// disagreeing lanes of the partial-mask lane-order probe (synchronising)
+THRS_API int thrsu_probe_lds_order_partial(int iters, unsigned int* bad) {
+  uint32_t* d = nullptr;
+  if (hipMalloc(&d, 4) != hipSuccess) return THRS_ERROR_HIP;
+  (void)hipMemset(d, 0, 4);
+  hipLaunchKernelGGL(k_probe_partial, dim3(256), dim3(256), 0, 0, d, iters);
+  int rc = ok(hipGetLastError());
+  if (rc == THRS_SUCCESS) rc = ok(hipMemcpy(bad, d, 4, hipMemcpyDeviceToHost));
   (void)hipFree(d);
   return rc;
 }

@@ -25,7 +25,8 @@ def tlib() -> ctypes.CDLL:
         L.thrsu_fingerprint.argtypes = [i32, vp, u64, ull_p, vp]
         L.thrsu_check_pairs.argtypes = [i32, i32, i32, vp, vp, vp, u64, i32, i32, ull_p, vp]
         L.thrsu_copy.argtypes = [vp, vp, u64, i32, vp]
-        for f in ("thrsu_copy", "thrsu_fill_keys", "thrsu_fill_dist", "thrsu_iota", "thrsu_check_sorted", "thrsu_fingerprint", "thrsu_check_pairs"):
+        L.thrsu_probe_lds_order_partial.argtypes = [i32, ctypes.POINTER(ctypes.c_uint)]
+        for f in ("thrsu_probe_lds_order_partial", "thrsu_copy", "thrsu_fill_keys", "thrsu_fill_dist", "thrsu_iota", "thrsu_check_sorted", "thrsu_fingerprint", "thrsu_check_pairs"):
             getattr(L, f).restype = i32
         _tl = L
     return _tl
@@ -93,3 +94,11 @@ def expected_index_fingerprint(n: int) -> tuple[int, int]:
 def copy(dst, src, nbytes: int, width16: bool = True, stream=None):
     """Streaming copy with 16-B (or 4-B) lanes: rocprofv3 byte-counter calibration."""
     _check(tlib().thrsu_copy(_ptr(dst), _ptr(src), nbytes, int(width16), _stream(stream)))
+
+
+def probe_lds_order_partial(iters: int = 64) -> int:
+    """Lanes whose LDS-atomic return broke lane order under a partial exec mask
+    (thrs_testutil.hip k_probe_partial); 0 = ordered on this device."""
+    bad = ctypes.c_uint(0)
+    _check(tlib().thrsu_probe_lds_order_partial(iters, ctypes.byref(bad)))
+    return int(bad.value)
