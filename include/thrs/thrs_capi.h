@@ -28,7 +28,7 @@ extern "C" {
 typedef struct ihipStream_t* hipStream_t; /* identical to HIP's own typedef */
 #endif
 
-#define THRS_ABI_VERSION 2
+#define THRS_ABI_VERSION 3
 
 typedef enum thrs_status {
   THRS_SUCCESS = 0,
@@ -158,16 +158,25 @@ int thrs_digit_histogram(const thrs_config* config, const void* keys, uint32_t n
 
 /* Device-side failures (no reference counterpart; the reference would hang
  * where these give up).  A look-back or tile-claim wait is bounded; when the
- * bound is hit the sort's output is wrong and the failure is recorded twice:
- *   - in `temporaryBuffer` (until its next sort):
- *     thrs_check_device_error synchronises `stream` and returns
- *     THRS_ERROR_LOOKBACK_TIMEOUT if the last sort on it failed;
- *   - in a per-device sticky word in host memory, which the NEXT thrs_sort_*
- *     call on that device reports (and clears) before doing anything:
- *     THRS_ERROR_LOOKBACK_TIMEOUT, without a synchronisation.
- * thrs_take_device_error reads and clears the sticky word without sorting
- * (non-blocking: it sees failures of sorts that have finished). */
+ * bound is hit the sort's output is wrong and the failure is recorded in the
+ * sort's own `temporaryBuffer` (until the next sort that uses it), and ORed
+ * into a per-device sticky word in host memory.  A sort never fails because
+ * of an EARLIER sort: each caller checks its own sort, either way below.
+ *   thrs_check_device_error         synchronises `stream`; returns
+ *                                   THRS_ERROR_LOOKBACK_TIMEOUT if the last sort
+ *                                   on `temporaryBuffer` failed;
+ *   thrs_accumulate_device_error    stream-ordered, no synchronisation:
+ *                                   *acc |= that sort's error word (device
+ *                                   memory, u32), so a sequence of sorts on one
+ *                                   temporary buffer (the multi-GPU exchange)
+ *                                   is checked once at its end;
+ *   thrs_take_device_error          reads and clears the DEVICE-WIDE sticky
+ *                                   word (non-blocking: it sees failures of
+ *                                   sorts that have finished, on any stream or
+ *                                   thread -- including ones already reported
+ *                                   through their temporary buffer). */
 int thrs_check_device_error(void* temporaryBuffer, hipStream_t stream);
+int thrs_accumulate_device_error(const void* temporaryBuffer, uint32_t* acc, hipStream_t stream);
 int thrs_take_device_error(void);
 
 /* Kernel timing for benchmarks (no reference counterpart; the reference's

@@ -16,8 +16,9 @@
 // and tuning choices, thrs_options; defaults = the library's choice), and
 // THRS_CHECKED: defined before including this header, every sortKeys /
 // sortPairs synchronises its stream and throws (aborts) on a device-side
-// failure of that sort (thrs_check_device_error) -- without it such a failure
-// is reported by the next sort on the device (thrs_capi.h).
+// failure of that sort (thrs_check_device_error) -- without it the caller
+// checks a sort with checkDeviceError(temporaryBuffer, stream) (thrs_capi.h,
+// "Device-side failures"); a sort never fails because of an earlier one.
 //
 // What changed underneath: no Orochi and no hipRTC.  Every call goes through
 // the C-ABI of libthrs.so (<thrs/thrs_capi.h>), whose kernels are compiled

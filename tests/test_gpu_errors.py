@@ -1,12 +1,18 @@
-"""Device-side failures reach the caller (thrs_capi.h "Device-side failures";
-the reference's THRS_ASSERT, tinyhipradixsort.hpp:14-15, fails loudly).
+"""Device-side failures reach the caller of the failing sort (thrs_capi.h
+"Device-side failures"; the reference's THRS_ASSERT, tinyhipradixsort.hpp:14-15,
+fails loudly), and only that caller.
 
 libthrs_spin0.so is the library built with THRS_SPIN_MAX=0: every look-back
-or tile-claim wait gives up at once, so a large sort fails on the device.
-The failure must surface (a) through checkDeviceError on its temporary
-buffer, (b) as the error of the NEXT sort call on the device, without a
-synchronisation, and (c) through take_device_error -- and the normal library
-must report nothing."""
+or tile-claim wait gives up at once, so a large sort fails on the device
+while a one-tile sort (no wait) succeeds.  The failure must surface
+  (a) through checkDeviceError on the failing sort's temporary buffer,
+  (b) through sortKeys(..., checked=True) of the failing sort itself,
+  (c) through accumulateDeviceError into a caller word (stream-ordered),
+  (d) through take_device_error (device-wide sticky word),
+and (e) an unrelated sort issued after the failure, on another temporary
+buffer, must run and succeed.  The normal library reports nothing.  A first
+sort issued inside a stream capture (the sticky word is not set up there)
+must not disable later sorts (init retried after it is skipped)."""
 import os
 import subprocess
 import sys
@@ -27,48 +33,90 @@ rs = T.RadixSort([], T.RadixSort.Config())
 n = 1 << 24
 keys = torch.empty(4 * n, dtype=torch.uint8, device="cuda")
 tmp = torch.empty(rs.getTemporaryBufferBytes(n).getTemporaryBufferBytesForSortKeys(), dtype=torch.uint8, device="cuda")
-small = torch.zeros(4 * 1000, dtype=torch.uint8, device="cuda")
-res = {{"check": 0, "next": 0, "take": 0, "clean_after": 1}}
-for attempt in range(8):
+m = 1000
+small = torch.empty(4 * m, dtype=torch.uint8, device="cuda")
+tmp2 = torch.empty(rs.getTemporaryBufferBytes(m).getTemporaryBufferBytesForSortKeys(), dtype=torch.uint8, device="cuda")
+acc = torch.zeros(1, dtype=torch.int32, device="cuda")
+res = dict(check=0, checked=0, acc=0, take=0, other_ok=0, other_bad=0, attempts=6)
+for attempt in range(res["attempts"]):
     TU.fill_keys(0, keys, n, start=attempt * n)
-    rs.sortKeys(keys, n, tmp, 0, 32)
-    torch.cuda.synchronize()
     try:
-        rs.sortKeys(small, 1000, tmp, 0, 32)   # must report the earlier failure
+        rs.sortKeys(keys, n, tmp, 0, 32, checked=True)                # (b)
     except T.ThrsError as e:
-        res["next"] += e.status == -5
-        continue
+        res["checked"] += e.status == -5
     try:
-        rs.checkDeviceError(tmp)
+        rs.checkDeviceError(tmp)                                     # (a)
     except T.ThrsError as e:
         res["check"] += e.status == -5
-# after a reported failure the sticky word is clear: a tiny sort (one tile, no wait) succeeds
-try:
-    rs.sortKeys(small, 1000, tmp, 0, 32)
+    acc.zero_()
+    rs.accumulateDeviceError(tmp, acc)                               # (c)
     torch.cuda.synchronize()
-    T.take_device_error()
-except T.ThrsError:
-    res["clean_after"] = 0
+    res["acc"] += int(acc.item()) != 0
+    try:
+        T.take_device_error()                                        # (d)
+    except T.ThrsError as e:
+        res["take"] += e.status == -5
+    TU.fill_keys(0, small, m, start=attempt)                         # (e) an unrelated sort still runs
+    try:
+        rs.sortKeys(small, m, tmp2, 0, 32, checked=True)
+        res["other_ok"] += TU.count_unsorted(0, small, m, 0, 32) == 0
+    except T.ThrsError:
+        res["other_bad"] += 1
 print(res)
 """
 
+CAPTURE = r"""
+import sys, torch
+sys.path.insert(0, {root!r})
+import tinyhipradixsort_amd as T
+from tinyhipradixsort_amd import testutil as TU
+torch.cuda.set_device(0)
+rs = T.RadixSort([], T.RadixSort.Config())
+n = 100003
+keys = torch.empty(4 * n, dtype=torch.uint8, device="cuda")
+tmp = torch.empty(rs.getTemporaryBufferBytes(n).getTemporaryBufferBytesForSortKeys(), dtype=torch.uint8, device="cuda")
+TU.fill_keys(0, keys, n, start=0)
+torch.cuda.synchronize()
+s = torch.cuda.Stream()
+g = torch.cuda.CUDAGraph()
+with torch.cuda.graph(g, stream=s):            # the library's FIRST call in this process is captured
+    rs.sortKeys(keys, n, tmp, 0, 32, stream=s)
+g.replay()
+torch.cuda.synchronize()
+ok_graph = TU.count_unsorted(0, keys, n, 0, 32) == 0
+TU.fill_keys(0, keys, n, start=n)
+rs.sortKeys(keys, n, tmp, 0, 32, checked=True)  # outside the capture: runs and publishes normally
+ok_after = TU.count_unsorted(0, keys, n, 0, 32) == 0
+T.take_device_error()
+print(dict(graph=ok_graph, after=ok_after))
+"""
 
-def _run(lib):
-    code = SCRIPT.format(root=ROOT, lib=lib)
+
+def _run(code):
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     return eval(r.stdout.strip().splitlines()[-1])
 
 
-def test_forced_timeout_is_reported():
+def test_forced_timeout_is_reported_to_its_own_caller():
     lib = os.path.join(ROOT, "tinyhipradixsort_amd", "libthrs_spin0.so")
     assert os.path.exists(lib), "build it first (make)"
-    res = _run(lib)
+    res = _run(SCRIPT.format(root=ROOT, lib=lib))
     print(res)
-    assert res["next"] >= 1, res           # the next call on the device raised
-    assert res["clean_after"] == 1, res
+    k = res["attempts"]
+    # the 2^24-key sort fails with no spinning allowed (1024 tiles: in practice
+    # every attempt); each failure is seen by all four reports of that sort
+    assert res["checked"] >= 1, res
+    assert res["check"] == res["checked"] == res["acc"] == res["take"], res
+    assert res["other_ok"] == k and res["other_bad"] == 0, res
 
 
 def test_normal_library_reports_nothing():
-    res = _run(os.path.join(ROOT, "tinyhipradixsort_amd", "libthrs.so"))
-    assert res == {"check": 0, "next": 0, "take": 0, "clean_after": 1}, res
+    res = _run(SCRIPT.format(root=ROOT, lib=os.path.join(ROOT, "tinyhipradixsort_amd", "libthrs.so")))
+    k = res["attempts"]
+    assert res == dict(check=0, checked=0, acc=0, take=0, other_ok=k, other_bad=0, attempts=k), res
+
+
+def test_first_sort_under_stream_capture():
+    res = _run(CAPTURE.format(root=ROOT))
+    assert res == {"graph": True, "after": True}, res

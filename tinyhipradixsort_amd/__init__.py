@@ -31,7 +31,7 @@ from dataclasses import dataclass
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libthrs.so")
 TESTUTIL_PATH = os.path.join(_HERE, "libthrs_testutil.so")
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 __all__ = ["KeyType", "ValueType", "SortOrder", "bytesOf", "div_round_up64", "next_multiple64", "Buffer",
            "RadixSort", "Options", "ThrsError", "lib", "LIB_PATH", "take_device_error"]
@@ -72,6 +72,7 @@ def lib() -> ctypes.CDLL:
         L.thrs_digit_histogram.argtypes = [ctypes.POINTER(_CConfig), vp, u32, u64, u64, i32, vp, vp]
         L.thrs_digit_histogram.restype = i32
         L.thrs_check_device_error.argtypes = [vp, vp]
+        L.thrs_accumulate_device_error.argtypes = [vp, vp, vp]
         L.thrs_partition_pass.argtypes = [ctypes.POINTER(_CConfig), vp, vp, u32, vp, vp, vp, i32, vp, vp]
         L.thrs_malloc.argtypes = [ctypes.POINTER(vp), i64]
         L.thrs_free.argtypes = [vp]
@@ -88,7 +89,8 @@ def lib() -> ctypes.CDLL:
         L.thrs_rank_mode.restype = i32
         for f in ("thrs_profile_enable", "thrs_profile_read", "thrs_profile_read_kind",
                   "thrs_get_temporary_buffer_bytes", "thrs_sort_keys", "thrs_sort_pairs", "thrs_sort_keys_ex",
-                  "thrs_sort_pairs_ex", "thrs_check_device_error", "thrs_partition_pass",
+                  "thrs_sort_pairs_ex", "thrs_check_device_error", "thrs_accumulate_device_error",
+                  "thrs_partition_pass",
                   "thrs_malloc", "thrs_free", "thrs_memcpy_htod_async", "thrs_memcpy_dtoh", "thrs_memcpy_dtod_async",
                   "thrs_stream_create", "thrs_stream_destroy", "thrs_stream_synchronize"):
             getattr(L, f).restype = i32
@@ -142,7 +144,8 @@ class Options:
 
 def take_device_error():
     """Raise (and clear) a device-side failure of any earlier sort on the
-    current device that has finished (thrs_take_device_error; non-blocking)."""
+    current device that has finished, on any stream or thread
+    (thrs_take_device_error; non-blocking, device-wide)."""
     _check(lib().thrs_take_device_error())
 
 
@@ -329,16 +332,26 @@ class RadixSort:
         return RadixSort.TemporaryBufferDef(d.pSumBuffer, d.keyOutBuffer, d.valueOutBuffer)
 
     def sortKeys(self, inputKeyBuffer, numberOfInputs: int, temporaryBuffer, startBits: int, endBits: int,
-                 stream=None):
+                 stream=None, checked: bool = False):
+        """hpp:845.  Asynchronous on `stream`; checked=True synchronises it and
+        raises this sort's own device-side failure (THRS_CHECKED in the C++
+        header)."""
+        s = _stream(stream)
         _check(lib().thrs_sort_keys_ex(ctypes.byref(self._c()), ctypes.byref(self.options._c()),
                                        _ptr(inputKeyBuffer), _n(numberOfInputs), _ptr(temporaryBuffer),
-                                       int(startBits), int(endBits), _stream(stream)))
+                                       int(startBits), int(endBits), s))
+        if checked:
+            _check(lib().thrs_check_device_error(_ptr(temporaryBuffer), s))
 
     def sortPairs(self, inputKeyBuffer, inputValueBuffer, numberOfInputs: int, temporaryBuffer, startBits: int,
-                  endBits: int, stream=None):
+                  endBits: int, stream=None, checked: bool = False):
+        """hpp:849.  As sortKeys."""
+        s = _stream(stream)
         _check(lib().thrs_sort_pairs_ex(ctypes.byref(self._c()), ctypes.byref(self.options._c()),
                                         _ptr(inputKeyBuffer), _ptr(inputValueBuffer), _n(numberOfInputs),
-                                        _ptr(temporaryBuffer), int(startBits), int(endBits), _stream(stream)))
+                                        _ptr(temporaryBuffer), int(startBits), int(endBits), s))
+        if checked:
+            _check(lib().thrs_check_device_error(_ptr(temporaryBuffer), s))
 
     def partitionPass(self, inputKeyBuffer, inputValueBuffer, numberOfInputs: int, temporaryBuffer, outputKeyBuffer,
                       outputValueBuffer, bitLocation: int, counts, stream=None):
@@ -359,8 +372,14 @@ class RadixSort:
                                           int(bitLocation), _ptr(counts), _stream(stream)))
 
     def checkDeviceError(self, temporaryBuffer, stream=None):
-        """Synchronising: raises if a look-back spin bound was hit in the last sort."""
+        """Synchronising: raises if a look-back spin bound was hit in the last
+        sort on temporaryBuffer."""
         _check(lib().thrs_check_device_error(_ptr(temporaryBuffer), _stream(stream)))
+
+    def accumulateDeviceError(self, temporaryBuffer, acc, stream=None):
+        """Stream-ordered, no synchronisation: acc (device u32) |= the error
+        word of the last sort on temporaryBuffer (thrs_accumulate_device_error)."""
+        _check(lib().thrs_accumulate_device_error(_ptr(temporaryBuffer), _ptr(acc), _stream(stream)))
 
 
 def profile_enable(on: bool = True):

@@ -1,0 +1,593 @@
+// thrs_host.hpp -- host side of libthrs.so shared by its translation units:
+// temporary-buffer layout, the launch plan and the launch sequence (run_sort)
+// for one key type.  The sequence is instantiated per key type in
+// thrs_run.hip (compiled once per key type, in parallel); thrs_capi.hip holds
+// the C-ABI and the process-wide state (profiling events, rank probe, error
+// words).
+//
+// The pass loop follows RadixSort::sort (tinyhipradixsort.hpp:854-944): one
+// pass per bitLocation = startBits + 8i < endBits, ping-pong between the
+// caller's buffers and the keyOut/valueOut regions of the temporary buffer,
+// and a copy-back when the pass count is odd so the result always lands in the
+// caller's buffers.  Differences, all deliberate:
+//   * one histogram launch for all passes + one tiny scan, then ONE launch per
+//     pass (the reference launches blockCount + prefixSumExclusiveInplace +
+//     reorder per pass, :872-922);
+//   * the odd-pass copy is stream-ordered (hipMemcpyAsync on `stream`); the
+//     reference's oroMemcpyDtoD (:938-941) is not;
+//   * a pass whose bit location is at or past the key width reads only zero
+//     bits, is the identity permutation, and is skipped;
+//   * errors are returned, never __debugbreak (:14-15).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+
+#include "thrs/thrs_capi.h"
+#include "thrs_kernels.hpp"
+#include "thrs_hybrid.hpp"
+
+namespace thrs_host {
+using namespace thrs_dev;
+
+constexpr uint64_t kAlign = 256;
+constexpr uint64_t kHistOff = 0;                       // u32 [8][256]
+constexpr uint64_t kBaseOff = 8 * 256 * 4;             // u32 [8][256]
+constexpr uint64_t kCounterOff = 2 * 8 * 256 * 4;      // u32 [8]
+constexpr uint64_t kErrOff = kCounterOff + 8 * 4;      // u32
+constexpr uint64_t kHeaderBytes = 16640;               // 65 * 256
+
+inline uint64_t round_up(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
+constexpr uint64_t round_up_c(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
+
+inline bool valid_key(int k) { return k >= THRS_KEY_U32 && k <= THRS_KEY_F64; }
+inline bool valid_value(int v) { return v >= THRS_VALUE_U32 && v <= THRS_VALUE_U128; }
+inline int key_bytes_of(int k) { return (k == THRS_KEY_U32 || k == THRS_KEY_F32) ? 4 : 8; }
+inline int value_bytes_of(int v) { return v == THRS_VALUE_U32 ? 4 : v == THRS_VALUE_U64 ? 8 : 16; }
+
+// keys per tile of the pass kernel, per (key bytes, value bytes) -- PassCfg in
+// thrs_kernels.hpp
+inline uint64_t tile_keys(int kb, int vb) {
+  switch (kb * 100 + vb) {
+    case 400: return PassGeom<4, 0>::TILE;
+    case 404: return PassGeom<4, 4>::TILE;
+    case 408: return PassGeom<4, 8>::TILE;
+    case 416: return PassGeom<4, 16>::TILE;
+    case 800: return PassGeom<8, 0>::TILE;
+    case 804: return PassGeom<8, 4>::TILE;
+    case 808: return PassGeom<8, 8>::TILE;
+    default: return PassGeom<8, 16>::TILE;
+  }
+}
+
+
+struct Plan {
+  int kb, vb;         // key / value bytes (vb = 0 for sortKeys)
+  uint64_t tileKeys;  // keys per tile of the pass kernel
+  uint64_t nTiles;
+  bool wideStatus;    // 64-bit look-back words (n >= 2^31)
+  uint64_t statusBytes;   // per-tile rows [nTiles][256]
+  uint64_t gaBytes;       // group aggregates [nGroups][256] u32 (kGroup > 0)
+  uint64_t gpBytes;       // group prefixes   [nGroups][256] status words
+  uint64_t setBytes;      // one look-back table set = status + ga + gp
+  uint64_t claimBytes;    // per pass: XCD-block claim state (tickets, block counter, 8 block tables)
+  uint64_t hybridOff;     // 3-pass path (thrs_hybrid.hpp): bucket histogram, chunk table, meta
+  uint64_t hiPlaneOff;    // u32 keys without values: the bucket path's u8 plane (n bytes)
+  uint64_t scratchBytes;  // header + 2 sets (ping-pong between passes) + 8 claim areas + hybrid area [+ u8 plane]
+};
+
+// hybrid area: u32 joint[65536] | segHistA[8][256] | rowHist[256] | meta[64]
+// (all zeroed up front) | chunkOff[65537] | chunkB0[65537] | segment tables
+// of the two top-digit passes
+constexpr uint64_t kJointBytes = kBuckets * 4;
+constexpr uint64_t kSegHistAOff = kJointBytes;                    // per position segment: second-digit counts
+constexpr uint64_t kRowHistOff = kSegHistAOff + kSegs * 256 * 4;  // top-digit counts (thrs_hist_joint)
+constexpr uint64_t kMetaOff = kRowHistOff + 256 * 4;              // zero: thrs_plan_rows raises its flags atomically
+constexpr uint64_t kJointZero = kMetaOff + 256;
+constexpr uint64_t kChunkOffOff = kJointZero;
+constexpr uint64_t kChunkB0Off = kChunkOffOff + round_up_c((kBuckets + 1) * 4, 256);
+constexpr uint64_t kSegInfoOff = kChunkB0Off + round_up_c((kBuckets + 1) * 4, 256);  // segPos[9] | segTiles[9] ... tickets[8] at +256 B (thrs_pass_seg)
+constexpr uint64_t kSegBaseOff = kSegInfoOff + 512;   // u32 [8][256] per-segment top-digit bases
+constexpr uint64_t kSegInfoAOff = kSegBaseOff + kSegs * 256 * 4;  // the same two for the second-digit pass
+constexpr uint64_t kSegBaseAOff = kSegInfoAOff + 512;
+constexpr uint64_t kHybridBytes = kSegBaseAOff + kSegs * 256 * 4;
+// tile ids of the segmented pass: each of the 8 segments adds at most one
+// partial tile and rounds its id range up to a multiple of kGroup
+constexpr uint64_t kSegTilePad = kSegs * kGroup;
+
+inline Plan make_plan(int keyType, int valueBytesOrZero, uint32_t n) {
+  Plan p{};
+  p.kb = key_bytes_of(keyType);
+  p.vb = valueBytesOrZero;
+  p.tileKeys = tile_keys(p.kb, p.vb);
+  p.nTiles = std::max<uint64_t>(1, ((uint64_t)n + p.tileKeys - 1) / p.tileKeys);
+  p.wideStatus = (uint64_t)n >= (1ull << 31);
+  const uint64_t rows = p.nTiles + kSegTilePad;  // + the segmented pass's extra tile ids
+  p.statusBytes = round_up(rows * kBins * (p.wideStatus ? 8 : 4), kAlign);
+  const uint64_t nGroups = kGroup > 0 ? (rows + kGroup - 1) / kGroup : 0;
+  p.gaBytes = round_up(nGroups * kBins * 4, kAlign);
+  p.gpBytes = round_up(nGroups * kBins * (p.wideStatus ? 8 : 4), kAlign);
+  p.setBytes = p.statusBytes + p.gaBytes + p.gpBytes;
+  const uint64_t nXb = (p.nTiles + kXcdBlock - 1) / kXcdBlock + 16;  // table stride (see xb_claim)
+  p.claimBytes = round_up((16 + 8 * nXb) * 4, kAlign);
+  p.hybridOff = kHeaderBytes + 2 * p.setBytes + 8 * p.claimBytes;
+  p.scratchBytes = p.hybridOff + kHybridBytes;
+  // the u8 plane of the planes codecs (thrs_kernels.hpp kCodecSplit): the u16
+  // planes fill keyOut, which is all a sortKeys caller must allocate
+  // (getTemporaryBufferBytesForSortKeys = pSumBuffer + keyOutBuffer)
+  p.hiPlaneOff = p.scratchBytes;
+  if (keyType == THRS_KEY_U32 && valueBytesOrZero == 0) p.scratchBytes += round_up(n, kAlign);
+  return p;
+}
+
+// ---- process-wide state, defined in thrs_capi.hip
+int cu_count();
+// HIP-event timing of the launches (thrs_profile_*): kind 0 = histogram +
+// plan, 1 = device-wide digit pass, 2 = local sort, 3 = fallback-only launches
+hipEvent_t prof_begin(hipStream_t s);
+void prof_end(hipEvent_t a, hipStream_t s, int kind);
+struct ProfScope {  // records [a, b) around the launches issued in its lifetime
+  hipStream_t s;
+  int kind;
+  hipEvent_t a;
+  ProfScope(hipStream_t s_, int k) : s(s_), kind(k), a(prof_begin(s_)) {}
+  ~ProfScope() {
+    if (a) prof_end(a, s, kind);
+  }
+};
+extern uint64_t* g_stamps;   // THRS_STAMPS diagnostic builds only (thrs_debug_set_stamps)
+extern uint64_t* g_lstamps;  // same, local sort: [chunk][8] (thrs_debug_set_local_stamps)
+// 1 = lane-ordered LDS atomics on this device (fast rank), 0 = ballot match
+int probe_rank_mode(hipStream_t stream);
+// device view of the current device's sticky error word, or nullptr (not
+// set up: the sort then runs without publishing to it)
+uint32_t* sticky_dev(hipStream_t stream);
+
+template <typename F>
+hipError_t allow_lds(F kernel, size_t bytes) {
+  if (bytes <= 65536) return hipSuccess;
+  return hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)bytes);
+}
+
+// One launch sequence.  Sort mode (counts == nullptr): the result lands in
+// keys/vals.  Partition mode (counts != nullptr, nPass == 1,
+// thrs_partition_pass): the pass writes keyOutBuf/valOutBuf, which are the
+// caller's, and the digit's 256 bucket counts go to `counts`.
+//   LSD path:    histogram of every digit + scan, nPass ping-pong passes,
+//                copy-back after an odd pass count.
+//   bucket path: 4-byte keys (u32 keys + 4-byte values over the whole key),
+//                nPass >= 3 (thrs_hybrid.hpp): bucket histogram + plan,
+//                [low-digit passes + copy, gated on the fallback flag], the
+//                two top-digit passes (skipped when one bucket holds every
+//                key), local sort.
+// Every hipFuncSetAttribute happens before the first enqueue, so a failure
+// there leaves the caller's buffers untouched.
+#ifdef THRS_RUN_KT
+template <int KT, int VB, typename ST>
+int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, void* valOutBuf, int startBits, int nPass,
+             bool desc, const Plan& plan, const thrs_options& opt, hipStream_t stream, uint32_t* counts = nullptr) {
+  using U = typename KeyTraits<KT>::U;
+  using VW = typename ValueWord<VB>::T;
+  using G = PassGeom<sizeof(U), VB>;
+
+  char* scratch = static_cast<char*>(tmp);
+  uint32_t* hist = reinterpret_cast<uint32_t*>(scratch + kHistOff);
+  uint32_t* base = reinterpret_cast<uint32_t*>(scratch + kBaseOff);
+  uint32_t* counters = reinterpret_cast<uint32_t*>(scratch + kCounterOff);
+  uint32_t* err = reinterpret_cast<uint32_t*>(scratch + kErrOff);
+  // table sets: [status | ga | gp] x 2; pass p uses set p&1 and clears its
+  // rows of set (p+1)&1 for the next pass
+  ST* status[2];
+  GroupTables<ST> grp[2];
+  for (int i = 0; i < 2; ++i) {
+    char* set = scratch + kHeaderBytes + i * plan.setBytes;
+    status[i] = reinterpret_cast<ST*>(set);
+    grp[i].ga = reinterpret_cast<uint32_t*>(set + plan.statusBytes);
+    grp[i].gp = reinterpret_cast<ST*>(set + plan.statusBytes + plan.gaBytes);
+    grp[i].nTiles = (uint32_t)plan.nTiles;
+  }
+  char* hyb = scratch + plan.hybridOff;
+  uint32_t* joint = reinterpret_cast<uint32_t*>(hyb);
+  uint32_t* chunkOff = reinterpret_cast<uint32_t*>(hyb + kChunkOffOff);
+  uint32_t* chunkB0 = reinterpret_cast<uint32_t*>(hyb + kChunkB0Off);
+  uint32_t* meta = reinterpret_cast<uint32_t*>(hyb + kMetaOff);
+  U* keyOut = static_cast<U*>(keyOutBuf);
+  VW* valOut = static_cast<VW*>(valOutBuf);
+
+  const U orderMask = desc ? (U)~(U)0 : (U)0;
+  // 4-byte keys without values; u32 keys with 4-byte values over the whole
+  // key; 8-byte keys without values or with 8-byte values over the whole key
+  constexpr bool kBucket32 = sizeof(U) == 4 && (VB == 0 || (VB == 4 && KT == 0));
+  constexpr bool kBucket64 = sizeof(U) == 8 && (VB == 0 || VB == 8);
+  constexpr bool kBucketType = kBucket32 || kBucket64;
+  const bool fullWindow = startBits == 0 && nPass * 8 >= (int)(8 * sizeof(U));
+  // Size window of the default (uniform keys: n / 65536 keys per bucket;
+  // docs/EXPERIMENTS.md row 29): the local sort costs about the same per chunk
+  // whatever its size, so below 2^28 the two passes it replaces are cheaper;
+  // above 2^30 + 2^26 the largest of 65536 uniform buckets (mean + ~4.5 sigma)
+  // outgrows the chunk capacity and the fallback would pay for the bucket
+  // histogram in vain.  THRS_PATH_BUCKET forces the path for any n (tests).
+  // Local geometries (thrs_hybrid.hpp LocG): LocSmall (9216-key chunks,
+  // uniform buckets of 4-8K keys) for n <= 2^29, LocBig (18432) above.
+  const uint64_t nn = n;
+  // (8-byte keys: one 17408-slot chunk per bucket, so up to 2^30 + 2^24: the
+  // largest uniform bucket stays ~3 sigma below the capacity)
+  const bool sizeOk = nn >= (1ull << 28) && nn <= (1ull << 30) + (sizeof(U) == 8 ? (1ull << 24) : (1ull << 26));
+  // u32 keys without values over the whole key: up to 2^31 + 2^25 with the
+  // wide 16-bit local sort (Loc16Wide: 34816-key chunks)
+  const bool wideOk = KT == 0 && VB == 0 && fullWindow && nn > (1ull << 30) + (1ull << 26) &&
+                      nn <= (1ull << 31) + (1ull << 25);
+  const bool smallLocal = opt.localGeometry == THRS_LOCAL_SMALL ? true
+                          : opt.localGeometry != THRS_LOCAL_AUTO  // BIG, BIG32 and the 16-bit kernels
+                              ? false
+                              : nn <= (1ull << 29);
+  const bool bucket = kBucketType && !counts && nPass >= 3 &&
+                      (opt.path == THRS_PATH_BUCKET || (opt.path == THRS_PATH_AUTO && (sizeOk || wideOk))) &&
+                      ((kBucket32 && VB == 0) || fullWindow);
+  const int nLow = nPass - 2;
+  // u32 keys over the whole key, large chunks: the local sort on 16-bit items
+  // (thrs_hybrid.hpp thrs_local16) over single-bucket chunks
+  const bool local16 = bucket && KT == 0 && VB == 0 && fullWindow && !smallLocal &&
+                       opt.localGeometry != THRS_LOCAL_BIG32;
+  // ... sorted by counting (thrs_local_count16) or by two LSD rounds (thrs_local16)
+  // ... in 34816-key chunks (explicitly, or by default above 2^30 + 2^26)
+  const bool wide16 = local16 && (opt.localGeometry == THRS_LOCAL_WIDE16 ||
+                                  (opt.localGeometry == THRS_LOCAL_AUTO && nn > (1ull << 30) + (1ull << 26)));
+  // (counting only when asked: it measured slower, docs/EXPERIMENTS.md row 56)
+  const bool count16 = local16 && !wide16 && opt.localGeometry == THRS_LOCAL_COUNT16;
+  const bool segTop = opt.segmented != THRS_SEG_NONE;
+  const bool segA = opt.segmented == THRS_SEG_AUTO;
+  // local16 with both top-digit passes segmented: the passes carry the keys
+  // as planes (thrs_kernels.hpp kCodecSplit / kCodecPlanes): keyOut (4n bytes)
+  // = lo u16[n] | lo2 u16[n], the u8 plane hi[n] at the end of the scratch
+  const bool planes = local16 && segA && opt.planes != THRS_PLANES_OFF &&
+                      plan.scratchBytes - plan.hiPlaneOff >= (uint64_t)n;
+  uint16_t* loP = static_cast<uint16_t*>(keyOutBuf);
+  uint16_t* lo2P = loP + n;
+  uint8_t* hiP = reinterpret_cast<uint8_t*>(scratch + plan.hiPlaneOff);
+  const bool atomicRank = opt.rank == THRS_RANK_ATOMIC ? true
+                          : opt.rank == THRS_RANK_BALLOT ? false
+                                                         : probe_rank_mode(stream) != 0;
+  // XCD-block claims (thrs_pass_xb) pay off where runs are short and the
+  // grid is large: 4-byte keys without values, n >= 2^29 (docs/EXPERIMENTS.md
+  // row 19: +4-6% there, neutral at 2^28, -2..-6% for pairs / f32 at 2^28).
+  const bool useXb = opt.tileClaims == THRS_CLAIMS_XCD_BLOCKS ? true
+                     : opt.tileClaims == THRS_CLAIMS_TICKET ? false
+                                                            : (sizeof(U) == 4 && VB == 0 && n >= (1u << 29));
+  uint32_t* sticky = sticky_dev(stream);
+
+  // ---- kernels and their LDS opt-ins, before anything is enqueued
+  const size_t lds = G::LDS_BYTES;
+  auto kernelXb = atomicRank ? thrs_pass_xb<KT, VB, ST, true> : thrs_pass_xb<KT, VB, ST, false>;
+  auto kernelPersist = atomicRank ? thrs_pass_persist<KT, VB, ST, true> : thrs_pass_persist<KT, VB, ST, false>;
+  auto kernel = useXb ? kernelXb : (atomicRank ? thrs_pass<KT, VB, ST, true> : thrs_pass<KT, VB, ST, false>);
+  auto sk = atomicRank ? thrs_pass_seg<KT, VB, ST, true> : thrs_pass_seg<KT, VB, ST, false>;
+  // plane codecs (u32 keys-only instantiations only; `planes` is false elsewhere)
+  auto skSplit = atomicRank ? thrs_pass_seg<KT, VB, ST, true, (KT == 0 && VB == 0) ? kCodecSplit : kCodecKeys>
+                            : thrs_pass_seg<KT, VB, ST, false, (KT == 0 && VB == 0) ? kCodecSplit : kCodecKeys>;
+  auto skPlanes = atomicRank ? thrs_pass_seg<KT, VB, ST, true, (KT == 0 && VB == 0) ? kCodecPlanes : kCodecKeys>
+                             : thrs_pass_seg<KT, VB, ST, false, (KT == 0 && VB == 0) ? kCodecPlanes : kCodecKeys>;
+  const int histPasses = bucket ? nLow : nPass;
+  const size_t histLds = (size_t)histPasses * kBins * hist_copies<(int)sizeof(U)>() * 4;
+  if (allow_lds(thrs_hist<KT>, histLds) != hipSuccess || allow_lds(kernel, lds) != hipSuccess ||
+      allow_lds(kernelXb, lds) != hipSuccess || allow_lds(kernelPersist, lds) != hipSuccess)
+    return THRS_ERROR_HIP;
+  if (bucket) {
+    if (allow_lds(thrs_hist_joint<KT>, kJointLds) != hipSuccess || allow_lds(sk, lds) != hipSuccess)
+      return THRS_ERROR_HIP;
+    if (planes && (allow_lds(skSplit, lds) != hipSuccess || allow_lds(skPlanes, lds) != hipSuccess))
+      return THRS_ERROR_HIP;
+    if constexpr (kBucket64) {
+      if (allow_lds(atomicRank ? thrs_local64<KT, VB, true> : thrs_local64<KT, VB, false>, Loc64::LDS) != hipSuccess)
+        return THRS_ERROR_HIP;
+    } else if constexpr (kBucketType) {
+      if (local16) {
+        if constexpr (KT == 0 && VB == 0) {
+          if (allow_lds(atomicRank ? thrs_local16<true, Loc16> : thrs_local16<false, Loc16>, Loc16::LDS) !=
+                  hipSuccess ||
+              allow_lds(atomicRank ? thrs_local16<true, Loc16Wide> : thrs_local16<false, Loc16Wide>,
+                        Loc16Wide::LDS) != hipSuccess ||
+              allow_lds(thrs_local_count16<true>, LocCount::LDS) != hipSuccess ||
+              allow_lds(thrs_local_count16<false>, LocCount::LDS) != hipSuccess)
+            return THRS_ERROR_HIP;
+        }
+      } else if constexpr (VB == 4) {
+        if (allow_lds(atomicRank ? thrs_local_pairs<true, LocBig> : thrs_local_pairs<false, LocBig>,
+                      LocBig::lds<U>()) != hipSuccess ||
+            allow_lds(atomicRank ? thrs_local_pairs<true, LocSmall> : thrs_local_pairs<false, LocSmall>,
+                      LocSmall::lds<U>()) != hipSuccess)
+          return THRS_ERROR_HIP;
+      } else {
+        if (allow_lds(atomicRank ? thrs_local<KT, true, LocBig> : thrs_local<KT, false, LocBig>, LocBig::lds<U>()) !=
+                hipSuccess ||
+            allow_lds(atomicRank ? thrs_local<KT, true, LocSmall> : thrs_local<KT, false, LocSmall>,
+                      LocSmall::lds<U>()) != hipSuccess)
+          return THRS_ERROR_HIP;
+      }
+    }
+  }
+  // persistent grids (occupancy x CUs): the XCD-block kernel, and the bucket
+  // path's fallback-only passes (thrs_pass_persist): a launch of nTiles
+  // workgroups that all exit at once still costs ~0.1 ms at 2^18 tiles
+  auto persistent_grid = [&](auto kern) -> uint32_t {
+    int perCU = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, kern, G::THREADS, lds) != hipSuccess || perCU < 1)
+      perCU = 1;
+    return (uint32_t)std::min<uint64_t>(plan.nTiles, (uint64_t)perCU * cu_count());
+  };
+  const uint32_t gridXb = useXb ? persistent_grid(kernelXb) : (uint32_t)plan.nTiles;
+  const uint32_t gridPersist = bucket ? persistent_grid(kernelPersist) : (uint32_t)plan.nTiles;
+  const uint32_t grid = useXb ? gridXb : (uint32_t)plan.nTiles;
+  int segPerCU = 0;
+  if (bucket &&
+      (hipOccupancyMaxActiveBlocksPerMultiprocessor(&segPerCU, sk, G::THREADS, lds) != hipSuccess || segPerCU < 1))
+    segPerCU = 1;
+
+  // header (histograms, tile counters, error word) + first status table; the
+  // bucket path with an odd number of (skippable) low passes starts on set 1
+  // too, and zeroes its bucket histogram
+  // Bucket path: ONE memset from the header through the bucket histogram --
+  // both table sets (the top-digit passes use set nLow&1 and the other one,
+  // and no launch before them dirties the other unless it also cleans it:
+  // fallback passes clear their successor's rows), all 8 claim areas, joint.
+  if (bucket) {
+    if (hipMemsetAsync(scratch, 0, plan.hybridOff + kJointZero, stream) != hipSuccess) return THRS_ERROR_HIP;
+  } else if (hipMemsetAsync(scratch, 0, kHeaderBytes + plan.setBytes, stream) != hipSuccess) {
+    return THRS_ERROR_HIP;
+  }
+  char* claim = scratch + kHeaderBytes + 2 * plan.setBytes;  // 8 per-pass claim areas
+
+  {  // histograms of every pass in one read of the keys
+    ProfScope prof(stream, 0);
+    const int vec = (reinterpret_cast<uintptr_t>(keys) % 16) == 0;
+    const uint64_t want = ((uint64_t)n + kHistThreads * 64 - 1) / (kHistThreads * 64);
+    const int hgrid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cu_count() * THRS_HIST_GRID_MULT));
+    if (bucket) {
+      hipLaunchKernelGGL(thrs_hist_joint<KT>, dim3(hgrid), dim3(kHistThreads), kJointLds, stream,
+                         static_cast<const U*>(keys), n, orderMask, startBits + 8 * nLow, vec, joint,
+                         reinterpret_cast<uint32_t*>(hyb + kSegHistAOff), reinterpret_cast<uint32_t*>(hyb + kRowHistOff));
+      const uint32_t cap = kBucket64 ? Loc64::CAP : smallLocal ? LocSmall::CAP : wide16 ? Loc16Wide::CAP : LocBig::CAP;
+      if (VB || local16 || kBucket64) {
+        // single-bucket chunks: one workgroup per top digit
+        hipLaunchKernelGGL(thrs_plan_rows, dim3(kBins), dim3(kPlanRowThreads), 0, stream, joint,
+                           reinterpret_cast<const uint32_t*>(hyb + kRowHistOff),
+                           reinterpret_cast<const uint32_t*>(hyb + kSegHistAOff), n, cap, base + nLow * kBins,
+                           chunkOff, chunkB0, meta, reinterpret_cast<uint32_t*>(hyb + kSegInfoOff),
+                           reinterpret_cast<uint32_t*>(hyb + kSegBaseOff), (uint32_t)G::TILE, (uint32_t)hgrid,
+                           reinterpret_cast<uint32_t*>(hyb + kSegInfoAOff), reinterpret_cast<uint32_t*>(hyb + kSegBaseAOff));
+      } else {
+        // chunks: whole buckets; neighbouring buckets below kLocCap/2 keys share one
+        hipLaunchKernelGGL(thrs_plan, dim3(1), dim3(kPlanThreads), 0, stream, joint, n, base + nLow * kBins, chunkOff,
+                           chunkB0, meta, cap, (VB || local16 || kBucket64) ? -1 : smallLocal ? kLocSmallLogT : kLocLogT,
+                           reinterpret_cast<uint32_t*>(hyb + kSegInfoOff), reinterpret_cast<uint32_t*>(hyb + kSegBaseOff),
+                           (uint32_t)G::TILE, reinterpret_cast<const uint32_t*>(hyb + kSegHistAOff), (uint32_t)hgrid,
+                           reinterpret_cast<uint32_t*>(hyb + kSegInfoAOff), reinterpret_cast<uint32_t*>(hyb + kSegBaseAOff));
+      }
+      // the low digits' histograms + bases: needed only on the fallback path
+      hipLaunchKernelGGL(thrs_hist<KT>, dim3(hgrid), dim3(kHistThreads), histLds, stream, static_cast<const U*>(keys),
+                         n, orderMask, startBits, nLow, vec, hist, meta + kMetaFallback);
+      hipLaunchKernelGGL(thrs_scan, dim3(1), dim3(kThreads), 0, stream, hist, base, nLow, meta + kMetaFallback);
+    } else {
+      hipLaunchKernelGGL(thrs_hist<KT>, dim3(hgrid), dim3(kHistThreads), histLds, stream, static_cast<const U*>(keys),
+                         n, orderMask, startBits, nPass, vec, hist, nullptr);
+      hipLaunchKernelGGL(thrs_scan, dim3(1), dim3(kThreads), 0, stream, hist, base, nPass, nullptr);
+    }
+    if (counts && hipMemcpyAsync(counts, hist, kBins * sizeof(uint32_t), hipMemcpyDeviceToDevice, stream) != hipSuccess)
+      return THRS_ERROR_HIP;
+  }
+
+  if (useXb && !bucket && hipMemsetAsync(claim, 0, (size_t)nPass * plan.claimBytes, stream) != hipSuccess)
+    return THRS_ERROR_HIP;
+
+  // pass p: digit at startBits + 8p, tables of set p&1; gate != nullptr runs
+  // it only if bit *gate of gateMask is set (meta words written by thrs_plan)
+  auto launch_pass = [&](int p, U* kin, U* kout, VW* vin, VW* vout, const uint32_t* gate, uint32_t gateMask) {
+    const bool more = p + 1 < nPass;
+    ST* next = more ? status[(p + 1) & 1] : nullptr;
+    GroupTables<ST> g = grp[p & 1];
+    g.gaNext = more ? grp[(p + 1) & 1].ga : nullptr;
+    g.gpNext = more ? grp[(p + 1) & 1].gp : nullptr;
+    ProfScope prof(stream, gate && (gateMask == kGateFallback || gateMask == kGateMode1) ? 3 : 1);  // fallback-only passes are timed apart
+    // fallback-only launches (most exit at once): persistent ticket kernel,
+    // unless the XCD-block kernel runs anyway
+    const bool fallbackOnly = gate && (gateMask == kGateFallback || gateMask == kGateMode1);
+    const bool persist = bucket && fallbackOnly && !useXb;
+    hipLaunchKernelGGL(persist ? kernelPersist : kernel, dim3(persist ? gridPersist : grid), dim3(G::THREADS), lds,
+                       stream, kin, kout, vin, vout, n, orderMask, startBits + 8 * p, base + p * kBins, status[p & 1],
+                       next, useXb ? reinterpret_cast<uint32_t*>(claim + p * plan.claimBytes) : counters + p, err, g,
+                       g_stamps ? g_stamps + (uint64_t)p * plan.nTiles * kStampSlots : nullptr, gate, gateMask);
+  };
+  auto publish_error = [&]() -> int {
+    if (sticky) hipLaunchKernelGGL(thrs_err_publish, dim3(1), dim3(1), 0, stream, err, sticky);
+    return hipGetLastError() == hipSuccess ? THRS_SUCCESS : THRS_ERROR_HIP;
+  };
+
+  if (!bucket) {
+    U* kin = static_cast<U*>(keys);
+    U* kout = keyOut;
+    VW* vin = static_cast<VW*>(vals);
+    VW* vout = valOut;
+    for (int p = 0; p < nPass; ++p) {
+      launch_pass(p, kin, kout, vin, vout, nullptr, 0u);
+      std::swap(kin, kout);
+      std::swap(vin, vout);
+    }
+    if (hipGetLastError() != hipSuccess) return THRS_ERROR_HIP;
+    if ((nPass & 1) && !counts) {  // result must end in the caller's buffers (hpp:936-943), stream-ordered here
+      if (hipMemcpyAsync(keys, keyOut, (size_t)n * sizeof(U), hipMemcpyDeviceToDevice, stream) != hipSuccess)
+        return THRS_ERROR_HIP;
+      if (VB && hipMemcpyAsync(vals, valOut, (size_t)n * VB, hipMemcpyDeviceToDevice, stream) != hipSuccess)
+        return THRS_ERROR_HIP;
+    }
+    return publish_error();
+  }
+
+  // ---- bucket path: fallback-only low passes, the two top digits, local sort
+  if constexpr (kBucketType) {
+    U* K = static_cast<U*>(keys);
+    VW* V = static_cast<VW*>(vals);
+    uint32_t* fallback = meta + kMetaFallback;
+    uint32_t* mode = meta + kMetaMode;
+    {
+      U* kin = K;
+      U* kout = keyOut;
+      VW* vin = V;
+      VW* vout = valOut;
+      for (int p = 0; p < nLow; ++p) {
+        launch_pass(p, kin, kout, vin, vout, fallback, kGateFallback);
+        std::swap(kin, kout);
+        std::swap(vin, vout);
+      }
+      if (nLow & 1) {  // fallback result is in keyOut: the top-digit passes read K
+        hipLaunchKernelGGL(thrs_copy_gated, dim3(2048), dim3(256), 0, stream,
+                           reinterpret_cast<const uint32_t*>(keyOut), reinterpret_cast<uint32_t*>(K),
+                           (uint64_t)n * sizeof(U) / 4, fallback, 1u);
+        if (VB)
+          hipLaunchKernelGGL(thrs_copy_gated, dim3(2048), dim3(256), 0, stream,
+                             reinterpret_cast<const uint32_t*>(valOut), reinterpret_cast<uint32_t*>(V),
+                             (uint64_t)n * VB / 4, fallback, 1u);
+      }
+    }
+    // The two top digits: XCD-segmented passes (thrs_kernels.hpp
+    // thrs_pass_seg) -- the second digit over position segments (the bucket
+    // histogram's workgroup ranges), the top digit over second-digit ranges.
+    // Gates on meta[kMetaMode]: mode 0 (local path) the segmented second-digit
+    // pass, mode 1 (fallback) the plain one (the position segments' counts are
+    // those of the INPUT order, not the low passes' output), mode 2 (one
+    // bucket holds every key: both top digits constant) neither, and no
+    // top-digit pass either (both are identities, and skipping both keeps the
+    // result in K).
+    auto launch_seg = [&](int p, U* kin, U* kout, VW* vin, VW* vout, uint64_t infoOff, uint64_t baseOff,
+                          const uint32_t* gate, uint32_t gateMask, int codec = kCodecKeys) {
+      ProfScope prof(stream, gateMask == kGateMode1 ? 3 : 1);  // fallback-only launches are timed apart
+      auto kern = codec == kCodecSplit ? skSplit : codec == kCodecPlanes ? skPlanes : sk;
+      // kCodecPlanes: image-space input (orderMask 0), digit at bits 16-23 of k'
+      hipLaunchKernelGGL(kern, dim3((uint32_t)segPerCU * cu_count()), dim3(G::THREADS), lds, stream, kin, kout, vin,
+                         vout, codec == kCodecPlanes ? (U)0 : orderMask, codec == kCodecPlanes ? 16 : startBits + 8 * p,
+                         reinterpret_cast<uint32_t*>(hyb + infoOff), reinterpret_cast<const uint32_t*>(hyb + baseOff),
+                         status[p & 1], err, grp[p & 1], gate, gateMask, hiP);
+    };
+    const uint64_t sw = plan.wideStatus ? 8 : 4;
+    const int setB = (nLow + 1) & 1;
+    if (segA) {
+      // Both table sets are clean: zeroed up front, and on the fallback each
+      // low pass clears its successor's rows; the segmented passes' extra
+      // tile ids (rows past nTiles) are touched by nothing else.
+      if (planes)
+        launch_seg(nLow, K, reinterpret_cast<U*>(loP), V, valOut, kSegInfoAOff, kSegBaseAOff, mode, kGateMode0,
+                   kCodecSplit);
+      else
+        launch_seg(nLow, K, keyOut, V, valOut, kSegInfoAOff, kSegBaseAOff, mode, kGateMode0);
+      launch_pass(nLow, K, keyOut, V, valOut, mode, kGateMode1);
+    } else {
+      launch_pass(nLow, K, keyOut, V, valOut, mode, kGateMode0 | kGateMode1);
+      // the segmented pass's tile ids reach past nTiles (per-segment
+      // rounding): clear those rows (pass nLow cleared rows [0, nTiles))
+      const uint64_t nGroups0 = (plan.nTiles + kGroup - 1) / kGroup;
+      if (hipMemsetAsync(reinterpret_cast<char*>(status[setB]) + plan.nTiles * kBins * sw, 0,
+                         kSegTilePad * kBins * sw, stream) != hipSuccess ||
+          hipMemsetAsync(grp[setB].ga + nGroups0 * kBins, 0, (kSegs + 1) * kBins * 4, stream) != hipSuccess ||
+          hipMemsetAsync(reinterpret_cast<char*>(grp[setB].gp) + nGroups0 * kBins * sw, 0, (kSegs + 1) * kBins * sw,
+                         stream) != hipSuccess)
+        return THRS_ERROR_HIP;
+    }
+    if (planes) {  // mode 0: planes -> lo2; mode 1 (fallback): keys
+      launch_seg(nLow + 1, reinterpret_cast<U*>(loP), reinterpret_cast<U*>(lo2P), valOut, V, kSegInfoOff, kSegBaseOff,
+                 mode, kGateMode0, kCodecPlanes);
+      launch_seg(nLow + 1, keyOut, K, valOut, V, kSegInfoOff, kSegBaseOff, mode, kGateMode1);
+    } else if (segTop)
+      launch_seg(nLow + 1, keyOut, K, valOut, V, kSegInfoOff, kSegBaseOff, mode, kGateMode0 | kGateMode1);
+    else
+      launch_pass(nLow + 1, keyOut, K, valOut, V, mode, kGateMode0 | kGateMode1);
+    {
+      ProfScope prof(stream, 2);
+      // never more workgroups than chunks can exist: <= 256 (one per top digit)
+      // + 2 per non-empty bucket, and <= the number of buckets
+      // (single-bucket chunks -- pairs, local16, 8-byte keys: thrs_plan makes
+      // every bucket a chunk, empty or not)
+      const bool singleChunks = VB || local16 || kBucket64;
+      const uint64_t maxChunks = singleChunks ? kBuckets : std::min<uint64_t>(kBuckets, 256 + 2 * (uint64_t)n);
+      auto launch_local = [&](auto geom) {
+        using LG = decltype(geom);
+        const size_t llds = LG::template lds<U>();
+        if constexpr (kBucket64) {
+          (void)llds;
+        } else if constexpr (VB == 4) {
+          auto lk = atomicRank ? thrs_local_pairs<true, LG> : thrs_local_pairs<false, LG>;
+          hipLaunchKernelGGL(lk, dim3((uint32_t)maxChunks), dim3(LG::THREADS), llds, stream,
+                             reinterpret_cast<uint32_t*>(K), reinterpret_cast<uint32_t*>(V), (uint32_t)orderMask,
+                             chunkOff, chunkB0, meta);
+        } else {
+          auto lk = atomicRank ? thrs_local<KT, true, LG> : thrs_local<KT, false, LG>;
+          hipLaunchKernelGGL(lk, dim3((uint32_t)maxChunks), dim3(LG::THREADS), llds, stream, K, orderMask, startBits,
+                             nLow, chunkOff, chunkB0, meta, g_lstamps);
+        }
+      };
+      if constexpr (kBucket64) {
+        auto lk = atomicRank ? thrs_local64<KT, VB, true> : thrs_local64<KT, VB, false>;
+        hipLaunchKernelGGL(lk, dim3((uint32_t)maxChunks), dim3(Loc64::THREADS), Loc64::LDS, stream,
+                           reinterpret_cast<uint64_t*>(K), reinterpret_cast<uint64_t*>(V), (uint64_t)orderMask,
+                           chunkOff, chunkB0, meta);
+      } else if (local16) {
+        if constexpr (KT == 0 && VB == 0) {
+          if (count16) {
+            // persistent: one 128-KiB workgroup per CU walks the chunks
+            const uint32_t cgrid = (uint32_t)std::min<uint64_t>(maxChunks, (uint64_t)cu_count());
+            // planes off / mode 2: the items are the keys themselves (in place)
+            auto lk = planes ? thrs_local_count16<true> : thrs_local_count16<false>;
+            hipLaunchKernelGGL(lk, dim3(cgrid), dim3(LocCount::THREADS), LocCount::LDS, stream,
+                               reinterpret_cast<uint32_t*>(K), n, (uint32_t)orderMask, chunkOff, chunkB0, meta,
+                               static_cast<const uint16_t*>(lo2P), joint);
+          } else if (wide16) {
+            auto lk = atomicRank ? thrs_local16<true, Loc16Wide> : thrs_local16<false, Loc16Wide>;
+            hipLaunchKernelGGL(lk, dim3((uint32_t)maxChunks), dim3(Loc16Wide::THREADS), Loc16Wide::LDS, stream,
+                               reinterpret_cast<uint32_t*>(K), (uint32_t)orderMask, chunkOff, chunkB0, meta,
+                               planes ? static_cast<const uint16_t*>(lo2P) : nullptr);
+          } else {
+            auto lk = atomicRank ? thrs_local16<true, Loc16> : thrs_local16<false, Loc16>;
+            hipLaunchKernelGGL(lk, dim3((uint32_t)maxChunks), dim3(Loc16::THREADS), Loc16::LDS, stream,
+                               reinterpret_cast<uint32_t*>(K), (uint32_t)orderMask, chunkOff, chunkB0, meta,
+                               planes ? static_cast<const uint16_t*>(lo2P) : nullptr);
+          }
+        }
+      } else if (smallLocal) {
+        launch_local(LocSmall{});
+      } else {
+        launch_local(LocBig{});
+      }
+    }
+    if (hipGetLastError() != hipSuccess) return THRS_ERROR_HIP;
+  }
+  return publish_error();
+}
+
+template <int KT, int VB>
+int run_st(void* keys, void* vals, uint32_t n, void* tmp, void* ko, void* vo, int startBits, int nPass, bool desc,
+           const Plan& plan, const thrs_options& opt, hipStream_t stream, uint32_t* counts) {
+  if (plan.wideStatus)
+    return run_sort<KT, VB, uint64_t>(keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, opt, stream, counts);
+  return run_sort<KT, VB, uint32_t>(keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, opt, stream, counts);
+}
+
+template <int KT>
+int run_vb(int vb, void* keys, void* vals, uint32_t n, void* tmp, void* ko, void* vo, int startBits, int nPass,
+           bool desc, const Plan& plan, const thrs_options& opt, hipStream_t stream, uint32_t* counts = nullptr) {
+  switch (vb) {
+    case 0: return run_st<KT, 0>(keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, opt, stream, counts);
+    case 4: return run_st<KT, 4>(keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, opt, stream, counts);
+    case 8: return run_st<KT, 8>(keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, opt, stream, counts);
+    case 16: return run_st<KT, 16>(keys, vals, n, tmp, ko, vo, startBits, nPass, desc, plan, opt, stream, counts);
+  }
+  return THRS_ERROR_INVALID_VALUE;
+}
+
+#else
+template <int KT>
+int run_vb(int vb, void* keys, void* vals, uint32_t n, void* tmp, void* ko, void* vo, int startBits, int nPass,
+           bool desc, const Plan& plan, const thrs_options& opt, hipStream_t stream, uint32_t* counts = nullptr);
+#endif
+
+}  // namespace thrs_host

@@ -33,6 +33,9 @@
 #include "thrs_kernels.hpp"
 
 namespace thrs_dev {
+// (internal linkage: every translation unit of libthrs.so gets its own copy
+// of the kernels it launches)
+namespace {
 
 constexpr uint32_t kBuckets = 65536;  // 16-bit bucket = the window's top two digits
 // meta[kMetaMode]: 0 = local path (no bucket above the local capacity);
@@ -51,18 +54,7 @@ constexpr uint32_t kGateMode0 = 1u << 0, kGateMode1 = 1u << 1, kGateMode2 = 1u <
 // carry can reach the neighbouring field, so any skew is counted exactly.
 // (The two top digits' histograms are the row and column sums of this one:
 // thrs_plan.)
-#ifndef THRS_LOC_STORE_HOIST
-#define THRS_LOC_STORE_HOIST 1  // local sort write-out: all stage reads before the stores
-#endif
-#ifndef THRS_HJ_UN
-#define THRS_HJ_UN 4  // 16-byte loads in flight per lane
-#endif
-#ifndef THRS_HJ_BATCHCARRY
-#define THRS_HJ_BATCHCARRY 0  // 1: one guard-bit test per 16 adds (measured slower, EXPERIMENTS row 50)
-#endif
-#ifndef THRS_HJ_PF
-#define THRS_HJ_PF 1  // bucket histogram: next iteration's loads in flight during the adds
-#endif
+constexpr int kHjUnroll = 4;  // bucket histogram: 16-byte loads in flight per lane
 constexpr uint32_t kJointWords = kBuckets / 2;
 // Carries (32768 keys of one bucket) are logged in LDS and flushed once per
 // distinct bucket at the end: a constant input would otherwise send every
@@ -149,13 +141,12 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
   uint64_t tailStart = lo;
   if (vec) {  // 16-byte loads, UN in flight per lane (keys base 16-B aligned, checked on host)
     constexpr int PER = 16 / sizeof(U);
-    constexpr int UN = THRS_HJ_UN;
+    constexpr int UN = kHjUnroll;
     constexpr uint32_t ITERS_PER_EPOCH = kEpoch / (kHistThreads * UN * PER);
     static_assert(ITERS_PER_EPOCH >= 1, "one iteration must fit an epoch");
     const uint64_t v0 = lo / PER, nv = hi / PER;   // lo is a multiple of 4 (hj_len)
     const uint4* kv = reinterpret_cast<const uint4*>(keys);
     const uint64_t nIter = nv > v0 ? (nv - v0 + UN * gstride - 1) / (UN * gstride) : 0;
-#if THRS_HJ_PF
     // software pipelined: iteration it+1's loads are issued before iteration
     // it's LDS adds, so every wave keeps UN loads in flight while it counts.
     // Loads past the range read the range's last word (clamped, unconditional:
@@ -167,18 +158,12 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
     };
     uint4 qn[UN];
     if (nIter) load_iter(0, qn);
-#endif
     for (uint64_t it = 0; it < nIter; ++it) {
       const uint64_t i = v0 + it * UN * gstride + tid;
       uint4 q[UN];
-#if THRS_HJ_PF
 #pragma unroll
       for (int u = 0; u < UN; ++u) q[u] = qn[u];
       load_iter(min(it + 1, nIter - 1), qn);
-#else
-#pragma unroll
-      for (int u = 0; u < UN; ++u) q[u] = (i + u * gstride < nv) ? kv[i + u * gstride] : uint4{0, 0, 0, 0};
-#endif
       uint32_t b[UN * PER], o[UN * PER] = {}, inc[UN * PER];
 #pragma unroll
       for (int u = 0; u < UN; ++u) {
@@ -201,20 +186,8 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
         } else if (mode == kMixed) {
 #pragma unroll
           for (int e = 0; e < E; ++e) o[e] = add(b[e], 1u);
-#if THRS_HJ_BATCHCARRY
-          // a carry (field crossing 0x8000) flips its guard bit: one test for
-          // all E adds, the exact per-add check only when some lane carried
-          uint32_t flips = 0;
-#pragma unroll
-          for (int e = 0; e < E; ++e) flips |= (o[e] ^ (o[e] + (1u << ((b[e] & 1u) << 4)))) & 0x80008000u;
-          if (__ballot(flips != 0)) {
-#pragma unroll
-            for (int e = 0; e < E; ++e) check(b[e], o[e], 1u);
-          }
-#else
 #pragma unroll
           for (int e = 0; e < E; ++e) check(b[e], o[e], 1u);
-#endif
         } else {
 #pragma unroll
           for (int e = 0; e < E; ++e) {
@@ -884,18 +857,12 @@ __device__ __forceinline__ void loc_sort_chunk(typename KeyTraits<KT>::U (&k)[LG
       if (j * 64 < lim) src[j * 64] = k[j];
     return;
   }
-#if THRS_LOC_STORE_HOIST
   U o[KPT];  // stage reads first, then the lane-conditional stores (see thrs_local16)
 #pragma unroll
   for (int j = 0; j < KPT; ++j) o[j] = stw[j * 64];
 #pragma unroll
   for (int j = 0; j < KPT; ++j)
     if (j * 64 < lim) src[j * 64] = o[j];
-#else
-#pragma unroll
-  for (int j = 0; j < KPT; ++j)
-    if (j * 64 < lim) src[j * 64] = stw[j * 64];
-#endif
 #ifdef THRS_STAMPS
   loc_stamp(st, 4);
   if (st) {
@@ -1352,9 +1319,6 @@ __global__ __launch_bounds__(LocCount::THREADS) void thrs_local_count16(
 // rebuilt from the bucket and written, and the values are permuted through
 // the same LDS stage by the carried positions.  (f32 keys stay on the LSD
 // path: +0 and -0 share one image and could not be rebuilt bit-exactly.)
-#ifndef THRS_PAIRS_EARLY_VALUES
-#define THRS_PAIRS_EARLY_VALUES 0  // 1: load the values with the keys (spills 36 VGPRs at 8x36)
-#endif
 template <bool ATOMIC_RANK, typename LG>
 __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(4))) void thrs_local_pairs(
     uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, uint32_t orderMask,
@@ -1389,20 +1353,11 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(4))
     const uint32_t pos = myOff + j * 64;
     it[j] = (j * 64 < lim) ? (((it[j] ^ orderMask) << 16) | pos) : 0xFFFF0000u;  // padding: digits 255
   }
-#if THRS_PAIRS_EARLY_VALUES
-  uint32_t vv[KPT];  // values in flight during the rounds
-#pragma unroll
-  for (int j = 0; j < KPT; ++j) vv[j] = (j * 64 < lim) ? vsrc[j * 64] : 0u;
-#endif
   loc_rounds<0, ATOMIC_RANK, LG>(it, ch, 0u, 16, 2, smem, nullptr);
   pin(reinterpret_cast<uint32_t&>(lim));
-#if THRS_PAIRS_EARLY_VALUES
-#pragma unroll
-  for (int j = 0; j < KPT; ++j) it[j] = vv[j];
-#else
-  // values of this thread's positions (the item registers are free again)
+  // values of this thread's positions (the item registers are free again;
+  // loading them with the keys would spill: EXPERIMENTS row 31)
   load_run<KPT>(it, vals + ch.start, myOff, ch.size, avail);
-#endif
   uint32_t* stage = reinterpret_cast<uint32_t*>(smem);
   const uint32_t* stw = stage + w * CHUNK + lane;
   uint32_t id[(KPT + 1) / 2];  // carried positions, two 16-bit halves per register
@@ -1615,4 +1570,5 @@ __global__ void thrs_copy_gated(const uint32_t* __restrict__ src, uint32_t* __re
     dst[i] = src[i];
 }
 
+}  // namespace
 }  // namespace thrs_dev

@@ -28,6 +28,9 @@
 #include <type_traits>
 
 namespace thrs_dev {
+// (internal linkage: every translation unit of libthrs.so gets its own copy
+// of the kernels it launches)
+namespace {
 
 constexpr int kRadixBits = 8;
 constexpr int kBins = 256;
@@ -131,9 +134,6 @@ __device__ __forceinline__ void match_digit(uint32_t d, uint32_t& mlo, uint32_t&
 //   kMixed       random input: one atomic per lane and item, no extra test.
 // Every lane of the wave is active in all of these.
 enum : uint32_t { kMixed = 0, kSomeUniform = 1, kAllUniform = 2 };
-#ifndef THRS_WAVE_MODE_EARLY
-#define THRS_WAVE_MODE_EARLY 0  // 1: test the first / last item before the others
-#endif
 
 __device__ __forceinline__ bool wave_uniform(uint32_t d) {
   const uint32_t d0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)d);
@@ -143,20 +143,6 @@ __device__ __forceinline__ bool wave_uniform(uint32_t d) {
 template <int N, typename F>
 __device__ __forceinline__ uint32_t wave_mode(F digit, int nItems, uint32_t& d0) {
   d0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)digit(0));
-#if THRS_WAVE_MODE_EARLY
-  // first and last item decide first: neither uniform (random input) is
-  // kMixed without looking at the others
-  bool some = wave_uniform(digit(0));
-#pragma unroll
-  for (int j = 1; j < N; ++j)
-    if (j == nItems - 1) some = some || wave_uniform(digit(j));
-  if (!some) return kMixed;
-  uint32_t diff = 0;
-#pragma unroll
-  for (int j = 0; j < N; ++j)
-    if (j < nItems) diff |= digit(j) ^ d0;
-  return __ballot(diff != 0) == 0 ? kAllUniform : kSomeUniform;
-#else
   uint32_t diff = 0;
 #pragma unroll
   for (int j = 0; j < N; ++j)
@@ -167,7 +153,6 @@ __device__ __forceinline__ uint32_t wave_mode(F digit, int nItems, uint32_t& d0)
   for (int j = 1; j < N; ++j)
     if (j == nItems - 1) some = some || wave_uniform(digit(j));
   return some ? kSomeUniform : kMixed;
-#endif
 }
 
 // true iff digit(j) is the same for every j < N in every lane; d0 = that digit
@@ -488,26 +473,11 @@ template <typename ST> struct GroupTables {
   uint32_t gmin = 0;  // first group of this tile's chain (segmented passes)
 };
 
-#ifndef THRS_RELOAD_KEYS
-#define THRS_RELOAD_KEYS 0
-#endif
 #ifndef THRS_RANK_PIPE
 #define THRS_RANK_PIPE 2  // pass rank: LDS atomics in flight per wave
 #endif
-#ifndef THRS_WO_FULL_PAIRS
-#define THRS_WO_FULL_PAIRS 0  // 1: whole-tile batched write-out for pairs too (slower: EXPERIMENTS row 51)
-#endif
 #ifndef THRS_WO_BATCH
 #define THRS_WO_BATCH 8
-#endif
-#ifndef THRS_LATE_CLEAR
-#define THRS_LATE_CLEAR 1
-#endif
-#ifndef THRS_PUB_BY_WALKERS
-#define THRS_PUB_BY_WALKERS 0
-#endif
-#ifndef THRS_EARLY_WINDOW
-#define THRS_EARLY_WINDOW 0
 #endif
 
 // Tile configuration per (key bytes, value bytes).  A tile is what one
@@ -592,9 +562,7 @@ __device__ __forceinline__ uint32_t xcc_id() {
 // sends one round of status loads (this group's earlier tile rows + a window
 // of group rows); finish() consumes rounds until the walk ends, writes the
 // digit's global write offset to s_gofs[d] and, from the group's last tile,
-// publishes the group's inclusive prefix.  The first round may be issued
-// early (THRS_EARLY_WINDOW: right after the tile aggregate) so its round trip
-// overlaps the local scan and the rank.
+// publishes the group's inclusive prefix.
 template <typename ST>
 struct GroupWalk {
   const ST* status;
@@ -664,7 +632,7 @@ struct GroupWalk {
     }
     return stall;
   }
-  __device__ __forceinline__ void finish(bool issued, uint32_t realTot, uint32_t myBase, uint32_t localStart,
+  __device__ __forceinline__ void finish(uint32_t realTot, uint32_t myBase, uint32_t localStart,
                                          uint32_t* s_gofs, uint32_t* s_misc, uint32_t* errFlag,
                                          uint64_t* __restrict__ stamps) {
 #ifdef THRS_STAMPS
@@ -676,8 +644,7 @@ struct GroupWalk {
     (void)stamps;
 #endif
     while (walking()) {
-      if (!issued) issue();
-      issued = false;
+      issue();
       const bool stall = consume();
 #ifdef THRS_STAMPS
       if (st0 && rounds == 1) {
@@ -713,12 +680,6 @@ struct GroupWalk {
     s_gofs[d] = myBase + total - localStart;
     if (tile == gend - 1) {
       store_agent(grp->gp + (uint64_t)g * kBins + d, Status<ST>::pre(total + realTot));
-#if !THRS_LATE_CLEAR
-      if (grp->gaNext) {
-        grp->gaNext[(uint64_t)g * kBins + d] = 0;
-        grp->gpNext[(uint64_t)g * kBins + d] = 0;
-      }
-#endif
     }
   }
 };
@@ -814,12 +775,12 @@ __device__ __forceinline__ void pass_tile(
   using U = typename KeyTraits<KT>::U;
   using VW = typename ValueWord<VB>::T;
   using G = PassGeom<sizeof(U), VB>;
-  static_assert(CODEC == kCodecKeys || (sizeof(U) == 4 && VB == 0 && !THRS_RELOAD_KEYS), "codecs: u32 keys only");
+  static_assert(CODEC == kCodecKeys || (sizeof(U) == 4 && VB == 0), "codecs: u32 keys only");
   constexpr int WAVES = G::WAVES, KPT = G::KPT, ROUNDS = G::ROUNDS, THREADS = G::THREADS;
   constexpr uint32_t T = G::TILE, STAGE = G::STAGE, CHUNK = 64 * KPT;
   constexpr int STAGE_SHIFT = __builtin_ctz(STAGE);
   // threads [PUB_LO, PUB_LO+256) publish the tile's status row (see phase B)
-  constexpr uint32_t PUB_LO = (WAVES >= 8 && !THRS_PUB_BY_WALKERS) ? 256u : 0u;
+  constexpr uint32_t PUB_LO = WAVES >= 8 ? 256u : 0u;
   U* stage_k = reinterpret_cast<U*>(smem);
   VW* stage_v = reinterpret_cast<VW*>(smem + STAGE * sizeof(U));
   uint32_t* s_cnt = reinterpret_cast<uint32_t*>(smem + STAGE * (sizeof(U) + VB));  // [WAVES][256]
@@ -915,11 +876,6 @@ __device__ __forceinline__ void pass_tile(
                              __HIP_MEMORY_SCOPE_AGENT);
   }
   GroupWalk<ST> gw(status, grp, tile, d);
-  if constexpr (kGroup > 0) {
-#if THRS_EARLY_WINDOW
-    if (tid < 256 && tile != 0) gw.issue();  // first round in flight during the scan and the rank
-#endif
-  }
   // Look-back window loader: rows j, j-1, ... of column d.  32-bit byte offsets
   // from the uniform base -> saddr loads, one VGPR each.
   ST win[kLookWindow];
@@ -933,11 +889,6 @@ __device__ __forceinline__ void pass_tile(
                                                             (off0 - (uint32_t)q * kBins * sizeof(ST))))
                    : (ST)0;
   };
-#if THRS_EARLY_WINDOW
-  // first window in flight during the local scan and the rank (phase C)
-  if constexpr (kGroup == 0)
-    if (tid < 256 && tile != chainStart) issue_window();
-#endif
   // local exclusive scan over the 256 digits (waves 0-3)
   uint32_t localStart = 0;
   {
@@ -1026,11 +977,7 @@ __device__ __forceinline__ void pass_tile(
   // ---- D: decoupled look-back for digit d, kLookWindow rows per round trip;
   // a not-yet-published word stops the window and is re-polled.
   if constexpr (kGroup > 0) {
-    if (tid < 256) gw.finish(THRS_EARLY_WINDOW && tile != 0, realTot, myBase, localStart, s_gofs, s_misc, errFlag,
-                             stamps);
-#if !THRS_LATE_CLEAR
-    if (tid < 256 && statusNext) statusNext[(uint64_t)tile * kBins + d] = 0;  // ready for the next pass
-#endif
+    if (tid < 256) gw.finish(realTot, myBase, localStart, s_gofs, s_misc, errFlag, stamps);
 #ifdef THRS_STAMPS
     if (stamps && lane == 0 && w < 4) {  // slots 12..15: waves 0..3 arrive at the post-walk barrier
       uint32_t dep = s_gofs[d & 255];
@@ -1046,10 +993,8 @@ __device__ __forceinline__ void pass_tile(
 #endif
     if (tile != chainStart) {
       uint32_t spins = 0;
-      bool pending = THRS_EARLY_WINDOW && kGroup == 0;  // the first window is already in flight
       while (true) {
-        if (!pending) issue_window();
-        pending = false;
+        issue_window();
 #ifdef THRS_STAMPS
         ++dbgRounds;
 #endif
@@ -1086,9 +1031,6 @@ __device__ __forceinline__ void pass_tile(
 #endif
     }
     s_gofs[d] = myBase + excl - localStart;
-#if !THRS_LATE_CLEAR
-    if (statusNext) statusNext[(uint64_t)tile * kBins + d] = 0;  // ready for the next pass
-#endif
   }
   lds_barrier();
   THRS_STAMP(5);
@@ -1103,24 +1045,12 @@ __device__ __forceinline__ void pass_tile(
       // out of the round loop as 32 live registers and spilled)
 #pragma unroll
       for (int j = 0; j < (KPT + 1) / 2; ++j) pin(sl[j]);
-#if THRS_RELOAD_KEYS
-      // re-read this round's keys from the tile's input (L2 / Infinity Cache
-      // hits) rather than holding KPT keys in registers across the walk
-      const uint64_t chunkBase = keyStart + w * CHUNK;
-#endif
 #pragma unroll
       for (int j = 0; j < KPT; ++j) {
         const uint32_t slot = slot_of(j);
         if ((slot >> STAGE_SHIFT) == (uint32_t)r) {
-#if THRS_RELOAD_KEYS
-          // padding items of a partial tile (j*64 >= lim) lie past n: never read them
-          const bool real = full || j * 64 < lim;
-          stage_k[slot & (STAGE - 1)] = real ? keysIn[chunkBase + j * 64 + lane] : (U)0;
-          if constexpr (VB != 0) stage_v[slot & (STAGE - 1)] = real ? valsIn[chunkBase + j * 64 + lane] : VW{};
-#else
           stage_k[slot & (STAGE - 1)] = k[j];
           if constexpr (VB != 0) stage_v[slot & (STAGE - 1)] = v[j];
-#endif
         }
       }
       lds_barrier();
@@ -1139,7 +1069,7 @@ __device__ __forceinline__ void pass_tile(
       }
       if constexpr (VB != 0) valsOut[dst] = vv;
     };
-    if ((VB == 0 || THRS_WO_FULL_PAIRS) && full) {
+    if (VB == 0 && full) {
       // whole tile: no lane conditions, so each batch's stage reads,
       // then its offset reads, are issued back to back (a read under a lane
       // condition is waited for before the next one issues)
@@ -1181,7 +1111,6 @@ __device__ __forceinline__ void pass_tile(
     }
     if (r + 1 < ROUNDS) lds_barrier();
   }
-#if THRS_LATE_CLEAR
   // Clear this tile's rows of the next pass's tables only now: a store issued
   // before the look-back barrier waits for room in the CU's in-order vector
   // memory queue (behind the other workgroup's loads) and holds the barrier.
@@ -1195,7 +1124,6 @@ __device__ __forceinline__ void pass_tile(
       }
     }
   }
-#endif
 #ifdef THRS_STAMPS
 #ifndef THRS_STAMPS_NOWAIT
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // slot 6 = stores drained (NOWAIT: issued)
@@ -1494,6 +1422,13 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
   }
 }
 
+// Last launch of every sort: ORs the sort's device error word into the
+// device's sticky word (host-mapped, thrs_capi.h "Device-side failures").
+__global__ void thrs_err_publish(const uint32_t* __restrict__ err, uint32_t* __restrict__ sticky) {
+  const uint32_t e = *err;
+  if (e) __hip_atomic_fetch_or(sticky, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // ================================================================ self-probe
 // Does ds_add_rtn_u32 hand out values in lane order when several lanes of one
 // fully active wave hit the same LDS word?  Compared against the ballot-match
@@ -1524,4 +1459,5 @@ __global__ __launch_bounds__(256) void thrs_probe_lds_order(uint32_t* bad, int i
   if (b) atomicAdd(bad, b);
 }
 
+}  // namespace
 }  // namespace thrs_dev
