@@ -86,7 +86,21 @@ typedef struct thrs_options {
                             plane (12 instead of 16 bytes per key over the two
                             passes, 6 instead of 8 in the local sort).  AUTO = ON
                             where it applies; OFF = full keys                      */
-  int32_t reserved[2];   /* zero */
+  int32_t keyRange;      /* 1: the caller promises rangeLo <= img(k) <= rangeHi for every
+                            key, img(k) = getKeyBits(k) ^ (descending ? ~0 : 0) (fpKey.hpp
+                            and kernel.cu:18-24), and a full-window sort orders by
+                            ((img - rangeLo) << sh), sh = the leading zero bits of
+                            rangeHi - rangeLo: monotone on the range, so the output is
+                            the same bytes, while keys confined to a narrow range fill
+                            the bucket path's 16-bit buckets evenly (the multi-GPU
+                            finish, tinyhipradixsort_amd/dist.py).  rangeLo == rangeHi:
+                            every key is equal, the sort returns at once.  Ignored
+                            where it does not apply (windows; 4-byte keys-only sorts
+                            on the 32-bit local sort).  A false promise gives
+                            unspecified output.  0 = no range.                     */
+  int32_t reserved;      /* zero */
+  uint64_t rangeLo;
+  uint64_t rangeHi;
 } thrs_options;
 
 /* == RadixSort::TemporaryBufferDef (tinyhipradixsort.hpp:806-832).

@@ -113,7 +113,8 @@ class _CConfig(ctypes.Structure):
 class _COptions(ctypes.Structure):
     _fields_ = [("path", ctypes.c_int32), ("localGeometry", ctypes.c_int32), ("segmented", ctypes.c_int32),
                 ("tileClaims", ctypes.c_int32), ("rank", ctypes.c_int32), ("planes", ctypes.c_int32),
-                ("reserved", ctypes.c_int32 * 2)]
+                ("keyRange", ctypes.c_int32), ("reserved", ctypes.c_int32), ("rangeLo", ctypes.c_uint64),
+                ("rangeHi", ctypes.c_uint64)]
 
 
 @dataclass
@@ -127,6 +128,9 @@ class Options:
     tileClaims: str = "auto"      # auto | xcd_blocks | ticket
     rank: str = "auto"            # auto | atomic | ballot
     planes: str = "auto"          # auto | on | off
+    # key range promise (thrs_options.keyRange): every key's image
+    # getKeyBits(k) ^ (descending ? ~0 : 0) lies in [rangeLo, rangeHi]; None = no promise
+    keyRange: "tuple[int, int] | None" = None
 
     _ENUMS = {"path": ("auto", "lsd", "bucket"), "localGeometry": ("auto", "big", "small", "big32", "count16", "rank16", "wide16"),
               "segmented": ("auto", "top_only", "none"), "tileClaims": ("auto", "xcd_blocks", "ticket"),
@@ -139,6 +143,9 @@ class Options:
             if v not in names:
                 raise ThrsError(-1, f"Options.{f}: {v!r} is not one of {names}")
             setattr(o, f, names.index(v))
+        if self.keyRange is not None:
+            lo, hi = (int(x) for x in self.keyRange)
+            o.keyRange, o.rangeLo, o.rangeHi = 1, lo, hi
         return o
 
 

@@ -155,7 +155,8 @@ bool valid_options(const thrs_options& o) {
   return o.path >= THRS_PATH_AUTO && o.path <= THRS_PATH_BUCKET && o.localGeometry >= THRS_LOCAL_AUTO &&
          o.localGeometry <= THRS_LOCAL_WIDE16 && o.segmented >= THRS_SEG_AUTO && o.segmented <= THRS_SEG_NONE &&
          o.tileClaims >= THRS_CLAIMS_AUTO && o.tileClaims <= THRS_CLAIMS_TICKET && o.rank >= THRS_RANK_AUTO &&
-         o.rank <= THRS_RANK_BALLOT && o.planes >= THRS_PLANES_AUTO && o.planes <= THRS_PLANES_OFF;
+         o.rank <= THRS_RANK_BALLOT && o.planes >= THRS_PLANES_AUTO && o.planes <= THRS_PLANES_OFF &&
+         (o.keyRange == 0 || (o.keyRange == 1 && o.rangeLo <= o.rangeHi));
 }
 
 // Scratch is sized for the larger of the keys-only and pairs tile plans so
@@ -188,6 +189,11 @@ int sort_impl(const thrs_config* cfg, const thrs_options* options, void* keys, v
   if (nPass == 0) return THRS_SUCCESS;
   if (!keys || !tmp || (pairs && !vals)) return THRS_ERROR_INVALID_VALUE;
   const int vb = pairs ? value_bytes_of(cfg->valueType) : 0;
+  if (opt.keyRange == 1) {
+    if (kb == 4 && opt.rangeHi > 0xFFFFFFFFull) return THRS_ERROR_INVALID_VALUE;
+    // every key has one image: the stable sort is the identity (full window)
+    if (opt.rangeLo == opt.rangeHi && startBits == 0 && endBits >= width) return THRS_SUCCESS;
+  }
   const Plan plan = make_plan(cfg->keyType, vb, n);
   const bool desc = cfg->sortOrder == THRS_ORDER_DESCENDING;
   // [pSumBuffer = scratch][keyOut][valueOut], exactly as getTemporaryBufferBytes

@@ -245,6 +245,19 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   // = lo u16[n] | lo2 u16[n], the u8 plane hi[n] at the end of the scratch
   const bool planes = local16 && segA && opt.planes != THRS_PLANES_OFF &&
                       plan.scratchBytes - plan.hiPlaneOff >= (uint64_t)n;
+  // The key range (thrs_options.keyRange, thrs_kernels.hpp KeyMap): for
+  // full-window sorts, except the 32-bit local sort (it sorts the keys
+  // themselves and pads with keys)
+  const bool local32 = bucket && kBucket32 && VB == 0 && !local16;
+  const bool ranged = opt.keyRange == 1 && fullWindow && !counts && !local32;
+  KeyMap<U> km{orderMask, (U)0, 0u};
+  if (ranged) {
+    const U span = (U)opt.rangeHi - (U)opt.rangeLo;  // > 0 (sort_impl returns at once for 0)
+    km.lo = (U)opt.rangeLo;
+    km.sh = sizeof(U) == 4 ? (uint32_t)__builtin_clz((uint32_t)span) : (uint32_t)__builtin_clzll((uint64_t)span);
+  }
+  const KeyMap<U> kid{(U)0, (U)0, 0u};  // image-space input (the planes codec)
+  const KeyMap<uint32_t> km32{(uint32_t)km.mask, (uint32_t)km.lo, km.sh};
   uint16_t* loP = static_cast<uint16_t*>(keyOutBuf);
   uint16_t* lo2P = loP + n;
   uint8_t* hiP = reinterpret_cast<uint8_t*>(scratch + plan.hiPlaneOff);
@@ -347,7 +360,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     const int hgrid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cu_count() * THRS_HIST_GRID_MULT));
     if (bucket) {
       hipLaunchKernelGGL(thrs_hist_joint<KT>, dim3(hgrid), dim3(kHistThreads), kJointLds, stream,
-                         static_cast<const U*>(keys), n, orderMask, startBits + 8 * nLow, vec, joint,
+                         static_cast<const U*>(keys), n, km, startBits + 8 * nLow, vec, joint,
                          reinterpret_cast<uint32_t*>(hyb + kSegHistAOff), reinterpret_cast<uint32_t*>(hyb + kRowHistOff));
       const uint32_t cap = kBucket64 ? Loc64::CAP : smallLocal ? LocSmall::CAP : wide16 ? Loc16Wide::CAP : LocBig::CAP;
       if (VB || local16 || kBucket64) {
@@ -368,11 +381,11 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
       }
       // the low digits' histograms + bases: needed only on the fallback path
       hipLaunchKernelGGL(thrs_hist<KT>, dim3(hgrid), dim3(kHistThreads), histLds, stream, static_cast<const U*>(keys),
-                         n, orderMask, startBits, nLow, vec, hist, meta + kMetaFallback);
+                         n, km, startBits, nLow, vec, hist, meta + kMetaFallback);
       hipLaunchKernelGGL(thrs_scan, dim3(1), dim3(kThreads), 0, stream, hist, base, nLow, meta + kMetaFallback);
     } else {
       hipLaunchKernelGGL(thrs_hist<KT>, dim3(hgrid), dim3(kHistThreads), histLds, stream, static_cast<const U*>(keys),
-                         n, orderMask, startBits, nPass, vec, hist, nullptr);
+                         n, km, startBits, nPass, vec, hist, nullptr);
       hipLaunchKernelGGL(thrs_scan, dim3(1), dim3(kThreads), 0, stream, hist, base, nPass, nullptr);
     }
     if (counts && hipMemcpyAsync(counts, hist, kBins * sizeof(uint32_t), hipMemcpyDeviceToDevice, stream) != hipSuccess)
@@ -396,7 +409,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     const bool fallbackOnly = gate && (gateMask == kGateFallback || gateMask == kGateMode1);
     const bool persist = bucket && fallbackOnly && !useXb;
     hipLaunchKernelGGL(persist ? kernelPersist : kernel, dim3(persist ? gridPersist : grid), dim3(G::THREADS), lds,
-                       stream, kin, kout, vin, vout, n, orderMask, startBits + 8 * p, base + p * kBins, status[p & 1],
+                       stream, kin, kout, vin, vout, n, km, startBits + 8 * p, base + p * kBins, status[p & 1],
                        next, useXb ? reinterpret_cast<uint32_t*>(claim + p * plan.claimBytes) : counters + p, err, g,
                        g_stamps ? g_stamps + (uint64_t)p * plan.nTiles * kStampSlots : nullptr, gate, gateMask);
   };
@@ -464,9 +477,9 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                           const uint32_t* gate, uint32_t gateMask, int codec = kCodecKeys) {
       ProfScope prof(stream, gateMask == kGateMode1 ? 3 : 1);  // fallback-only launches are timed apart
       auto kern = codec == kCodecSplit ? skSplit : codec == kCodecPlanes ? skPlanes : sk;
-      // kCodecPlanes: image-space input (orderMask 0), digit at bits 16-23 of k'
+      // kCodecPlanes: image-space input (identity map), digit at bits 16-23 of k'
       hipLaunchKernelGGL(kern, dim3((uint32_t)segPerCU * cu_count()), dim3(G::THREADS), lds, stream, kin, kout, vin,
-                         vout, codec == kCodecPlanes ? (U)0 : orderMask, codec == kCodecPlanes ? 16 : startBits + 8 * p,
+                         vout, codec == kCodecPlanes ? kid : km, codec == kCodecPlanes ? 16 : startBits + 8 * p,
                          reinterpret_cast<uint32_t*>(hyb + infoOff), reinterpret_cast<const uint32_t*>(hyb + baseOff),
                          status[p & 1], err, grp[p & 1], gate, gateMask, hiP);
     };
@@ -518,18 +531,19 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
         } else if constexpr (VB == 4) {
           auto lk = atomicRank ? thrs_local_pairs<true, LG> : thrs_local_pairs<false, LG>;
           hipLaunchKernelGGL(lk, dim3((uint32_t)maxChunks), dim3(LG::THREADS), llds, stream,
-                             reinterpret_cast<uint32_t*>(K), reinterpret_cast<uint32_t*>(V), (uint32_t)orderMask,
+                             reinterpret_cast<uint32_t*>(K), reinterpret_cast<uint32_t*>(V), km32,
                              chunkOff, chunkB0, meta);
         } else {
           auto lk = atomicRank ? thrs_local<KT, true, LG> : thrs_local<KT, false, LG>;
-          hipLaunchKernelGGL(lk, dim3((uint32_t)maxChunks), dim3(LG::THREADS), llds, stream, K, orderMask, startBits,
+          hipLaunchKernelGGL(lk, dim3((uint32_t)maxChunks), dim3(LG::THREADS), llds, stream, K, km, startBits,
                              nLow, chunkOff, chunkB0, meta, g_lstamps);
         }
       };
       if constexpr (kBucket64) {
         auto lk = atomicRank ? thrs_local64<KT, VB, true> : thrs_local64<KT, VB, false>;
         hipLaunchKernelGGL(lk, dim3((uint32_t)maxChunks), dim3(Loc64::THREADS), Loc64::LDS, stream,
-                           reinterpret_cast<uint64_t*>(K), reinterpret_cast<uint64_t*>(V), (uint64_t)orderMask,
+                           reinterpret_cast<uint64_t*>(K), reinterpret_cast<uint64_t*>(V),
+                           KeyMap<uint64_t>{(uint64_t)km.mask, (uint64_t)km.lo, km.sh},
                            chunkOff, chunkB0, meta);
       } else if (local16) {
         if constexpr (KT == 0 && VB == 0) {
@@ -539,17 +553,17 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
             // planes off / mode 2: the items are the keys themselves (in place)
             auto lk = planes ? thrs_local_count16<true> : thrs_local_count16<false>;
             hipLaunchKernelGGL(lk, dim3(cgrid), dim3(LocCount::THREADS), LocCount::LDS, stream,
-                               reinterpret_cast<uint32_t*>(K), n, (uint32_t)orderMask, chunkOff, chunkB0, meta,
+                               reinterpret_cast<uint32_t*>(K), n, km32, chunkOff, chunkB0, meta,
                                static_cast<const uint16_t*>(lo2P), joint);
           } else if (wide16) {
             auto lk = atomicRank ? thrs_local16<true, Loc16Wide> : thrs_local16<false, Loc16Wide>;
             hipLaunchKernelGGL(lk, dim3((uint32_t)maxChunks), dim3(Loc16Wide::THREADS), Loc16Wide::LDS, stream,
-                               reinterpret_cast<uint32_t*>(K), (uint32_t)orderMask, chunkOff, chunkB0, meta,
+                               reinterpret_cast<uint32_t*>(K), km32, chunkOff, chunkB0, meta,
                                planes ? static_cast<const uint16_t*>(lo2P) : nullptr);
           } else {
             auto lk = atomicRank ? thrs_local16<true, Loc16> : thrs_local16<false, Loc16>;
             hipLaunchKernelGGL(lk, dim3((uint32_t)maxChunks), dim3(Loc16::THREADS), Loc16::LDS, stream,
-                               reinterpret_cast<uint32_t*>(K), (uint32_t)orderMask, chunkOff, chunkB0, meta,
+                               reinterpret_cast<uint32_t*>(K), km32, chunkOff, chunkB0, meta,
                                planes ? static_cast<const uint16_t*>(lo2P) : nullptr);
           }
         }

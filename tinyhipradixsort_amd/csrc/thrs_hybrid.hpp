@@ -79,7 +79,7 @@ __device__ __forceinline__ uint32_t hj_seg_pos(uint32_t n, uint32_t G, uint32_t 
 
 template <int KT>
 __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename KeyTraits<KT>::U* __restrict__ keys,
-                                                                uint32_t n, typename KeyTraits<KT>::U orderMask,
+                                                                uint32_t n, KeyMap<typename KeyTraits<KT>::U> km,
                                                                 int bucketShift, int vec,
                                                                 uint32_t* __restrict__ joint,
                                                                 uint32_t* __restrict__ segHist /* [8][256] */,
@@ -99,7 +99,7 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
 
   const uint32_t lane = tid & 63;
   auto bucket_of = [&](U k) -> uint32_t {
-    return (uint32_t)((KeyTraits<KT>::bits(k) ^ orderMask) >> bucketShift) & 0xFFFFu;
+    return (uint32_t)(kimg<KT>(km, k) >> bucketShift) & 0xFFFFu;
   };
   // Adds are wave-aggregated as in wave_count_items (sorted input would
   // otherwise make every add a 64-way same-address conflict): a wave whose 16
@@ -659,7 +659,9 @@ __device__ __forceinline__ LocChunk loc_chunk(uint32_t c, int nLow, const uint32
 
 // padding image: ones in every low digit, (b0 - 1) in the second digit (its
 // multi-round digit is 255), zero elsewhere -- bits 24..31 are never a local
-// digit and stay 0, so the image is never 0x7FFFFFFF (the one unbits32 miss)
+// digit and stay 0, so the image is never 0x7FFFFFFF (the one unbits32 miss).
+// (thrs_local sorts the keys themselves, so it runs only without a key range:
+// the padding must be a key.)
 template <int KT>
 __device__ __forceinline__ uint32_t loc_pad(uint32_t b0, int nLow, int startBits, uint32_t orderMask) {
   const uint32_t padT = (((1u << (8 * nLow)) - 1u) << startBits) | (((b0 - 1u) & 0xFFu) << (startBits + 8 * nLow));
@@ -724,7 +726,7 @@ __device__ __forceinline__ void loc_stamp(uint64_t* st, int i) {
 // the chunk's items in sorted order; returns the number of rounds run.
 template <int KT, bool ATOMIC_RANK, typename LG>
 __device__ __forceinline__ int loc_rounds(typename KeyTraits<KT>::U (&k)[LG::KPT], const LocChunk& ch,
-                                          typename KeyTraits<KT>::U orderMask, int startBits, int nLow,
+                                          KeyMap<typename KeyTraits<KT>::U> km, int startBits, int nLow,
                                           unsigned char* smem, uint64_t* st) {
   using U = typename KeyTraits<KT>::U;
   constexpr int KPT = LG::KPT;
@@ -745,7 +747,7 @@ __device__ __forceinline__ int loc_rounds(typename KeyTraits<KT>::U (&k)[LG::KPT
     const int shift = r < nLow ? startBits + 8 * r : startBits + 8 * nLow;
     const uint32_t sub = r < nLow ? 0u : ch.b0;
     auto digit_of = [&](U key) -> uint32_t {
-      return ((uint32_t)((KeyTraits<KT>::bits(key) ^ orderMask) >> shift) - sub) & 0xFFu;
+      return ((uint32_t)(kimg<KT>(km, key) >> shift) - sub) & 0xFFu;
     };
 #pragma unroll
     for (int i = 0; i < kBins / 64; ++i) cnt[i * 64 + lane] = 0;
@@ -838,12 +840,12 @@ __device__ __forceinline__ int loc_rounds(typename KeyTraits<KT>::U (&k)[LG::KPT
 template <int KT, bool ATOMIC_RANK, typename LG>
 __device__ __forceinline__ void loc_sort_chunk(typename KeyTraits<KT>::U (&k)[LG::KPT],
                                                typename KeyTraits<KT>::U* __restrict__ keys, const LocChunk& ch,
-                                               typename KeyTraits<KT>::U orderMask, int startBits, int nLow,
+                                               KeyMap<typename KeyTraits<KT>::U> km, int startBits, int nLow,
                                                unsigned char* smem, uint64_t* st = nullptr) {
   using U = typename KeyTraits<KT>::U;
   constexpr int KPT = LG::KPT;
   constexpr uint32_t CHUNK = 64 * KPT;
-  const int roundsRun = loc_rounds<KT, ATOMIC_RANK, LG>(k, ch, orderMask, startBits, nLow, smem, st);
+  const int roundsRun = loc_rounds<KT, ATOMIC_RANK, LG>(k, ch, km, startBits, nLow, smem, st);
   const U* stage = reinterpret_cast<const U*>(smem);
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -874,7 +876,7 @@ __device__ __forceinline__ void loc_sort_chunk(typename KeyTraits<KT>::U (&k)[LG
 
 template <int KT, bool ATOMIC_RANK, typename LG>
 __global__ __launch_bounds__(LG::THREADS) void thrs_local(typename KeyTraits<KT>::U* __restrict__ keys,
-                                                          typename KeyTraits<KT>::U orderMask, int startBits,
+                                                          KeyMap<typename KeyTraits<KT>::U> km, int startBits,
                                                           int nLow, const uint32_t* __restrict__ chunkOff,
                                                           const uint32_t* __restrict__ chunkB0,
                                                           uint32_t* __restrict__ meta, uint64_t* __restrict__ stamps) {
@@ -890,7 +892,7 @@ __global__ __launch_bounds__(LG::THREADS) void thrs_local(typename KeyTraits<KT>
   const LocChunk ch = loc_chunk<KT>(c, nLow, chunkOff, chunkB0);
   if (ch.size == 0) return;
   U k[LG::KPT];
-  loc_load<KT, LG>(k, keys, ch, loc_pad<KT>(ch.b0, nLow, startBits, (uint32_t)orderMask));
+  loc_load<KT, LG>(k, keys, ch, loc_pad<KT>(ch.b0, nLow, startBits, (uint32_t)km.mask));
 #ifdef THRS_STAMPS
   if (st) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -903,7 +905,7 @@ __global__ __launch_bounds__(LG::THREADS) void thrs_local(typename KeyTraits<KT>
     }
   }
 #endif
-  loc_sort_chunk<KT, ATOMIC_RANK, LG>(k, keys, ch, orderMask, startBits, nLow, smem, st);
+  loc_sort_chunk<KT, ATOMIC_RANK, LG>(k, keys, ch, km, startBits, nLow, smem, st);
 }
 
 // ------------------------------------------------- local sort, 16-bit items
@@ -943,7 +945,7 @@ static_assert(Loc16::CAP == LocBig::CAP, "same chunk capacity as the 32-bit geom
 using Loc16Wide = Loc16G<THRS_WIDE_W, THRS_WIDE_K, 4, THRS_WIDE_K / 2>;
 
 template <bool ATOMIC_RANK, typename LG>
-__global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(LG::WPE))) void thrs_local16(uint32_t* __restrict__ keys, uint32_t orderMask,
+__global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(LG::WPE))) void thrs_local16(uint32_t* __restrict__ keys, KeyMap<uint32_t> km,
                                                             const uint32_t* __restrict__ chunkOff,
                                                             const uint32_t* __restrict__ chunkB0,
                                                             const uint32_t* __restrict__ meta,
@@ -1001,8 +1003,8 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(LG:
 #pragma unroll
       for (int jj = 0; jj < LB; jj += 2) {
         const int j = h + jj;
-        const uint32_t a = (j * 64 < lim) ? ((raw[jj] ^ orderMask) & 0xFFFFu) : 0xFFFFu;
-        const uint32_t b = (j + 1 < KPT && (j + 1) * 64 < lim) ? ((raw[jj + 1] ^ orderMask) & 0xFFFFu) : 0xFFFFu;
+        const uint32_t a = (j * 64 < lim) ? (kimg<0>(km, raw[jj]) & 0xFFFFu) : 0xFFFFu;
+        const uint32_t b = (j + 1 < KPT && (j + 1) * 64 < lim) ? (kimg<0>(km, raw[jj + 1]) & 0xFFFFu) : 0xFFFFu;
         it[j >> 1] = a | (b << 16);
       }
     }
@@ -1100,7 +1102,7 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(LG:
     for (int jj = 0; jj < LB; ++jj) o[jj] = stw[(h + jj) * LG::ROW];
 #pragma unroll
     for (int jj = 0; jj < LB; ++jj)
-      if ((h + jj) * 64 < lim) src[(h + jj) * 64] = (hiBits | o[jj]) ^ orderMask;
+      if ((h + jj) * 64 < lim) src[(h + jj) * 64] = kinv_int(km, hiBits | o[jj]);
   }
 }
 
@@ -1160,7 +1162,7 @@ __device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
 // nobody reads (the bucket histogram, consumed by thrs_plan before this launch).
 template <bool PLANE>
 __global__ __launch_bounds__(LocCount::THREADS) void thrs_local_count16(
-    uint32_t* __restrict__ keys, uint32_t n, uint32_t orderMask, const uint32_t* __restrict__ chunkOff,
+    uint32_t* __restrict__ keys, uint32_t n, KeyMap<uint32_t> km, const uint32_t* __restrict__ chunkOff,
     const uint32_t* __restrict__ chunkB0, const uint32_t* __restrict__ meta, const uint16_t* __restrict__ lo,
     uint32_t* __restrict__ sink) {
   using LC = LocCount;
@@ -1228,7 +1230,7 @@ __global__ __launch_bounds__(LocCount::THREADS) void thrs_local_count16(
       pin(rc);
 #pragma unroll
       for (int k = 0; k < IT; ++k) {
-        const uint32_t v = rc + (uint32_t)k * LC::THREADS < size ? (PLANE ? it[k] : (it[k] ^ orderMask) & 0xFFFFu) : NONE;
+        const uint32_t v = rc + (uint32_t)k * LC::THREADS < size ? (PLANE ? it[k] : kimg<0>(km, it[k]) & 0xFFFFu) : NONE;
         const bool uni = __all(__builtin_amdgcn_readfirstlane(v) == v);
         const uint32_t add = uni ? (lane == 0 ? 64u : 0u) : 1u;
         if (v != NONE && add != 0)
@@ -1290,7 +1292,7 @@ __global__ __launch_bounds__(LocCount::THREADS) void thrs_local_count16(
       for (int k = 0; k < IT; ++k) {
         const uint32_t x = max(wave_incl_max(y[k]), carry);
         carry = lane63(x);
-        *reinterpret_cast<uint32_t*>(dbase + min(d0 + 64u * k, size - 1) * 4u) = (hiBits | x) ^ orderMask;
+        *reinterpret_cast<uint32_t*>(dbase + min(d0 + 64u * k, size - 1) * 4u) = kinv_int(km, hiBits | x);
       }
     } else {
       // empty chunk: as many (dummy) stores as a full one, so the vmcnt
@@ -1321,7 +1323,7 @@ __global__ __launch_bounds__(LocCount::THREADS) void thrs_local_count16(
 // path: +0 and -0 share one image and could not be rebuilt bit-exactly.)
 template <bool ATOMIC_RANK, typename LG>
 __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(4))) void thrs_local_pairs(
-    uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, uint32_t orderMask,
+    uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, KeyMap<uint32_t> km,
     const uint32_t* __restrict__ chunkOff, const uint32_t* __restrict__ chunkB0, const uint32_t* __restrict__ meta) {
   constexpr int KPT = LG::KPT;
   constexpr uint32_t CHUNK = 64 * KPT;
@@ -1351,9 +1353,9 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(4))
 #pragma unroll
   for (int j = 0; j < KPT; ++j) {
     const uint32_t pos = myOff + j * 64;
-    it[j] = (j * 64 < lim) ? (((it[j] ^ orderMask) << 16) | pos) : 0xFFFF0000u;  // padding: digits 255
+    it[j] = (j * 64 < lim) ? ((kimg<0>(km, it[j]) << 16) | pos) : 0xFFFF0000u;  // padding: digits 255
   }
-  loc_rounds<0, ATOMIC_RANK, LG>(it, ch, 0u, 16, 2, smem, nullptr);
+  loc_rounds<0, ATOMIC_RANK, LG>(it, ch, KeyMap<uint32_t>{0u, 0u, 0u}, 16, 2, smem, nullptr);
   pin(reinterpret_cast<uint32_t&>(lim));
   // values of this thread's positions (the item registers are free again;
   // loading them with the keys would spill: EXPERIMENTS row 31)
@@ -1376,7 +1378,7 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(4))
       const int j = j0 + jj;
       if (j < KPT) {
         id[j / 2] |= (j * 64 < lim ? (o[jj] & 0xFFFFu) : 0u) << (16 * (j & 1));
-        if (j * 64 < lim) ksrc[j * 64] = (hiImg | (o[jj] >> 16)) ^ orderMask;
+        if (j * 64 < lim) ksrc[j * 64] = kinv_int(km, hiImg | (o[jj] >> 16));
       }
     }
   }
@@ -1417,7 +1419,7 @@ static_assert(Loc64::CAP < 65536, "positions are carried in 16 bits");
 
 template <int KT, int VB, bool ATOMIC_RANK>
 __global__ __launch_bounds__(Loc64::THREADS) void thrs_local64(uint64_t* __restrict__ keys,
-                                                              uint64_t* __restrict__ vals, uint64_t orderMask,
+                                                              uint64_t* __restrict__ vals, KeyMap<uint64_t> km,
                                                               const uint32_t* __restrict__ chunkOff,
                                                               const uint32_t* __restrict__ chunkB0,
                                                               const uint32_t* __restrict__ meta) {
@@ -1451,7 +1453,7 @@ __global__ __launch_bounds__(Loc64::THREADS) void thrs_local64(uint64_t* __restr
   load_run<KPT>(it, keys + start, myOff, size, limw);
 #pragma unroll
   for (int j = 0; j < KPT; ++j) {
-    const uint64_t img = KeyTraits<KT>::bits(it[j]) ^ orderMask;
+    const uint64_t img = kimg<KT>(km, it[j]);
     it[j] = (j * 64 < lim) ? ((img << 16) | (uint64_t)(myOff + j * 64)) : ~0xFFFFull;
   }
   for (int r = 0; r < 6; ++r) {
@@ -1533,7 +1535,7 @@ __global__ __launch_bounds__(Loc64::THREADS) void thrs_local64(uint64_t* __restr
   if constexpr (!PERMUTE_KEYS) {
 #pragma unroll
     for (int j = 0; j < KPT; ++j)
-      if (j * 64 < lim) kdst[j * 64] = (hiImg | (it[j] >> 16)) ^ orderMask;  // u64: image == key ^ orderMask
+      if (j * 64 < lim) kdst[j * 64] = kinv_int(km, hiImg | (it[j] >> 16));  // u64: getKeyBits is the identity
   }
   if constexpr (PERMUTE_KEYS || VB == 8) {
     // carried positions; then each permuted array goes through the stage

@@ -63,6 +63,29 @@ template <> struct KeyTraits<3> {  // F64
   }
 };
 
+// The image a sort orders by: getKeyBits (above) XOR the descending mask
+// (kernel.cu:18-24), optionally restated on a range the caller promises
+// (thrs_options.keyRange -- the multi-GPU finish, where a rank's keys lie in a
+// known [lo, hi]):  img(k) = ((getKeyBits(k) ^ mask) - lo) << sh, sh = the
+// leading zero bits of hi - lo.  On the range it is monotone and one-to-one,
+// so sorting by img is sorting by the key, and the range's keys fill the
+// whole image width (the bucket path's 16-bit buckets stay balanced).
+// Without a range lo = sh = 0.
+template <typename U> struct KeyMap {
+  U mask;
+  U lo;
+  uint32_t sh;
+};
+template <int KT>
+__device__ __forceinline__ typename KeyTraits<KT>::U kimg(const KeyMap<typename KeyTraits<KT>::U>& m,
+                                                          typename KeyTraits<KT>::U k) {
+  return ((KeyTraits<KT>::bits(k) ^ m.mask) - m.lo) << m.sh;
+}
+// the key whose image is y (u32 / u64: getKeyBits is the identity)
+template <typename U> __device__ __forceinline__ U kinv_int(const KeyMap<U>& m, U y) {
+  return ((y >> m.sh) + m.lo) ^ m.mask;
+}
+
 // value payloads: 4, 8 or 16 bytes moved as opaque words
 template <int VB> struct ValueWord;
 template <> struct ValueWord<4> { using T = uint32_t; };
@@ -278,7 +301,7 @@ constexpr int kHistThreads = 1024;
 template <int KB> constexpr int hist_copies() { return KB == 4 ? THRS_HIST_COPIES : THRS_HIST_COPIES / 2; }
 template <int KT>
 __global__ __launch_bounds__(kHistThreads) void thrs_hist(const typename KeyTraits<KT>::U* __restrict__ keys,
-                                                          uint32_t n, typename KeyTraits<KT>::U orderMask,
+                                                          uint32_t n, KeyMap<typename KeyTraits<KT>::U> km,
                                                           int startBits, int nPass, int vec,
                                                           uint32_t* __restrict__ hist,
                                                           const uint32_t* __restrict__ gate = nullptr) {
@@ -294,7 +317,7 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist(const typename KeyTrai
   uint32_t* my = s_hist + (tid % COPIES);
 
   auto count = [&](U k) {
-    const U b = KeyTraits<KT>::bits(k) ^ orderMask;
+    const U b = kimg<KT>(km, k);
 #pragma unroll
     for (int p = 0; p < NP_MAX; ++p) {
       if (p < nPass) {
@@ -704,7 +727,7 @@ struct GroupWalk {
 //                 second digit (bits 16-23), which this pass sorts by, is
 //                 implied by the output position
 //   kCodecPlanes  in: the two planes, as k' = top byte << 16 | low 16 bits (the
-//                 pass's digit at shift 16, orderMask 0); out: the low 16 bits
+//                 pass's digit at shift 16, identity map); out: the low 16 bits
 //                 to a u16 plane -- the local sort rebuilds the top 16 bits
 //                 from its chunk's bucket
 // 7 + 5 bytes per key instead of 8 + 8 for the two top-digit passes, 6
@@ -766,7 +789,7 @@ template <int KT, int VB, typename ST, bool ATOMIC_RANK, typename Mid, int CODEC
 __device__ __forceinline__ void pass_tile(
     const typename KeyTraits<KT>::U* __restrict__ keysIn, typename KeyTraits<KT>::U* __restrict__ keysOut,
     const typename ValueWord<VB>::T* __restrict__ valsIn, typename ValueWord<VB>::T* __restrict__ valsOut,
-    uint64_t keyStart, uint32_t valid, typename KeyTraits<KT>::U orderMask, int shift, uint32_t myBase,
+    uint64_t keyStart, uint32_t valid, KeyMap<typename KeyTraits<KT>::U> km, int shift, uint32_t myBase,
     ST* __restrict__ status, ST* __restrict__ statusNext, uint32_t* __restrict__ errFlag, uint32_t tile,
     uint32_t chainStart, const GroupTables<ST>& grp, unsigned char* smem, uint64_t* __restrict__ stamps,
     typename KeyTraits<KT>::U (&k)[PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::KPT],
@@ -819,7 +842,7 @@ __device__ __forceinline__ void pass_tile(
   int32_t lim = (int32_t)valid - (int32_t)(w * CHUNK + lane);
   pin(reinterpret_cast<uint32_t&>(lim));
   auto digit_of = [&](U key, int j) -> uint32_t {
-    uint32_t dd = (uint32_t)((KeyTraits<KT>::bits(key) ^ orderMask) >> shift) & 0xFFu;
+    uint32_t dd = (uint32_t)(kimg<KT>(km, key) >> shift) & 0xFFu;
     if (!full) dd = (j * 64 < lim) ? dd : 0xFFu;  // padding sorts after every real key
     return dd;
   };
@@ -1059,7 +1082,7 @@ __device__ __forceinline__ void pass_tile(
     auto put = [&](U key, uint32_t i, uint32_t off, const VW& vv) __attribute__((always_inline)) {
       const uint32_t dst = off + (uint32_t)r * STAGE + i;
       if constexpr (CODEC == kCodecSplit) {
-        const uint32_t img = (uint32_t)(KeyTraits<KT>::bits(key) ^ orderMask);
+        const uint32_t img = (uint32_t)kimg<KT>(km, key);
         reinterpret_cast<uint16_t*>(keysOut)[dst] = (uint16_t)img;
         hiOut[dst] = (uint8_t)(img >> 24);
       } else if constexpr (CODEC == kCodecPlanes) {
@@ -1087,7 +1110,7 @@ __device__ __forceinline__ void pass_tile(
           }
 #pragma unroll
         for (int b = 0; b < WB; ++b)
-          if (j0 + b < NS) off[b] = s_gofs[(uint32_t)((KeyTraits<KT>::bits(key[b]) ^ orderMask) >> shift) & 0xFFu];
+          if (j0 + b < NS) off[b] = s_gofs[(uint32_t)(kimg<KT>(km, key[b]) >> shift) & 0xFFu];
 #pragma unroll
         for (int b = 0; b < WB; ++b)
           if (j0 + b < NS) put(key[b], (j0 + b) * THREADS + tid, off[b], val[VB ? b : 0]);
@@ -1100,7 +1123,7 @@ __device__ __forceinline__ void pass_tile(
       const uint32_t slot = (uint32_t)r * STAGE + i;
       if (full || slot < valid) {
         const U key = stage_k[i];
-        const uint32_t dd = (uint32_t)((KeyTraits<KT>::bits(key) ^ orderMask) >> shift) & 0xFFu;
+        const uint32_t dd = (uint32_t)(kimg<KT>(km, key) >> shift) & 0xFFu;
         VW vv{};
         if constexpr (VB != 0) vv = stage_v[i];
         put(key, i, s_gofs[dd], vv);
@@ -1146,7 +1169,7 @@ __global__ __launch_bounds__((PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::T
 __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::WPE))) void thrs_pass(
     const typename KeyTraits<KT>::U* __restrict__ keysIn, typename KeyTraits<KT>::U* __restrict__ keysOut,
     const typename ValueWord<VB>::T* __restrict__ valsIn, typename ValueWord<VB>::T* __restrict__ valsOut,
-    uint32_t n, typename KeyTraits<KT>::U orderMask, int shift, const uint32_t* __restrict__ digitBase,
+    uint32_t n, KeyMap<typename KeyTraits<KT>::U> km, int shift, const uint32_t* __restrict__ digitBase,
     ST* __restrict__ status, ST* __restrict__ statusNext, uint32_t* __restrict__ tileCounter,
     uint32_t* __restrict__ errFlag, GroupTables<ST> grp, uint64_t* __restrict__ stamps,
     const uint32_t* __restrict__ gate, uint32_t gateMask) {
@@ -1179,7 +1202,7 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
   typename ValueWord<VB>::T v[VB ? G::KPT : 1];
   load_tile<KT, VB>(keysIn, valsIn, (uint64_t)tile * G::TILE, tile_valid<G::TILE>(n, tile), k, v);
   pass_tile<KT, VB, ST, ATOMIC_RANK>(keysIn, keysOut, valsIn, valsOut, (uint64_t)tile * G::TILE,
-                                     tile_valid<G::TILE>(n, tile), orderMask, shift, myBase, status,
+                                     tile_valid<G::TILE>(n, tile), km, shift, myBase, status,
                                      statusNext, errFlag, tile, 0, grp, smem, stamps, k, v, NoMid{});
 }
 
@@ -1193,7 +1216,7 @@ __global__ __launch_bounds__((PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::T
 __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::WPE))) void thrs_pass_persist(
     const typename KeyTraits<KT>::U* __restrict__ keysIn, typename KeyTraits<KT>::U* __restrict__ keysOut,
     const typename ValueWord<VB>::T* __restrict__ valsIn, typename ValueWord<VB>::T* __restrict__ valsOut,
-    uint32_t n, typename KeyTraits<KT>::U orderMask, int shift, const uint32_t* __restrict__ digitBase,
+    uint32_t n, KeyMap<typename KeyTraits<KT>::U> km, int shift, const uint32_t* __restrict__ digitBase,
     ST* __restrict__ status, ST* __restrict__ statusNext, uint32_t* __restrict__ tileCounter,
     uint32_t* __restrict__ errFlag, GroupTables<ST> grp, uint64_t* __restrict__ stamps,
     const uint32_t* __restrict__ gate, uint32_t gateMask) {
@@ -1218,7 +1241,7 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
     if (tile >= nTiles) break;
     load_tile<KT, VB>(keysIn, valsIn, (uint64_t)tile * G::TILE, tile_valid<G::TILE>(n, tile), k, v);
     pass_tile<KT, VB, ST, ATOMIC_RANK>(keysIn, keysOut, valsIn, valsOut, (uint64_t)tile * G::TILE,
-                                       tile_valid<G::TILE>(n, tile), orderMask, shift, myBase, status,
+                                       tile_valid<G::TILE>(n, tile), km, shift, myBase, status,
                                        statusNext, errFlag, tile, 0, grp, smem, nullptr, k, v, NoMid{});
     lds_barrier();  // stage, s_gofs and s_misc[0] are reused by the next tile
   }
@@ -1296,7 +1319,7 @@ __global__ __launch_bounds__((PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::T
 __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::WPE))) void thrs_pass_xb(
     const typename KeyTraits<KT>::U* __restrict__ keysIn, typename KeyTraits<KT>::U* __restrict__ keysOut,
     const typename ValueWord<VB>::T* __restrict__ valsIn, typename ValueWord<VB>::T* __restrict__ valsOut,
-    uint32_t n, typename KeyTraits<KT>::U orderMask, int shift, const uint32_t* __restrict__ digitBase,
+    uint32_t n, KeyMap<typename KeyTraits<KT>::U> km, int shift, const uint32_t* __restrict__ digitBase,
     ST* __restrict__ status, ST* __restrict__ statusNext, uint32_t* __restrict__ claimState,
     uint32_t* __restrict__ errFlag, GroupTables<ST> grp, uint64_t* __restrict__ stamps,
     const uint32_t* __restrict__ gate, uint32_t gateMask) {
@@ -1331,7 +1354,7 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
     if (tile == kXbDone) break;
     load_tile<KT, VB>(keysIn, valsIn, (uint64_t)tile * G::TILE, tile_valid<G::TILE>(n, tile), k, v);
     pass_tile<KT, VB, ST, ATOMIC_RANK>(keysIn, keysOut, valsIn, valsOut, (uint64_t)tile * G::TILE,
-                                       tile_valid<G::TILE>(n, tile), orderMask, shift, myBase, status,
+                                       tile_valid<G::TILE>(n, tile), km, shift, myBase, status,
                                        statusNext, errFlag, tile, 0, grp, smem, stamps, k, v, NoMid{});
     lds_barrier();  // stage, s_gofs and s_misc[0] are reused by the next tile
   }
@@ -1362,7 +1385,7 @@ __global__ __launch_bounds__((PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::T
 __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::WPE))) void thrs_pass_seg(
     const typename KeyTraits<KT>::U* __restrict__ keysIn, typename KeyTraits<KT>::U* __restrict__ keysOut,
     const typename ValueWord<VB>::T* __restrict__ valsIn, typename ValueWord<VB>::T* __restrict__ valsOut,
-    typename KeyTraits<KT>::U orderMask, int shift, uint32_t* __restrict__ segInfo,
+    KeyMap<typename KeyTraits<KT>::U> km, int shift, uint32_t* __restrict__ segInfo,
     const uint32_t* __restrict__ segBase, ST* __restrict__ status, uint32_t* __restrict__ errFlag,
     GroupTables<ST> grp, const uint32_t* __restrict__ gate, uint32_t gateMask, uint8_t* __restrict__ hiPlane) {
   using U = typename KeyTraits<KT>::U;
@@ -1415,7 +1438,7 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
     g.gpNext = nullptr;
     const uint32_t myBase = segBase[seg * kBins + (tid & 255u)];
     load_tile<KT, VB, CODEC>(keysIn, valsIn, keyStart, valid, k, v, hiPlane);
-    pass_tile<KT, VB, ST, ATOMIC_RANK, NoMid, CODEC>(keysIn, keysOut, valsIn, valsOut, keyStart, valid, orderMask,
+    pass_tile<KT, VB, ST, ATOMIC_RANK, NoMid, CODEC>(keysIn, keysOut, valsIn, valsOut, keyStart, valid, km,
                                                      shift, myBase, status, nullptr, errFlag, chain + t, chain, g, smem,
                                                      nullptr, k, v, NoMid{}, hiPlane);
     lds_barrier();  // stage, s_gofs and s_misc are reused by the next tile
