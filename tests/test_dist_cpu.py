@@ -30,6 +30,7 @@ class OracleOps:
     def __init__(self, kt, vb, desc):
         self.kt, self.vb, self.desc = kt, vb, desc
         self.dt = NP_KEY[kt]
+        self.ranges = 0
 
     def partition(self, keys, vals, n, bit):
         k = keys.numpy().view(self.dt)[:n]
@@ -48,10 +49,15 @@ class OracleOps:
         d = ((t[sel] >> np.uint64(bit)) & np.uint64(0xFF)).astype(np.int64)
         return torch.from_numpy(np.bincount(d, minlength=256).astype(np.int32))
 
-    def sort(self, keys, vals, n, s, e, finish=True):
+    def sort(self, keys, vals, n, s, e, finish=True, key_range=None):
         if n == 0:
             return
         k = keys.numpy().view(self.dt)[:n]
+        if key_range is not None:   # the split's range promise (thrs_options.keyRange) must hold
+            t = O.key_bits_np(self.kt, k, self.desc)
+            lo, hi = key_range
+            assert int(t.min()) >= lo and int(t.max()) <= hi, ("key range promise broken", lo, hi)
+            self.ranges += 1
         v = vals.numpy().reshape(n, self.vb) if vals is not None else None
         k2, v2 = O.lsd_sort(self.kt, k, v, s, e, self.desc)
         keys.copy_(torch.from_numpy(k2.view(np.uint8).reshape(-1)))
@@ -107,6 +113,8 @@ def _worker(rank, world, port, cases):
             vt = {0: None, 4: 0, 8: 1, 16: 2}[vb]
             sorter = D.DistributedRadixSort(kt, vt, int(desc), ops=OracleOps(kt, vb, desc))
             ko, vo, n_out = sorter.sort(keys, sizes[rank], vals, s, e)
+            if s == 0 and e >= 8 * O.KEY_BYTES[kt] and n_out:   # the finish got (and kept) a key range
+                assert sorter.ops.ranges == 1 and sorter.last_range is not None, ci
             # expected: one stable sort of the concatenation
             ev = None
             if vb:

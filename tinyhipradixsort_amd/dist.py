@@ -24,9 +24,20 @@ One sort:
                 rank computes every rank's cut points from the gathered counts.
                 Buckets holding a boundary are sorted locally (stable, same
                 window) so each cut is one position.
-  4. exchange   all_to_all_single of keys (then values); rank g receives the
-                segments in source-rank order, each in source order.
-  5. finish     a local stable sort of the received keys over the window.
+  4. exchange   ONE grouped point-to-point exchange (batch_isend_irecv: one
+                RCCL group) of keys and values together; rank g receives the
+                segments in source-rank order, each in source order, straight
+                into its output buffers (its own segment is a device copy).
+  5. finish     a local stable sort of the received keys over the window.  The
+                split fixes the image range [lo_g, hi_g] every key of rank g
+                lies in (key_range below); the finish passes it to the library
+                (thrs_options.keyRange), which orders by ((img - lo_g) << sh) --
+                the same order -- so the bucket path's 16-bit buckets stay
+                balanced although the rank holds ~1/G of the key space.
+  6. check      every libthrs step ORs its temporary buffer's device-error
+                word into one device word; it is read once at the end and a
+                look-back / claim timeout in any step raises (thrs_capi.h
+                "Device-side failures").
 
 Why this is exact: rank g receives exactly the keys of global ranks
 [T_g, T_g+1) (keys below v_g, plus the first equal ones by (rank, position)).
@@ -117,6 +128,23 @@ def refine(targets: list[Target], hist: np.ndarray, loc: int):
         t.value |= d << loc
 
 
+def key_range(targets: list[Target], rank: int, key_bytes: int) -> tuple[int, int]:
+    """[lo, hi] of the images (getKeyBits ^ descending mask) of the keys rank
+    `rank` receives, from the split of a FULL-window sort.  Boundary g (the
+    first key of rank g) has its digits fixed down to some level: every key of
+    rank g is >= t.value (fixed digits, zeros below); the keys of rank g-1 are
+    < t.value when the cut lies at the start of that prefix group (offset 0),
+    and <= t.value when it lies inside it (refined to the full key, equal keys
+    split by (rank, position))."""
+    lo, hi = 0, (1 << (8 * key_bytes)) - 1
+    if rank >= 1:
+        lo = targets[rank - 1].value
+    if rank + 1 <= len(targets):
+        t = targets[rank]
+        hi = t.value if t.offset > 0 else t.value - 1
+    return lo, max(lo, hi)
+
+
 def cut_points(counts: np.ndarray, targets: list[Target]) -> np.ndarray:
     """cuts[r][g], g = 0 .. world: rank r sends positions [cuts[r][g],
     cuts[r][g+1]) of its partitioned (and split-bucket sorted) keys to rank g.
@@ -157,13 +185,10 @@ class HipLocalOps:
     """The product's local steps: libthrs.so on the tensors' GPU."""
 
     def __init__(self, config: RadixSort.Config):
+        self.config = config
         self.rs = RadixSort([], config)
-        # the finish: a rank's keys share ~256/world top digits, so the bucket
-        # path's 16-bit buckets would overflow its local sort (fallback + a
-        # wasted bucket histogram): plain LSD passes, asked for explicitly
-        self.rs_lsd = RadixSort([], config, Options(path="lsd"))
         self._tmp = None
-        self.lsd_finish = False  # set by DistributedRadixSort for world > 1
+        self._acc = None   # device u32: OR of every step's device-error word
 
     def temp(self, n: int, like):
         import torch
@@ -171,7 +196,24 @@ class HipLocalOps:
         need = d.getTemporaryBufferBytesForSortPairs()
         if self._tmp is None or self._tmp.numel() < need or self._tmp.device != like.device:
             self._tmp = torch.empty(need, dtype=torch.uint8, device=like.device)
+        if self._acc is None or self._acc.device != like.device:
+            self._acc = torch.zeros(1, dtype=torch.int32, device=like.device)
         return self._tmp
+
+    def _note(self, tmp):
+        """stream-ordered: acc |= the error word of the step that just ran on tmp"""
+        self.rs.accumulateDeviceError(tmp, self._acc)
+
+    def check_errors(self):
+        """Synchronising: raise if any step since the last check hit a device
+        look-back / claim timeout (its output would be wrong)."""
+        if self._acc is None:
+            return
+        bad = int(self._acc.item())
+        self._acc.zero_()
+        if bad:
+            from . import ThrsError
+            raise ThrsError(-5, "THRS_ERROR_LOOKBACK_TIMEOUT in a step of the distributed sort")
 
     def partition(self, keys, vals, n: int, bit: int):
         """-> (keys', vals', counts) with counts a device int32[256] tensor."""
@@ -179,7 +221,9 @@ class HipLocalOps:
         pk = torch.empty_like(keys)
         pv = torch.empty_like(vals) if vals is not None else None
         counts = torch.empty(BINS, dtype=torch.int32, device=keys.device)
-        self.rs.partitionPass(keys, vals, n, self.temp(n, keys), pk, pv, bit, counts)
+        tmp = self.temp(n, keys)
+        self.rs.partitionPass(keys, vals, n, tmp, pk, pv, bit, counts)
+        self._note(tmp)
         return pk, pv, counts
 
     def histogram(self, keys, n: int, mask: int, value: int, bit: int):
@@ -189,15 +233,18 @@ class HipLocalOps:
         self.rs.digitHistogram(keys, n, mask, value, bit, h)
         return h
 
-    def sort(self, keys, vals, n: int, start_bits: int, end_bits: int, finish: bool = True):
+    def sort(self, keys, vals, n: int, start_bits: int, end_bits: int, finish: bool = True, key_range=None):
+        """key_range: (lo, hi) images every key lies in (the finish of a
+        full-window sort) -> thrs_options.keyRange."""
         if n == 0:
             return
         tmp = self.temp(n, keys)
-        rs = self.rs_lsd if (finish and self.lsd_finish) else self.rs
+        rs = self.rs if key_range is None else RadixSort([], self.config, Options(keyRange=key_range))
         if vals is None:
             rs.sortKeys(keys, n, tmp, start_bits, end_bits)
         else:
             rs.sortPairs(keys, vals, n, tmp, start_bits, end_bits)
+        self._note(tmp)
 
 
 # ----------------------------------------------------------------- the sorter
@@ -219,33 +266,62 @@ class DistributedRadixSort:
         cfg = RadixSort.Config(keyType=self.key_type, valueType=self.value_type or ValueType.U32,
                                sortOrder=SortOrder(sort_order))
         self.ops = ops if ops is not None else HipLocalOps(cfg)
-        if hasattr(self.ops, "lsd_finish"):
-            self.ops.lsd_finish = self.world > 1
         self.backend = dist.get_backend(group)
         self.last_plan: ExchangePlan | None = None
         self.last_targets: list[Target] = []
+        self.last_range: tuple[int, int] | None = None
 
     # keys/values travel as flat byte tensors
     @staticmethod
     def _bytes(t):
         return t.contiguous().view(-1).view(__import__("torch").uint8)
 
-    def _a2a(self, out, inp, out_splits, in_splits):
-        """all_to_all_single on byte tensors; a gloo group (CPU tests) with
-        device tensors stages through host memory."""
+    def _exchange(self, rk, rv, pk, pv, plan: "ExchangePlan"):
+        """Keys and values of every segment in ONE grouped point-to-point
+        exchange (batch_isend_irecv: one RCCL group), received in source-rank
+        order straight into rk / rv; this rank's own segment is a local copy.
+        A gloo group (CPU tests) with device tensors stages through host
+        memory."""
         import torch
-        if self.backend == "gloo" and inp.device.type != "cpu":
-            o = torch.empty(out.numel(), dtype=torch.uint8)
-            self.dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits, group=self.group)
-            out.copy_(o)
-            return
-        self.dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
+        kb, vb = self.kb, self.vb
+        send_off = np.concatenate([[0], np.cumsum(plan.send)])
+        recv_off = np.concatenate([[0], np.cumsum(plan.recv)])
+        staged = self.backend == "gloo" and pk.device.type != "cpu"
+        srcs = [(pk, kb)] + ([(pv, vb)] if vb else [])
+        dsts = [(rk, kb)] + ([(rv, vb)] if vb else [])
+        if staged:
+            srcs = [(t.cpu(), w) for t, w in srcs]
+            hdst = [(torch.empty(t.numel(), dtype=torch.uint8), w) for t, w in dsts]
+        else:
+            hdst = dsts
+        ops = []
+        for peer in range(self.world):
+            for (src, w), (dst, _) in zip(srcs, hdst):
+                a, b = int(send_off[peer]) * w, int(send_off[peer + 1]) * w
+                c, d = int(recv_off[peer]) * w, int(recv_off[peer + 1]) * w
+                if peer == self.rank:
+                    if d > c:
+                        dst[c:d].copy_(src[a:b])
+                    continue
+                if b > a:
+                    ops.append(self.dist.P2POp(self.dist.isend, src[a:b], peer, self.group))
+                if d > c:
+                    ops.append(self.dist.P2POp(self.dist.irecv, dst[c:d], peer, self.group))
+        if ops:
+            for r in self.dist.batch_isend_irecv(ops):
+                r.wait()
+        if staged:
+            for (dst, _), (h, _) in zip(dsts, hdst):
+                dst.copy_(h)
 
     def _gather(self, t):
         """all_gather of a small int tensor -> host numpy [world, *t.shape]
-        (a host synchronisation)."""
+        (a host synchronisation).  Device counts are u32 (thrs_capi.h): read
+        as int32, they are widened without sign extension."""
         import torch
         c = t.to(torch.int64)
+        if t.dtype == torch.int32:
+            c &= 0xFFFFFFFF
         if self.backend == "gloo" and c.device.type != "cpu":
             c = c.cpu()
         parts = [torch.empty_like(c) for _ in range(self.world)]
@@ -303,15 +379,17 @@ class DistributedRadixSort:
         self.last_plan = plan
         clock.mark("split")
         rk = torch.empty(plan.n_out * kb, dtype=torch.uint8, device=dev)
-        self._a2a(rk, pk, [c * kb for c in plan.recv], [c * kb for c in plan.send])
-        rv = None
-        if vb:
-            rv = torch.empty(plan.n_out * vb, dtype=torch.uint8, device=dev)
-            self._a2a(rv, pv, [c * vb for c in plan.recv], [c * vb for c in plan.send])
+        rv = torch.empty(plan.n_out * vb, dtype=torch.uint8, device=dev) if vb else None
+        self._exchange(rk, rv, pk, pv, plan)
         del pk, pv
         clock.mark("exchange")
-        self.ops.sort(rk, rv, plan.n_out, start_bits, end_bits)
+        full = start_bits == 0 and end_bits >= kb * 8
+        rng = key_range(targets, self.rank, kb) if full else None
+        self.last_range = rng
+        self.ops.sort(rk, rv, plan.n_out, start_bits, end_bits, key_range=rng)
         clock.mark("finish")
+        if hasattr(self.ops, "check_errors"):
+            self.ops.check_errors()
         ko = rk.view(keys.dtype) if keys.dtype != torch.uint8 else rk
         vo = None
         if rv is not None:
