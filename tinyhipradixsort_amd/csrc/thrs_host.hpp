@@ -28,6 +28,7 @@
 #include "thrs/thrs_capi.h"
 #include "thrs_kernels.hpp"
 #include "thrs_hybrid.hpp"
+#include "thrs_fallback.hpp"
 
 namespace thrs_host {
 using namespace thrs_dev;
@@ -74,8 +75,14 @@ struct Plan {
   uint64_t setBytes;      // one look-back table set = status + ga + gp
   uint64_t claimBytes;    // per pass: XCD-block claim state (tickets, block counter, 8 block tables)
   uint64_t hybridOff;     // 3-pass path (thrs_hybrid.hpp): bucket histogram, chunk table, meta
+  uint64_t bigMax;        // most big chunks the per-bucket fallback can meet (thrs_fallback.hpp)
+  uint64_t bigHistOff;    // their low digits' counts [bigMax][key bytes - 2][256]
+  uint64_t fbRows;        // rows of one fallback look-back table: nTiles + bigMax
+  uint64_t fbOff;         // the two fallback look-back tables [2][fbRows][256] status words
+  uint64_t fbBytes;
   uint64_t hiPlaneOff;    // u32 keys without values: the bucket path's u8 plane (n bytes)
-  uint64_t scratchBytes;  // header + 2 sets (ping-pong between passes) + 8 claim areas + hybrid area [+ u8 plane]
+  uint64_t scratchBytes;  // header + 2 sets (ping-pong between passes) + 8 claim areas + hybrid area +
+                          // fallback area [+ u8 plane]
 };
 
 // hybrid area: u32 joint[65536] | segHistA[8][256] | rowHist[256] | meta[64]
@@ -92,7 +99,13 @@ constexpr uint64_t kSegInfoOff = kChunkB0Off + round_up_c((kBuckets + 1) * 4, 25
 constexpr uint64_t kSegBaseOff = kSegInfoOff + 512;   // u32 [8][256] per-segment top-digit bases
 constexpr uint64_t kSegInfoAOff = kSegBaseOff + kSegs * 256 * 4;  // the same two for the second-digit pass
 constexpr uint64_t kSegBaseAOff = kSegInfoAOff + 512;
-constexpr uint64_t kHybridBytes = kSegBaseAOff + kSegs * 256 * 4;
+// big chunks of the per-bucket fallback: chunk ids, size prefix, tile prefix
+constexpr uint64_t kBigBOff = kSegBaseAOff + kSegs * 256 * 4;
+constexpr uint64_t kBigPosOff = kBigBOff + round_up_c((kBuckets + 1) * 4, 256);
+constexpr uint64_t kBigTileOff = kBigPosOff + round_up_c((kBuckets + 1) * 4, 256);
+constexpr uint64_t kHybridBytes = kBigTileOff + round_up_c((kBuckets + 1) * 4, 256);
+// the smallest local-sort capacity (LocSmall): a big chunk holds more keys
+constexpr uint64_t kMinLocalCap = LocSmall::CAP;
 // tile ids of the segmented pass: each of the 8 segments adds at most one
 // partial tile and rounds its id range up to a multiple of kGroup
 constexpr uint64_t kSegTilePad = kSegs * kGroup;
@@ -113,12 +126,23 @@ inline Plan make_plan(int keyType, int valueBytesOrZero, uint32_t n) {
   const uint64_t nXb = (p.nTiles + kXcdBlock - 1) / kXcdBlock + 16;  // table stride (see xb_claim)
   p.claimBytes = round_up((16 + 8 * nXb) * 4, kAlign);
   p.hybridOff = kHeaderBytes + 2 * p.setBytes + 8 * p.claimBytes;
-  p.scratchBytes = p.hybridOff + kHybridBytes;
+  // the per-bucket fallback (thrs_fallback.hpp): big chunks hold > kMinLocalCap
+  // keys each, and there are at most 65536 buckets
+  p.bigMax = std::min<uint64_t>(kBuckets, (uint64_t)n / (kMinLocalCap + 1) + 1);
+  p.bigHistOff = p.hybridOff + kHybridBytes;
+  p.fbOff = p.bigHistOff + round_up(p.bigMax * (p.kb - 2) * kBins * 4, kAlign);
+  p.fbRows = p.nTiles + p.bigMax;  // one partial tile per big chunk at most
+  p.fbBytes = 2 * round_up(p.fbRows * kBins * (p.wideStatus ? 8 : 4), kAlign);
+  p.scratchBytes = p.fbOff + p.fbBytes;
   // the u8 plane of the planes codecs (thrs_kernels.hpp kCodecSplit): the u16
   // planes fill keyOut, which is all a sortKeys caller must allocate
-  // (getTemporaryBufferBytesForSortKeys = pSumBuffer + keyOutBuffer)
+  // (getTemporaryBufferBytesForSortKeys = pSumBuffer + keyOutBuffer).  Only
+  // where the default takes the bucket path with planes (u32 keys-only, n in
+  // [2^28, 2^31 + 2^25]); a forced bucket path elsewhere runs without them.
   p.hiPlaneOff = p.scratchBytes;
-  if (keyType == THRS_KEY_U32 && valueBytesOrZero == 0) p.scratchBytes += round_up(n, kAlign);
+  if (keyType == THRS_KEY_U32 && valueBytesOrZero == 0 && (uint64_t)n >= (1ull << 28) &&
+      (uint64_t)n <= (1ull << 31) + (1ull << 25))
+    p.scratchBytes += round_up(n, kAlign);
   return p;
 }
 
@@ -275,7 +299,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   // ---- kernels and their LDS opt-ins, before anything is enqueued
   const size_t lds = G::LDS_BYTES;
   auto kernelXb = atomicRank ? thrs_pass_xb<KT, VB, ST, true> : thrs_pass_xb<KT, VB, ST, false>;
-  auto kernelPersist = atomicRank ? thrs_pass_persist<KT, VB, ST, true> : thrs_pass_persist<KT, VB, ST, false>;
+  auto kernelBig = atomicRank ? thrs_pass_big<KT, VB, ST, true> : thrs_pass_big<KT, VB, ST, false>;
   auto kernel = useXb ? kernelXb : (atomicRank ? thrs_pass<KT, VB, ST, true> : thrs_pass<KT, VB, ST, false>);
   auto sk = atomicRank ? thrs_pass_seg<KT, VB, ST, true> : thrs_pass_seg<KT, VB, ST, false>;
   // plane codecs (u32 keys-only instantiations only; `planes` is false elsewhere)
@@ -283,10 +307,10 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                             : thrs_pass_seg<KT, VB, ST, false, (KT == 0 && VB == 0) ? kCodecSplit : kCodecKeys>;
   auto skPlanes = atomicRank ? thrs_pass_seg<KT, VB, ST, true, (KT == 0 && VB == 0) ? kCodecPlanes : kCodecKeys>
                              : thrs_pass_seg<KT, VB, ST, false, (KT == 0 && VB == 0) ? kCodecPlanes : kCodecKeys>;
-  const int histPasses = bucket ? nLow : nPass;
+  const int histPasses = nPass;
   const size_t histLds = (size_t)histPasses * kBins * hist_copies<(int)sizeof(U)>() * 4;
   if (allow_lds(thrs_hist<KT>, histLds) != hipSuccess || allow_lds(kernel, lds) != hipSuccess ||
-      allow_lds(kernelXb, lds) != hipSuccess || allow_lds(kernelPersist, lds) != hipSuccess)
+      allow_lds(kernelXb, lds) != hipSuccess || allow_lds(kernelBig, lds) != hipSuccess)
     return THRS_ERROR_HIP;
   if (bucket) {
     if (allow_lds(thrs_hist_joint<KT>, kJointLds) != hipSuccess || allow_lds(sk, lds) != hipSuccess)
@@ -322,9 +346,9 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
       }
     }
   }
-  // persistent grids (occupancy x CUs): the XCD-block kernel, and the bucket
-  // path's fallback-only passes (thrs_pass_persist): a launch of nTiles
-  // workgroups that all exit at once still costs ~0.1 ms at 2^18 tiles
+  // persistent grids (occupancy x CUs): the XCD-block kernel, and the
+  // per-bucket fallback's passes (thrs_pass_big): a launch of nTiles
+  // workgroups that all exit at once would cost ~0.1 ms at 2^18 tiles
   auto persistent_grid = [&](auto kern) -> uint32_t {
     int perCU = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, kern, G::THREADS, lds) != hipSuccess || perCU < 1)
@@ -332,7 +356,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     return (uint32_t)std::min<uint64_t>(plan.nTiles, (uint64_t)perCU * cu_count());
   };
   const uint32_t gridXb = useXb ? persistent_grid(kernelXb) : (uint32_t)plan.nTiles;
-  const uint32_t gridPersist = bucket ? persistent_grid(kernelPersist) : (uint32_t)plan.nTiles;
+  const uint32_t gridBig = bucket ? persistent_grid(kernelBig) : 1u;
   const uint32_t grid = useXb ? gridXb : (uint32_t)plan.nTiles;
   int segPerCU = 0;
   if (bucket &&
@@ -370,23 +394,21 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                            reinterpret_cast<const uint32_t*>(hyb + kSegHistAOff), n, cap, base + nLow * kBins,
                            chunkOff, chunkB0, meta, reinterpret_cast<uint32_t*>(hyb + kSegInfoOff),
                            reinterpret_cast<uint32_t*>(hyb + kSegBaseOff), (uint32_t)G::TILE, (uint32_t)hgrid,
-                           reinterpret_cast<uint32_t*>(hyb + kSegInfoAOff), reinterpret_cast<uint32_t*>(hyb + kSegBaseAOff));
+                           reinterpret_cast<uint32_t*>(hyb + kSegInfoAOff), reinterpret_cast<uint32_t*>(hyb + kSegBaseAOff),
+                           reinterpret_cast<uint32_t*>(hyb + kBigBOff));
       } else {
         // chunks: whole buckets; neighbouring buckets below kLocCap/2 keys share one
         hipLaunchKernelGGL(thrs_plan, dim3(1), dim3(kPlanThreads), 0, stream, joint, n, base + nLow * kBins, chunkOff,
                            chunkB0, meta, cap, (VB || local16 || kBucket64) ? -1 : smallLocal ? kLocSmallLogT : kLocLogT,
                            reinterpret_cast<uint32_t*>(hyb + kSegInfoOff), reinterpret_cast<uint32_t*>(hyb + kSegBaseOff),
                            (uint32_t)G::TILE, reinterpret_cast<const uint32_t*>(hyb + kSegHistAOff), (uint32_t)hgrid,
-                           reinterpret_cast<uint32_t*>(hyb + kSegInfoAOff), reinterpret_cast<uint32_t*>(hyb + kSegBaseAOff));
+                           reinterpret_cast<uint32_t*>(hyb + kSegInfoAOff), reinterpret_cast<uint32_t*>(hyb + kSegBaseAOff),
+                           reinterpret_cast<uint32_t*>(hyb + kBigBOff));
       }
-      // the low digits' histograms + bases: needed only on the fallback path
-      hipLaunchKernelGGL(thrs_hist<KT>, dim3(hgrid), dim3(kHistThreads), histLds, stream, static_cast<const U*>(keys),
-                         n, km, startBits, nLow, vec, hist, meta + kMetaFallback);
-      hipLaunchKernelGGL(thrs_scan, dim3(1), dim3(kThreads), 0, stream, hist, base, nLow, meta + kMetaFallback);
     } else {
       hipLaunchKernelGGL(thrs_hist<KT>, dim3(hgrid), dim3(kHistThreads), histLds, stream, static_cast<const U*>(keys),
-                         n, km, startBits, nPass, vec, hist, nullptr);
-      hipLaunchKernelGGL(thrs_scan, dim3(1), dim3(kThreads), 0, stream, hist, base, nPass, nullptr);
+                         n, km, startBits, nPass, vec, hist);
+      hipLaunchKernelGGL(thrs_scan, dim3(1), dim3(kThreads), 0, stream, hist, base, nPass);
     }
     if (counts && hipMemcpyAsync(counts, hist, kBins * sizeof(uint32_t), hipMemcpyDeviceToDevice, stream) != hipSuccess)
       return THRS_ERROR_HIP;
@@ -403,14 +425,10 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     GroupTables<ST> g = grp[p & 1];
     g.gaNext = more ? grp[(p + 1) & 1].ga : nullptr;
     g.gpNext = more ? grp[(p + 1) & 1].gp : nullptr;
-    ProfScope prof(stream, gate && (gateMask == kGateFallback || gateMask == kGateMode1) ? 3 : 1);  // fallback-only passes are timed apart
-    // fallback-only launches (most exit at once): persistent ticket kernel,
-    // unless the XCD-block kernel runs anyway
-    const bool fallbackOnly = gate && (gateMask == kGateFallback || gateMask == kGateMode1);
-    const bool persist = bucket && fallbackOnly && !useXb;
-    hipLaunchKernelGGL(persist ? kernelPersist : kernel, dim3(persist ? gridPersist : grid), dim3(G::THREADS), lds,
-                       stream, kin, kout, vin, vout, n, km, startBits + 8 * p, base + p * kBins, status[p & 1],
-                       next, useXb ? reinterpret_cast<uint32_t*>(claim + p * plan.claimBytes) : counters + p, err, g,
+    ProfScope prof(stream, 1);
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(G::THREADS), lds, stream, kin, kout, vin, vout, n, km, startBits + 8 * p,
+                       base + p * kBins, status[p & 1], next,
+                       useXb ? reinterpret_cast<uint32_t*>(claim + p * plan.claimBytes) : counters + p, err, g,
                        g_stamps ? g_stamps + (uint64_t)p * plan.nTiles * kStampSlots : nullptr, gate, gateMask);
   };
   auto publish_error = [&]() -> int {
@@ -438,44 +456,22 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     return publish_error();
   }
 
-  // ---- bucket path: fallback-only low passes, the two top digits, local sort
+  // ---- bucket path: the two top digits, the local sort, the per-bucket fallback
   if constexpr (kBucketType) {
     U* K = static_cast<U*>(keys);
     VW* V = static_cast<VW*>(vals);
-    uint32_t* fallback = meta + kMetaFallback;
     uint32_t* mode = meta + kMetaMode;
-    {
-      U* kin = K;
-      U* kout = keyOut;
-      VW* vin = V;
-      VW* vout = valOut;
-      for (int p = 0; p < nLow; ++p) {
-        launch_pass(p, kin, kout, vin, vout, fallback, kGateFallback);
-        std::swap(kin, kout);
-        std::swap(vin, vout);
-      }
-      if (nLow & 1) {  // fallback result is in keyOut: the top-digit passes read K
-        hipLaunchKernelGGL(thrs_copy_gated, dim3(2048), dim3(256), 0, stream,
-                           reinterpret_cast<const uint32_t*>(keyOut), reinterpret_cast<uint32_t*>(K),
-                           (uint64_t)n * sizeof(U) / 4, fallback, 1u);
-        if (VB)
-          hipLaunchKernelGGL(thrs_copy_gated, dim3(2048), dim3(256), 0, stream,
-                             reinterpret_cast<const uint32_t*>(valOut), reinterpret_cast<uint32_t*>(V),
-                             (uint64_t)n * VB / 4, fallback, 1u);
-      }
-    }
     // The two top digits: XCD-segmented passes (thrs_kernels.hpp
     // thrs_pass_seg) -- the second digit over position segments (the bucket
     // histogram's workgroup ranges), the top digit over second-digit ranges.
-    // Gates on meta[kMetaMode]: mode 0 (local path) the segmented second-digit
-    // pass, mode 1 (fallback) the plain one (the position segments' counts are
-    // those of the INPUT order, not the low passes' output), mode 2 (one
-    // bucket holds every key: both top digits constant) neither, and no
-    // top-digit pass either (both are identities, and skipping both keeps the
-    // result in K).
+    // Gates on meta[kMetaMode]: mode 0 (every bucket fits its local sort) and
+    // mode 1 (some big chunks: the per-bucket fallback needs the full keys,
+    // so the key-plane codecs run in mode 0 only); mode 2 (one bucket holds
+    // every key: both top digits constant) neither -- both are identities,
+    // and skipping both keeps the keys in K.
     auto launch_seg = [&](int p, U* kin, U* kout, VW* vin, VW* vout, uint64_t infoOff, uint64_t baseOff,
                           const uint32_t* gate, uint32_t gateMask, int codec = kCodecKeys) {
-      ProfScope prof(stream, gateMask == kGateMode1 ? 3 : 1);  // fallback-only launches are timed apart
+      ProfScope prof(stream, 1);
       auto kern = codec == kCodecSplit ? skSplit : codec == kCodecPlanes ? skPlanes : sk;
       // kCodecPlanes: image-space input (identity map), digit at bits 16-23 of k'
       hipLaunchKernelGGL(kern, dim3((uint32_t)segPerCU * cu_count()), dim3(G::THREADS), lds, stream, kin, kout, vin,
@@ -486,15 +482,15 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     const uint64_t sw = plan.wideStatus ? 8 : 4;
     const int setB = (nLow + 1) & 1;
     if (segA) {
-      // Both table sets are clean: zeroed up front, and on the fallback each
-      // low pass clears its successor's rows; the segmented passes' extra
-      // tile ids (rows past nTiles) are touched by nothing else.
-      if (planes)
+      // Both table sets are clean (zeroed up front); the segmented passes'
+      // extra tile ids (rows past nTiles) are touched by nothing else.
+      if (planes) {
         launch_seg(nLow, K, reinterpret_cast<U*>(loP), V, valOut, kSegInfoAOff, kSegBaseAOff, mode, kGateMode0,
                    kCodecSplit);
-      else
-        launch_seg(nLow, K, keyOut, V, valOut, kSegInfoAOff, kSegBaseAOff, mode, kGateMode0);
-      launch_pass(nLow, K, keyOut, V, valOut, mode, kGateMode1);
+        launch_seg(nLow, K, keyOut, V, valOut, kSegInfoAOff, kSegBaseAOff, mode, kGateMode1);
+      } else {
+        launch_seg(nLow, K, keyOut, V, valOut, kSegInfoAOff, kSegBaseAOff, mode, kGateMode0 | kGateMode1);
+      }
     } else {
       launch_pass(nLow, K, keyOut, V, valOut, mode, kGateMode0 | kGateMode1);
       // the segmented pass's tile ids reach past nTiles (per-segment
@@ -507,7 +503,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                          stream) != hipSuccess)
         return THRS_ERROR_HIP;
     }
-    if (planes) {  // mode 0: planes -> lo2; mode 1 (fallback): keys
+    if (planes) {  // mode 0: planes -> lo2; mode 1 (big chunks): keys
       launch_seg(nLow + 1, reinterpret_cast<U*>(loP), reinterpret_cast<U*>(lo2P), valOut, V, kSegInfoOff, kSegBaseOff,
                  mode, kGateMode0, kCodecPlanes);
       launch_seg(nLow + 1, keyOut, K, valOut, V, kSegInfoOff, kSegBaseOff, mode, kGateMode1);
@@ -550,7 +546,8 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
           if (count16) {
             // persistent: one 128-KiB workgroup per CU walks the chunks
             const uint32_t cgrid = (uint32_t)std::min<uint64_t>(maxChunks, (uint64_t)cu_count());
-            // planes off / mode 2: the items are the keys themselves (in place)
+            // planes off (or mode 1, big chunks): the items are the keys
+            // themselves (in place)
             auto lk = planes ? thrs_local_count16<true> : thrs_local_count16<false>;
             hipLaunchKernelGGL(lk, dim3(cgrid), dim3(LocCount::THREADS), LocCount::LDS, stream,
                                reinterpret_cast<uint32_t*>(K), n, km32, chunkOff, chunkB0, meta,
@@ -572,6 +569,28 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
       } else {
         launch_local(LocBig{});
       }
+    }
+    // ---- the per-bucket fallback (thrs_fallback.hpp): big chunks only,
+    // gated on meta[kMetaFallback]
+    {
+      ProfScope prof(stream, 3);
+      uint32_t* bigB = reinterpret_cast<uint32_t*>(hyb + kBigBOff);
+      uint32_t* bigPos = reinterpret_cast<uint32_t*>(hyb + kBigPosOff);
+      uint32_t* bigTile = reinterpret_cast<uint32_t*>(hyb + kBigTileOff);
+      uint32_t* bigHist = reinterpret_cast<uint32_t*>(scratch + plan.bigHistOff);
+      ST* fb0 = reinterpret_cast<ST*>(scratch + plan.fbOff);
+      ST* fb1 = reinterpret_cast<ST*>(scratch + plan.fbOff + plan.fbBytes / 2);
+      hipLaunchKernelGGL(thrs_big_plan, dim3(std::min<uint32_t>(256, cu_count())), dim3(kBigPlanThreads), 0, stream,
+                         chunkOff, meta, bigB, bigPos, bigTile, (uint32_t)G::TILE, reinterpret_cast<uint4*>(bigHist),
+                         nLow, reinterpret_cast<uint4*>(fb0), (uint64_t)(plan.fbBytes / 16));
+      hipLaunchKernelGGL(thrs_big_hist<KT>, dim3(cu_count()), dim3(kHistThreads),
+                         (size_t)nLow * kBins * kBigCopies * 4, stream, static_cast<const U*>(keys), km, startBits, nLow,
+                         chunkOff, meta, bigB, bigPos, bigHist);
+      for (int p = 0; p < nLow; ++p)
+        hipLaunchKernelGGL(kernelBig, dim3(gridBig), dim3(G::THREADS), lds, stream, K, keyOut, V, valOut, km,
+                           startBits + 8 * p, p, nLow, chunkOff, meta, bigB, bigPos, bigTile, bigHist, fb0, fb1, err);
+      hipLaunchKernelGGL((thrs_big_copy<U, VW>), dim3(2048), dim3(256), 0, stream, K, keyOut, VB ? V : nullptr, valOut,
+                         chunkOff, meta, bigB, bigPos);
     }
     if (hipGetLastError() != hipSuccess) return THRS_ERROR_HIP;
   }

@@ -25,10 +25,12 @@
 // keep their input order; the local LSD rounds are stable; so the result is
 // THE stable sort by the window bits -- bit-identical to P LSD passes.
 //
-// Fallback: a bucket larger than kLocCap (skewed input) cannot be sorted in
-// one workgroup.  thrs_plan then sets meta[kMetaFallback]; the low-digit
-// passes (launched gated on that flag) run first, thrs_local exits at once,
-// and the sequence is the plain P-pass LSD sort.  No host synchronisation.
+// Per-bucket fallback: a bucket larger than its local sort's capacity (skewed
+// or low-cardinality input) cannot be sorted in one workgroup.  The plan lists
+// such BIG chunks and sets meta[kMetaFallback]; the local sorts skip them and
+// only they get device-wide LSD passes on their low digits, each big chunk
+// its own segment (thrs_fallback.hpp; gated launches, no host
+// synchronisation).  The other buckets keep the local sort.
 #pragma once
 #include "thrs_kernels.hpp"
 
@@ -39,11 +41,21 @@ namespace {
 
 constexpr uint32_t kBuckets = 65536;  // 16-bit bucket = the window's top two digits
 // meta[kMetaMode]: 0 = local path (no bucket above the local capacity);
-// 1 = fallback: plain LSD passes; 2 = fallback and ONE bucket holds every key,
-// so both top digits are constant and their passes are identities (skipped)
-enum { kMetaChunks = 0, kMetaFallback = 1, kMetaMode = 3 };
+// 1 = some big chunks (the per-bucket fallback, thrs_fallback.hpp); 2 = ONE
+// bucket holds every key, so both top digits are constant and their passes
+// are identities (skipped).  meta[kMetaBigCount]: big chunks listed in bigB.
+// The fallback's own words follow (thrs_fallback.hpp).
+enum {
+  kMetaChunks = 0,
+  kMetaFallback = 1,
+  kMetaMode = 3,
+  kMetaBigCount = 4,
+  kMetaBigDone = 5,  // thrs_big_hist workgroups finished (last one plans the passes)
+  kMetaBigCopy = 6,  // 1: an odd number of low passes ran -- big chunks end in the temp buffer
+  kMetaBigPass = 8,  // [8]: per low pass p, bit 0 = runs (not the identity for every big chunk), bit 1 = parity
+  kMetaBigTicket = 16,  // [8]: per low pass p, its tile ticket
+};
 // gate masks of the gated launches: bit v set = run when the gate word is v
-constexpr uint32_t kGateFallback = 1u << 1;  // on meta[kMetaFallback]: fallback only
 constexpr uint32_t kGateMode0 = 1u << 0, kGateMode1 = 1u << 1, kGateMode2 = 1u << 2;  // on meta[kMetaMode]
 
 // ------------------------------------------------------------ joint histogram
@@ -292,7 +304,7 @@ __global__ __launch_bounds__(kPlanRowThreads) void thrs_plan_rows(
     uint32_t n, uint32_t cap, uint32_t* __restrict__ baseTop /* [2][256]: second, top */,
     uint32_t* __restrict__ chunkOff, uint32_t* __restrict__ chunkB0, uint32_t* __restrict__ meta,
     uint32_t* __restrict__ segInfo, uint32_t* __restrict__ segBase, uint32_t tileKeys, uint32_t histGrid,
-    uint32_t* __restrict__ segInfoA, uint32_t* __restrict__ segBaseA) {
+    uint32_t* __restrict__ segInfoA, uint32_t* __restrict__ segBaseA, uint32_t* __restrict__ bigB) {
   __shared__ uint32_t s_w[2][4], s_base, s_b2[kBins];
   const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6, r = blockIdx.x;
   // 256-thread exclusive scan (4 waves)
@@ -321,9 +333,10 @@ __global__ __launch_bounds__(kPlanRowThreads) void thrs_plan_rows(
   chunkB0[kBins * r + t] = kBins * r + t;
   if ((t & 31u) == 0) segBase[(t >> 5) * kBins + r] = base + pre;  // segment s = columns [32s, 32s+32)
   if (t == 0) baseTop[kBins + r] = base;
-  if (x > cap) {  // a bucket above the chunk capacity: fallback; all n keys in one bucket: mode 2
+  if (x > cap) {  // a bucket above the chunk capacity: a big chunk; all n keys in one bucket: mode 2
     atomicOr(&meta[kMetaFallback], 1u);
     atomicMax(&meta[kMetaMode], x == n ? 2u : 1u);
+    bigB[atomicAdd(&meta[kMetaBigCount], 1u)] = kBins * r + t;
   }
   if (r != 0) return;
   // second digit: totals over the position segments -> bases, segment bases
@@ -408,12 +421,13 @@ __global__ __launch_bounds__(kPlanThreads) void thrs_plan(const uint32_t* __rest
                                                           uint32_t* __restrict__ segBase, uint32_t tileKeys,
                                                           const uint32_t* __restrict__ segHistA, uint32_t histGrid,
                                                           uint32_t* __restrict__ segInfoA,
-                                                          uint32_t* __restrict__ segBaseA) {
+                                                          uint32_t* __restrict__ segBaseA, uint32_t* __restrict__ bigB) {
   // Wave w owns buckets [4096w, 4096w + 4096); in step i (0..63) lane l holds
   // bucket 4096w + 64i + l, so every load and every chunk-table store is
   // lane-consecutive; prefixes in bucket order come from wave scans.
   constexpr int WAVES = kPlanThreads / 64, STEPS = (int)kBuckets / kPlanThreads;  // 16, 64
-  __shared__ uint32_t s_col[WAVES][kBins], s_row[kBins], s_wsum[WAVES], s_wopen[WAVES], s_wlast[WAVES], s_flag, s_one;
+  __shared__ uint32_t s_col[WAVES][kBins], s_row[kBins], s_wsum[WAVES], s_wopen[WAVES], s_wlast[WAVES], s_flag, s_one,
+      s_nbig;
   // top-digit histogram of every second-digit segment [32s, 32s+32) (the
   // segmented top-digit pass, thrs_pass_seg) and the second digit's bases
   __shared__ uint32_t s_seg[kSegs][kBins], s_b2[kBins];
@@ -422,6 +436,7 @@ __global__ __launch_bounds__(kPlanThreads) void thrs_plan(const uint32_t* __rest
   if (tid == 0) {
     s_flag = 0;
     s_one = 0;
+    s_nbig = 0;
   }
   __syncthreads();  // before any wave can set them (a wave may finish sweep 1 before wave 0 starts)
   // logT < 0: single-bucket chunks (every non-empty bucket, and every bucket
@@ -562,6 +577,9 @@ __global__ __launch_bounds__(kPlanThreads) void thrs_plan(const uint32_t* __rest
                                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
         chunkOff[c] = off;
         chunkB0[c] = b;
+        // a bucket above cap is a chunk of its own (it opens one, and so does
+        // the bucket after it): a big chunk for the per-bucket fallback
+        if (x > cap) bigB[atomicAdd(&s_nbig, 1u)] = c;
       }
       nOpen += (uint32_t)__builtin_popcountll(m);
       run += lane63(inc);
@@ -583,12 +601,14 @@ __global__ __launch_bounds__(kPlanThreads) void thrs_plan(const uint32_t* __rest
     }
   }
   sweep(true, cbase);
+  __syncthreads();  // every big chunk appended
   if (tid == kPlanThreads - 1) {
     chunkOff[nChunks] = n;
     chunkB0[nChunks] = kBuckets;
     meta[kMetaChunks] = nChunks;
     meta[kMetaFallback] = s_flag;
     meta[kMetaMode] = s_flag ? (s_one ? 2u : 1u) : 0u;
+    meta[kMetaBigCount] = s_nbig;
   }
 }
 
@@ -882,7 +902,6 @@ __global__ __launch_bounds__(LG::THREADS) void thrs_local(typename KeyTraits<KT>
                                                           uint32_t* __restrict__ meta, uint64_t* __restrict__ stamps) {
   using U = typename KeyTraits<KT>::U;
   static_assert(sizeof(U) == 4, "the local sort is for 4-byte keys");
-  if (meta[kMetaFallback] != 0) return;  // the plain LSD passes sorted everything
   const uint32_t nChunks = meta[kMetaChunks];
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t c = blockIdx.x;
@@ -890,7 +909,7 @@ __global__ __launch_bounds__(LG::THREADS) void thrs_local(typename KeyTraits<KT>
   uint64_t* st = stamps ? stamps + (uint64_t)c * kLocStampSlots : nullptr;
   loc_stamp(st, 0);
   const LocChunk ch = loc_chunk<KT>(c, nLow, chunkOff, chunkB0);
-  if (ch.size == 0) return;
+  if (ch.size == 0 || ch.size > LG::CAP) return;  // big chunk: the per-bucket fallback sorts it
   U k[LG::KPT];
   loc_load<KT, LG>(k, keys, ch, loc_pad<KT>(ch.b0, nLow, startBits, (uint32_t)km.mask));
 #ifdef THRS_STAMPS
@@ -952,11 +971,10 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(LG:
                                                             const uint16_t* __restrict__ lo) {
   constexpr int KPT = LG::KPT, NP = LG::NP;
   constexpr uint32_t CHUNK = 64 * KPT;
-  if (meta[kMetaFallback] != 0) return;
   const uint32_t c = blockIdx.x;
   if (c >= meta[kMetaChunks]) return;
   const uint32_t start = chunkOff[c], size = chunkOff[c + 1] - start;
-  if (size == 0) return;
+  if (size == 0 || size > LG::CAP) return;  // big chunk: the per-bucket fallback sorts it
   const uint32_t hiBits = chunkB0[c] << 16;  // the bucket: the image's top 16 bits
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint16_t* stage = reinterpret_cast<uint16_t*>(smem);
@@ -1168,8 +1186,10 @@ __global__ __launch_bounds__(LocCount::THREADS) void thrs_local_count16(
   using LC = LocCount;
   constexpr int IT = LC::ITEMS, RW = LC::ROWW;
   constexpr uint32_t NONE = 0xFFFFFFFFu;
-  if (meta[kMetaFallback] != 0) return;
   const uint32_t nChunks = meta[kMetaChunks];
+  // the planes exist in mode 0 only (mode 1, big chunks: the top passes
+  // carried full keys)
+  const bool plane = PLANE && meta[kMetaMode] == 0;
   if (blockIdx.x >= nChunks) return;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint32_t* cnt = reinterpret_cast<uint32_t*>(smem);
@@ -1191,13 +1211,13 @@ __global__ __launch_bounds__(LocCount::THREADS) void thrs_local_count16(
   auto load_items = [&](uint32_t (&nx)[IT], uint32_t st, uint32_t sz) __attribute__((always_inline)) {
     const uint32_t last = sz ? sz - 1 : 0u;
     const size_t b = sz ? st : 0u;  // an empty chunk may start at n: read key 0 instead
-    const char* base = PLANE ? reinterpret_cast<const char*>(lo + b) : reinterpret_cast<const char*>(keys + b);
+    const char* base = plane ? reinterpret_cast<const char*>(lo + b) : reinterpret_cast<const char*>(keys + b);
     uint32_t r0 = tid;
     pin(r0);
 #pragma unroll
     for (int k = 0; k < IT; ++k) {
-      const uint32_t off = min(r0 + (uint32_t)k * LC::THREADS, last) * (PLANE ? 2u : 4u);
-      if constexpr (PLANE) nx[k] = *reinterpret_cast<const uint16_t*>(base + off);
+      const uint32_t off = min(r0 + (uint32_t)k * LC::THREADS, last) * (plane ? 2u : 4u);
+      if (plane) nx[k] = *reinterpret_cast<const uint16_t*>(base + off);
       else nx[k] = *reinterpret_cast<const uint32_t*>(base + off);
     }
   };
@@ -1212,7 +1232,8 @@ __global__ __launch_bounds__(LocCount::THREADS) void thrs_local_count16(
   uint32_t mStart = chunkOff[c2], mEnd = chunkOff[c2 + 1], mHi = chunkB0[c2];
 
   auto body = [&](uint32_t (&it)[IT], uint32_t (&nx)[IT]) __attribute__((always_inline)) {
-    const uint32_t start = nStart, size = nSize, hiBits = nHi << 16;
+    // a big chunk (the per-bucket fallback sorts it) takes the empty-chunk branch
+    const uint32_t start = nStart, size = nSize > LC::CAP ? 0u : nSize, hiBits = nHi << 16;
     // the next chunk's items in flight during this one (clamped: always a
     // valid load); the one after that: its offsets
     nStart = mStart;
@@ -1230,7 +1251,7 @@ __global__ __launch_bounds__(LocCount::THREADS) void thrs_local_count16(
       pin(rc);
 #pragma unroll
       for (int k = 0; k < IT; ++k) {
-        const uint32_t v = rc + (uint32_t)k * LC::THREADS < size ? (PLANE ? it[k] : kimg<0>(km, it[k]) & 0xFFFFu) : NONE;
+        const uint32_t v = rc + (uint32_t)k * LC::THREADS < size ? (plane ? it[k] : kimg<0>(km, it[k]) & 0xFFFFu) : NONE;
         const bool uni = __all(__builtin_amdgcn_readfirstlane(v) == v);
         const uint32_t add = uni ? (lane == 0 ? 64u : 0u) : 1u;
         if (v != NONE && add != 0)
@@ -1327,14 +1348,13 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(4))
     const uint32_t* __restrict__ chunkOff, const uint32_t* __restrict__ chunkB0, const uint32_t* __restrict__ meta) {
   constexpr int KPT = LG::KPT;
   constexpr uint32_t CHUNK = 64 * KPT;
-  if (meta[kMetaFallback] != 0) return;  // the plain LSD passes sorted everything
   const uint32_t c = blockIdx.x;
   const uint32_t nChunks = meta[kMetaChunks];
   if (c >= nChunks) return;
   LocChunk ch;
   ch.start = chunkOff[c];
   ch.size = chunkOff[c + 1] - ch.start;
-  if (ch.size == 0) return;
+  if (ch.size == 0 || ch.size > LG::CAP) return;  // big chunk: the per-bucket fallback sorts it
   ch.b0 = 0;
   ch.rounds = 2;  // single-bucket chunk: the two low digits of the key = the item's top 16 bits
   const uint32_t hiImg = chunkB0[c] << 16;
@@ -1428,11 +1448,10 @@ __global__ __launch_bounds__(Loc64::THREADS) void thrs_local64(uint64_t* __restr
   constexpr int KPT = Loc64::KPT, W = Loc64::WAVES;
   constexpr uint32_t CHUNK = 64 * KPT;
   constexpr bool PERMUTE_KEYS = KT == 3;  // f64: keys travel by position (their -0 is not rebuilt)
-  if (meta[kMetaFallback] != 0) return;   // the plain LSD passes sorted everything
   const uint32_t c = blockIdx.x;
   if (c >= meta[kMetaChunks]) return;
   const uint32_t start = chunkOff[c], size = chunkOff[c + 1] - start;
-  if (size == 0) return;
+  if (size == 0 || size > Loc64::CAP) return;  // big chunk: the per-bucket fallback sorts it
   const uint64_t hiImg = (uint64_t)chunkB0[c] << 48;  // the bucket: the image's top 16 bits
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint64_t* stage = reinterpret_cast<uint64_t*>(smem);
@@ -1561,15 +1580,6 @@ __global__ __launch_bounds__(Loc64::THREADS) void thrs_local64(uint64_t* __restr
     if constexpr (PERMUTE_KEYS) permute(keys);
     if constexpr (VB == 8) permute(vals);
   }
-}
-
-// Copy on the fallback path only (odd number of low passes: their result is
-// in the temporary buffer; the two top-digit passes read the caller's).
-__global__ void thrs_copy_gated(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, uint64_t words,
-                                const uint32_t* __restrict__ gate, uint32_t want) {
-  if (*gate != want) return;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += (uint64_t)gridDim.x * blockDim.x)
-    dst[i] = src[i];
 }
 
 }  // namespace

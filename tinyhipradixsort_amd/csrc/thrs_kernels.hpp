@@ -303,10 +303,8 @@ template <int KT>
 __global__ __launch_bounds__(kHistThreads) void thrs_hist(const typename KeyTraits<KT>::U* __restrict__ keys,
                                                           uint32_t n, KeyMap<typename KeyTraits<KT>::U> km,
                                                           int startBits, int nPass, int vec,
-                                                          uint32_t* __restrict__ hist,
-                                                          const uint32_t* __restrict__ gate = nullptr) {
+                                                          uint32_t* __restrict__ hist) {
   using U = typename KeyTraits<KT>::U;
-  if (gate && *gate == 0) return;  // fallback-only launch (thrs_hybrid.hpp) not needed
   constexpr int NP_MAX = sizeof(U);
   constexpr int COPIES = hist_copies<(int)sizeof(U)>();
   extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];  // [nPass][256][COPIES]
@@ -426,8 +424,7 @@ __global__ __launch_bounds__(kHistThreads) void thrs_digit_hist_u64(const uint64
 
 // exclusive scan of each pass's histogram -> global digit bases
 __global__ __launch_bounds__(kThreads) void thrs_scan(const uint32_t* __restrict__ hist, uint32_t* __restrict__ base,
-                                                      int nPass, const uint32_t* __restrict__ gate = nullptr) {
-  if (gate && *gate == 0) return;  // fallback-only launch (thrs_hybrid.hpp) not needed
+                                                      int nPass) {
   __shared__ uint32_t s_w[4];
   for (int p = 0; p < nPass; ++p) {
     uint32_t total;
@@ -785,7 +782,9 @@ struct NoMid {
   __device__ __forceinline__ void operator()() const {}
 };
 
-template <int KT, int VB, typename ST, bool ATOMIC_RANK, typename Mid, int CODEC = kCodecKeys>
+// GROUPED = false: the flat per-tile look-back (the per-bucket fallback,
+// whose chains may be shorter than a group; thrs_fallback.hpp).
+template <int KT, int VB, typename ST, bool ATOMIC_RANK, typename Mid, int CODEC = kCodecKeys, bool GROUPED = true>
 __device__ __forceinline__ void pass_tile(
     const typename KeyTraits<KT>::U* __restrict__ keysIn, typename KeyTraits<KT>::U* __restrict__ keysOut,
     const typename ValueWord<VB>::T* __restrict__ valsIn, typename ValueWord<VB>::T* __restrict__ valsOut,
@@ -894,7 +893,7 @@ __device__ __forceinline__ void pass_tile(
     ST* pub = status + (uint64_t)tile * kBins + dp;
     if (tile != chainStart) store_agent(pub, Status<ST>::agg(real2));
     else store_agent(pub, Status<ST>::pre(real2));
-    if constexpr (kGroup > 0)
+    if constexpr (kGroup > 0 && GROUPED)
       __hip_atomic_fetch_add(&grp.ga[(uint64_t)(tile / kGroup) * kBins + dp], real2 + kArrival, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -999,7 +998,7 @@ __device__ __forceinline__ void pass_tile(
 
   // ---- D: decoupled look-back for digit d, kLookWindow rows per round trip;
   // a not-yet-published word stops the window and is re-polled.
-  if constexpr (kGroup > 0) {
+  if constexpr (kGroup > 0 && GROUPED) {
     if (tid < 256) gw.finish(realTot, myBase, localStart, s_gofs, s_misc, errFlag, stamps);
 #ifdef THRS_STAMPS
     if (stamps && lane == 0 && w < 4) {  // slots 12..15: waves 0..3 arrive at the post-walk barrier
@@ -1139,7 +1138,7 @@ __device__ __forceinline__ void pass_tile(
   // memory queue (behind the other workgroup's loads) and holds the barrier.
   if (tid < 256) {
     if (statusNext) statusNext[(uint64_t)tile * kBins + d] = 0;
-    if constexpr (kGroup > 0) {
+    if constexpr (kGroup > 0 && GROUPED) {
       const uint32_t gend = min((tile / kGroup + 1) * (uint32_t)kGroup, grp.nTiles);
       if (grp.gaNext && tile == gend - 1) {
         grp.gaNext[(uint64_t)(tile / kGroup) * kBins + d] = 0;
@@ -1204,47 +1203,6 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
   pass_tile<KT, VB, ST, ATOMIC_RANK>(keysIn, keysOut, valsIn, valsOut, (uint64_t)tile * G::TILE,
                                      tile_valid<G::TILE>(n, tile), km, shift, myBase, status,
                                      statusNext, errFlag, tile, 0, grp, smem, stamps, k, v, NoMid{});
-}
-
-// Persistent form with plain ticket claims: the bucket path's fallback-only
-// passes (gated: they exit at once unless the fallback flag is set), where
-// one workgroup per tile would cost ~0.1 ms of empty dispatch at 2^18 tiles.
-// Tiles are claimed in ticket order, so every earlier tile is held by a
-// running workgroup (deadlock-free exactly as thrs_pass).
-template <int KT, int VB, typename ST, bool ATOMIC_RANK>
-__global__ __launch_bounds__((PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::THREADS))
-__attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::WPE))) void thrs_pass_persist(
-    const typename KeyTraits<KT>::U* __restrict__ keysIn, typename KeyTraits<KT>::U* __restrict__ keysOut,
-    const typename ValueWord<VB>::T* __restrict__ valsIn, typename ValueWord<VB>::T* __restrict__ valsOut,
-    uint32_t n, KeyMap<typename KeyTraits<KT>::U> km, int shift, const uint32_t* __restrict__ digitBase,
-    ST* __restrict__ status, ST* __restrict__ statusNext, uint32_t* __restrict__ tileCounter,
-    uint32_t* __restrict__ errFlag, GroupTables<ST> grp, uint64_t* __restrict__ stamps,
-    const uint32_t* __restrict__ gate, uint32_t gateMask) {
-  if (gate && !((gateMask >> *gate) & 1u)) return;  // not needed on this launch path (thrs_plan decides)
-  using U = typename KeyTraits<KT>::U;
-  using VW = typename ValueWord<VB>::T;
-  using G = PassGeom<sizeof(U), VB>;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  uint32_t* s_cnt = reinterpret_cast<uint32_t*>(smem + G::STAGE * (sizeof(U) + VB));
-  uint32_t* s_misc = s_cnt + (G::WAVES + 1) * kBins;
-  const uint32_t tid = threadIdx.x;
-  const uint32_t nTiles = (uint32_t)(((uint64_t)n + G::TILE - 1) / G::TILE);
-  const uint32_t myBase = digitBase[tid & 255u];
-  (void)stamps;
-  U k[G::KPT];
-  VW v[VB ? G::KPT : 1];
-  for (;;) {
-    if (tid == 0) s_misc[0] = atomicAdd(tileCounter, 1u);
-    for (uint32_t i = tid; i < (uint32_t)(G::WAVES * kBins); i += G::THREADS) s_cnt[i] = 0;
-    lds_barrier();
-    const uint32_t tile = s_misc[0];
-    if (tile >= nTiles) break;
-    load_tile<KT, VB>(keysIn, valsIn, (uint64_t)tile * G::TILE, tile_valid<G::TILE>(n, tile), k, v);
-    pass_tile<KT, VB, ST, ATOMIC_RANK>(keysIn, keysOut, valsIn, valsOut, (uint64_t)tile * G::TILE,
-                                       tile_valid<G::TILE>(n, tile), km, shift, myBase, status,
-                                       statusNext, errFlag, tile, 0, grp, smem, nullptr, k, v, NoMid{});
-    lds_barrier();  // stage, s_gofs and s_misc[0] are reused by the next tile
-  }
 }
 
 // ============================================================ XCD-block claims
