@@ -12,18 +12,24 @@ metric: "Gkeys/s and achieved HBM GB/s (% of peak), u32 keys N=2^30, 1/2/4/8 GPU
   histogram + plan, two device-wide passes for the top two digits, and one
   in-LDS local sort of every 16-bit bucket; other workloads run
   histogram + one pass per digit.
-* N>1: launched by torch.distributed.run, one rank per GPU; each rank holds
-  2^30 u32 keys (weak scaling) and one step is the bucket-exchange sort of all
-  N*2^30 keys (stable top-digit partition -> RCCL all-gather of counts ->
-  exact global-rank split (digit refinement over small all-gathers, split
-  buckets sorted locally) -> RCCL all-to-all -> local LSD finish): every rank
-  ends with exactly N*2^30/N keys, whatever the distribution.
+* N>1: launched by torch.distributed.run, one rank per GPU.  Default
+  (SURVEY.md s8(d)): STRONG scaling -- C2's 2^30 keys split over the N ranks
+  (--scaling weak: the workload's n per rank; C5 is weak by definition, 2^30
+  per GPU).  One step is the bucket-exchange sort of all keys (stable
+  top-digit partition -> RCCL all-gather of counts -> exact global-rank split
+  (digit refinement over small all-gathers, split buckets sorted locally) ->
+  one grouped RCCL point-to-point exchange of keys and values -> local finish
+  with the rank's key range, tinyhipradixsort_amd/dist.py): every rank ends
+  with exactly its share of the global order, whatever the distribution.
 
 Timing: W warm-up steps, then barrier + synchronize, K steps, synchronize +
-barrier; the max over ranks.  rank 0 prints ONE JSON line.  `roofline` uses the
-dominant kernel (thrs_pass) timed with HIP events on the sort's own stream
-inside the timed region; `cpu_baseline` times the reference's CPU path
-(std::sort, unittest.cpp:156) on a bounded sample on this host.
+barrier; the max over ranks.  rank 0 prints ONE JSON line.  `roofline` prices
+the DOMINANT kernel kind -- device passes, local sort or the per-bucket
+fallback's passes, whichever took the most time -- from per-launch HIP events
+on the sort's own stream inside the timed region (gated launches that found
+nothing to do, < 20 us, are not launches of the kernel's work); `cpu_baseline`
+times the reference's CPU path (std::sort, unittest.cpp:156) on bounded
+samples on this host, with the C1 size (2^20 keys) as its own legs.
 """
 from __future__ import annotations
 
@@ -47,6 +53,11 @@ WORKLOADS = {
     "c4": (2, 0, 1 << 28, "uniform", "C4: sortKeys f32 via fpKey transform, N=2^28 (bits & 0xFF7FFFFF)"),
     "c5": (1, 8, 1 << 30, "uniform", "C5: sortPairs u64 key + u64 index payload, 2^30 per GPU"),
     "u64k": (1, 0, 1 << 30, "uniform", "sortKeys u64, N=2^30 uniform (64-bit keys without payload)"),
+    # f1: wide payloads (unittest.cpp:433-487: K32V64 / K32V128 / K64V128 / KF32V32)
+    "k32v128": (0, 16, 1 << 30, "uniform", "sortPairs u32 key + 16-B payload (ValueType::U128), N=2^30"),
+    "k64v128": (1, 16, 1 << 29, "uniform", "sortPairs u64 key + 16-B payload (K64V128), N=2^29"),
+    "k32v64": (0, 8, 1 << 30, "uniform", "sortPairs u32 key + u64 payload, N=2^30"),
+    "kf32v32": (2, 4, 1 << 30, "uniform", "sortPairs f32 key + u32 payload, N=2^30"),
     "u32large": (0, 0, (1 << 31) + 100, "uniform", "u32Large: sortKeys u32, N=2^31+100 uniform (unittest.cpp:688-717)"),
     # low-entropy inputs of C2's shape (not bench lines of BASELINE.json: robustness)
     "c2_sorted": (0, 0, 1 << 30, "sorted", "C2 shape, already-sorted input (stratified sorted uniform sample)"),
@@ -75,6 +86,9 @@ def parse():
     p.add_argument("--lib", default=None, help="experiments: a variant build of libthrs.so (make variants)")
     p.add_argument("--force-dist", action="store_true",
                    help="run the bucket-exchange path even at world size 1 (RCCL smoke test)")
+    p.add_argument("--scaling", default="auto", choices=["auto", "strong", "weak"],
+                   help="N>1: strong = the workload's n split over the ranks (default; C5: weak), "
+                        "weak = the workload's n per rank")
     return p.parse_args()
 
 
@@ -114,7 +128,24 @@ def cpu_baseline(kt: int, vb: int, n_target_s: float) -> dict:
         return O.randomize_np(kt, O.splitmix64_stream(0, n)).astype(kdt)
 
     legs = []
-    per = n_target_s / 2
+    per = n_target_s / 3
+    # C1 as configured (BASELINE.json configs[0]: 2^20 keys, unittest.cpp
+    # harness size): std::sort / stable_sort on 1 thread and on all threads
+    n0 = 1 << 20
+    ks0 = keys_of(n0)
+    if vb:
+        vs0 = np.arange(n0, dtype={4: np.uint32, 8: np.uint64}.get(vb, np.uint64))
+        med, runs = _time_leg(lambda a: O.std_stable_sort_pairs(kt, a, vs0), lambda: ks0, per / 2, 3, 9)
+        legs.append({"name": "C1 size: std::stable_sort pairs", "threads": 1, "n": n0,
+                     "value": round(n0 / med / 1e9, 5), "runs": runs})
+        med, runs = _time_leg(lambda a: O.parallel_stable_sort_pairs(kt, a, vs0), lambda: ks0, per / 2, 3, 9)
+    else:
+        med, runs = _time_leg(lambda a: O.std_sort_keys(kt, a), lambda: ks0, per / 2, 3, 9)
+        legs.append({"name": "C1 size: std::sort (unittest.cpp:156)", "threads": 1, "n": n0,
+                     "value": round(n0 / med / 1e9, 5), "runs": runs})
+        med, runs = _time_leg(lambda a: O.parallel_sort(a, kt), lambda: ks0, per / 2, 3, 9)
+    legs.append({"name": "C1 size: __gnu_parallel sort", "threads": threads, "n": n0,
+                 "value": round(n0 / med / 1e9, 5), "runs": runs})
     # 1 thread: 2^24 keys (std::sort) / 2^22 pairs (stable_sort of pairs)
     if vb:
         n1 = 1 << 22
@@ -188,14 +219,14 @@ def vendor_bench(T, TU, kt, kb, vb, n, keys, vals, gen, stream, runs: int = 3):
     import ctypes
     import torch
     path = os.path.join(ROOT, "tinyhipradixsort_amd", "libthrs_vendor.so")
-    if not os.path.exists(path) or vb not in (0, kb):
+    if not os.path.exists(path):
         return None
     L = ctypes.CDLL(path)
     L.thrsv_temp_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64)]
     L.thrsv_sort.argtypes = [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 4 + [
         ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_int), ctypes.c_void_p]
     tb = ctypes.c_uint64()
-    if L.thrsv_temp_bytes(kb, vb, n, ctypes.byref(tb)) != 0:
+    if L.thrsv_temp_bytes(kt, vb, n, ctypes.byref(tb)) != 0:
         return None
     vtmp = torch.empty(max(1, tb.value), dtype=torch.uint8, device="cuda")
     kalt = torch.empty(n * kb, dtype=torch.uint8, device="cuda")
@@ -210,7 +241,7 @@ def vendor_bench(T, TU, kt, kb, vb, n, keys, vals, gen, stream, runs: int = 3):
         torch.cuda.synchronize()
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(stream)
-        rc = L.thrsv_sort(kb, vb, keys[j].data_ptr(), kalt.data_ptr(), vals[j].data_ptr() if vb else None,
+        rc = L.thrsv_sort(kt, vb, keys[j].data_ptr(), kalt.data_ptr(), vals[j].data_ptr() if vb else None,
                           valt.data_ptr() if vb else None, n, vtmp.data_ptr(), tb.value, ctypes.byref(sel),
                           stream.cuda_stream)
         b.record(stream)
@@ -226,6 +257,55 @@ def vendor_bench(T, TU, kt, kb, vb, n, keys, vals, gen, stream, runs: int = 3):
     return {"name": "hipcub::DeviceRadixSort::" + ("SortPairs" if vb else "SortKeys") + " (rocPRIM)",
             "value": round(n / (ms / 1e3) / 1e9, 3), "unit": "Gkeys/s", "ms_per_sort": round(ms, 4),
             "runs": runs, "inputs": "same generator, fresh per run"}
+
+
+GATED_NOOP_MS = 0.02   # a gated launch with nothing to do takes ~4-6 us; real launches at bench sizes > 0.2 ms
+KIND_NAMES = {0: "hist", 1: "pass", 2: "local", 3: "fallback"}
+
+
+def build_roofline(prof, steps, n, kb, vb, pinfo, elapsed, global_keys, world, wl):
+    """`roofline` of the bench line from per-launch HIP-event times (kinds:
+    0 histogram + plan, 1 device-wide digit passes, 2 local sort, 3 the
+    per-bucket fallback's launches)."""
+    if not prof:
+        return None
+    step_s = elapsed / steps
+    alg = 2 * n * (kb + vb)                      # per pass-like launch
+    kinds = {}
+    for k, ms in prof.items():
+        eff = [x for x in ms if x >= GATED_NOOP_MS]
+        kinds[KIND_NAMES[k]] = {"ms_per_sort": round(sum(eff) / steps, 4), "launches_per_sort": round(len(eff) / steps, 2),
+                                "avg_launch_ms": round(sum(eff) / len(eff), 4) if eff else None,
+                                "gated_noops_per_sort": round((len(ms) - len(eff)) / steps, 2)}
+    cand = {k: v for k, v in kinds.items() if k in ("pass", "local", "fallback") and v["avg_launch_ms"]}
+    if not cand:
+        return None
+    dom = max(cand, key=lambda k: cand[k]["ms_per_sort"])
+    avg = cand[dom]["avg_launch_ms"]
+    achieved = alg / (avg / 1e3) / 1e9
+    bucket = bool(pinfo and pinfo["path"] == "bucket")
+    names = {"pass": "thrs_pass_seg" if bucket else ("thrs_pass_xb" if kb == 4 and not vb and n >= (1 << 29) else "thrs_pass"),
+             "local": (pinfo or {}).get("local") or "local", "fallback": "thrs_pass_big"}
+    frac = achieved / PEAK_HBM_GBS
+    traffic, traffic_src = load_pmc_traffic(wl)
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": round(frac, 4) if frac <= 1 else None, "traffic": traffic, "traffic_source": traffic_src,
+            "kernel": names[dom], "kind": dom, "avg_launch_ms": avg, "alg_bytes_per_launch": alg,
+            "kinds": kinds}
+    if frac > 1:   # e.g. fallback passes over only part of the keys: not a roofline
+        roof["note"] = "dominant launches moved fewer than 2*n*(K+V) bytes; frac withheld"
+    # whole sort: B_alg = P*2*N*(K+V) for P 8-bit digits (SURVEY.md s8(d)), the
+    # work of P LSD passes whatever path ran ...
+    passes = kb
+    roof["sort_alg_GBps"] = round(passes * 2 * global_keys * (kb + vb) / step_s / 1e9, 1)
+    roof["sort_frac_of_peak"] = round(roof["sort_alg_GBps"] / PEAK_HBM_GBS / max(1, world), 4)
+    # ... and on the bytes the path that ran must move at least (thrs_path_info)
+    if pinfo:
+        roof["path"] = pinfo
+        roof["sort_min_bytes"] = pinfo["min_bytes"]
+        roof["sort_min_GBps"] = round(pinfo["min_bytes"] / step_s / 1e9, 1)
+        roof["sort_min_frac"] = round(pinfo["min_bytes"] / step_s / 1e9 / PEAK_HBM_GBS, 4)
+    return roof
 
 
 def cpu_model() -> str:
@@ -282,7 +362,17 @@ def main():
     wl = args.workload or "c2"
     kt, vb, n_default, dist_name, desc = WORKLOADS[wl]
     dist_kind = dist_name
-    n = args.n or n_default
+    # the 1/2/4/8-GPU curve is C2's 2^30 keys split over the
+    # GPUs (strong); C5 is 2^30 per GPU (weak).  --n = the workload's size
+    # (the total for strong scaling, per GPU for weak).
+    scaling = args.scaling if args.scaling != "auto" else ("weak" if wl == "c5" else "strong")
+    n_work = args.n or n_default
+    if scaling == "strong":
+        n = n_work * (rank + 1) // world - n_work * rank // world
+        global_keys = n_work
+    else:
+        n = n_work
+        global_keys = n_work * world
     kb = KEY_BYTES[kt]
     steps, warmup = args.steps, args.warmup
     stream = torch.cuda.current_stream()
@@ -354,7 +444,7 @@ def main():
         torch.cuda.synchronize()
         barrier()
         t1 = time.perf_counter()
-        prof = T.profile_read()
+        prof = {k: T.profile_launches(k) for k in range(4)}
         T.profile_enable(False)
         rs.checkDeviceError(tmp)      # raises on a look-back / claim timeout in any timed step
         # correctness of the last timed step (outside the timed region)
@@ -375,8 +465,6 @@ def main():
             ref_gpu = reference_gpu_bench(TU, kt, kb, vb, n, keys, vals, gen, stream)
         recycled = False
         elapsed = t1 - t0
-        scaling = "weak"
-        global_keys = n
         parallelism = "single"
         phase = None
     else:
@@ -388,16 +476,17 @@ def main():
         # of place (inputs are never modified), so a pool of 2 stays fresh.
         pool = 2
         keys, vals = [], []
+        first = n_work * rank // world if scaling == "strong" else n * rank   # this rank's first global index
         for i in range(pool):
             kbuf = torch.empty(n * kb, dtype=torch.uint8, device="cuda")
             if dist_kind == "uniform":
-                TU.fill_keys(kt, kbuf, n, start=(i * world + rank) * n)
+                TU.fill_keys(kt, kbuf, n, start=i * global_keys + first)
             else:
-                TU.fill_dist(kt, kbuf, n, dist_kind, start=(i * world + rank) * n)
+                TU.fill_dist(kt, kbuf, n, dist_kind, start=i * global_keys + first)
             keys.append(kbuf)
             if vb:
                 vbuf = torch.empty(n * vb, dtype=torch.uint8, device="cuda")
-                TU.iota(vb, vbuf, n, start=rank * n)
+                TU.iota(vb, vbuf, n, start=first)
                 vals.append(vbuf)
         torch.cuda.synchronize()
         out = None
@@ -421,7 +510,7 @@ def main():
         torch.cuda.synchronize()
         barrier()
         t1 = time.perf_counter()
-        prof = T.profile_read()
+        prof = {k: T.profile_launches(k) for k in range(4)}
         T.profile_enable(False)
         ko, _vo, n_out = out
         bad = TU.count_unsorted(kt, ko, n_out, 0, kb * 8)
@@ -431,8 +520,8 @@ def main():
         # rank r+1's first (unsigned key types compare as stored)
         tot = torch.tensor([n_out], dtype=torch.int64, device="cuda")
         dist.all_reduce(tot)
-        if int(tot.item()) != n * world:
-            raise SystemExit(f"bench: {int(tot.item())} keys after the exchange, expected {n * world}")
+        if int(tot.item()) != global_keys:
+            raise SystemExit(f"bench: {int(tot.item())} keys after the exchange, expected {global_keys}")
         if kt in (T.KeyType.U32, T.KeyType.U64):
             kdt = torch.int32 if kb == 4 else torch.int64
             kv = ko.view(kdt)[:n_out].to(torch.int64)
@@ -448,9 +537,7 @@ def main():
         recycled = False
         vendor = ref_gpu = None
         elapsed = t1 - t0
-        scaling = "weak"
-        global_keys = n * world
-        parallelism = f"bucket-exchange x{world} (RCCL all_gather + all_to_all)"
+        parallelism = f"bucket-exchange x{world} (RCCL all_gather + grouped point-to-point exchange)"
         phase = {k: round(v * 1e3, 3) for k, v in phase_s.items()}
         phase["n_out_rank0"] = n_out if rank == 0 else None
 
@@ -462,38 +549,15 @@ def main():
     ms_per_step = elapsed / steps * 1e3
     value = global_keys / (elapsed / steps) / 1e9
 
-    # roofline of the dominant kernel: one per-digit pass reads and writes every
-    # key (+ value) once -> algorithmic bytes per launch = 2 * n * (K + V)
-    roof = None
-    traffic, traffic_src = load_pmc_traffic(wl)
-    if prof and prof.get("pass_launches"):
-        avg_pass_ms = prof["pass_ms"] / prof["pass_launches"]
-        alg_bytes = 2 * n * (kb + vb)
-        achieved = alg_bytes / (avg_pass_ms / 1e3) / 1e9
-        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
-                "traffic_source": traffic_src,
-                # 3-HBM-pass path: the two top-digit passes are thrs_pass_seg
-                "kernel": "thrs_pass_seg" if prof.get("local_launches") else "thrs_pass",
-                "avg_launch_ms": round(avg_pass_ms, 4),
-                "alg_bytes_per_launch": alg_bytes,
-                "hist_avg_ms": round(prof["hist_ms"] / max(1, prof["hist_launches"]), 4)}
-        # whole-sort algorithmic rate (B_alg = P*2*N*(K+V) for P 8-bit digits,
-        # SURVEY.md s8(d)) -- the work of P LSD passes, whatever path ran
-        passes = kb * 8 // 8
-        roof["sort_alg_GBps"] = round(passes * alg_bytes * global_keys / n / (elapsed / steps) / 1e9, 1)
-        roof["sort_frac_of_peak"] = round(roof["sort_alg_GBps"] / PEAK_HBM_GBS / max(1, world), 4)
-        roof["pass_launches_per_sort"] = round(prof["pass_launches"] / steps, 2)
-        if prof.get("local_launches"):
-            # the 3-HBM-pass path's local bucket sort: reads and writes every key once
-            lm = prof["local_ms"] / prof["local_launches"]
-            la = alg_bytes / (lm / 1e3) / 1e9
-            # (u32 keys over the whole key above 2^29: 16-bit items; u32 pairs: items carry positions)
-            lk = ("thrs_local64" if kb == 8 else "thrs_local_pairs" if vb else
-                  "thrs_local16" if (kt == 0 and n > (1 << 29))
-                  else "thrs_local")
-            roof["local"] = {"kernel": lk, "avg_launch_ms": round(lm, 4), "achieved": round(la, 1),
-                             "frac": round(la / PEAK_HBM_GBS, 4), "alg_bytes_per_launch": alg_bytes}
+    # roofline of the DOMINANT kernel kind (device passes, local sort or the
+    # per-bucket fallback's passes: the most time inside the timed region);
+    # algorithmic bytes per launch = 2 * n * (K + V) (one read and one write of
+    # every key and value); gated launches that found nothing
+    # to do (< GATED_NOOP_MS) are not launches of the kernel's work
+    cfg_info = T.RadixSort.Config(keyType=T.KeyType(kt), valueType={0: T.ValueType.U32, 4: T.ValueType.U32,
+                                                                     8: T.ValueType.U64, 16: T.ValueType.U128}[vb])
+    pinfo = T.RadixSort([], cfg_info).pathInfo(n, 0, kb * 8, bool(vb)) if not use_dist else None
+    roof = build_roofline(prof, steps, n, kb, vb, pinfo, elapsed, global_keys, world, wl)
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline == "auto":
@@ -504,7 +568,8 @@ def main():
                "warmup": warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
                "scaling": scaling, "vs_baseline": None, "dtype": DTYPE[kt], "data": "synthetic",
                "config": {"workload": WORKLOADS[wl][4] if not use_dist else
-                          f"{DTYPE[kt]} keys, {n} per GPU x {world} GPUs, bucket-exchange sort",
+                          f"{WORKLOADS[wl][4]} -- {global_keys} keys over {world} GPUs ({scaling} scaling), "
+                          f"bucket-exchange sort",
                           "keys_per_gpu": n, "global_keys": global_keys, "key": DTYPE[kt],
                           "value": None if not vb else f"{vb}B index payload", "bits": [0, kb * 8],
                           "parallelism": parallelism,

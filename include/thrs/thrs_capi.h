@@ -69,12 +69,13 @@ typedef struct thrs_options {
   int32_t path;          /* THRS_PATH_*: LSD = one device pass per digit; BUCKET = the
                             3-HBM-pass path wherever the key/value types and window
                             allow it, for any n (AUTO: n in [2^28, 2^30 + 2^26])   */
-  int32_t localGeometry; /* THRS_LOCAL_*: the bucket path's in-LDS sort: 18432- or
-                            9216-key chunks; BIG32 = no 16-bit items (u32 keys);
-                            u32 keys-only over the whole key, 18432-key chunks:
-                            COUNT16 = counting sort of the 16-bit items, RANK16 =
-                            two LSD rounds on them; WIDE16 = the same rounds in
-                            34816-key chunks (AUTO above 2^30 + 2^26, to 2^31 + 2^25) */
+  int32_t localGeometry; /* THRS_LOCAL_*: the bucket path's in-LDS sort: 18432- (BIG) or
+                            9216-key (SMALL) chunks; 4-byte keys-only over the whole
+                            key sort 16-bit items, BIG32 = 32-bit items; u32 keys-only:
+                            COUNT16 = counting sort of the 16-bit items, RANK16 = two
+                            LSD rounds on them; WIDE16 = 34816-key chunks (AUTO above
+                            2^30 + 2^26, to 2^31 + 2^25).  Sorts with 8/16-byte values
+                            or 8-byte keys use 17408-key chunks whatever is asked.    */
   int32_t segmented;     /* THRS_SEG_*: XCD-segmented top-digit passes (AUTO: both)   */
   int32_t tileClaims;    /* THRS_CLAIMS_*: XCD-block tile claims in the digit passes
                             (AUTO: 4-byte keys without values, n >= 2^29)            */
@@ -206,12 +207,42 @@ int thrs_profile_read(double* histMs, int* histLaunches, double* passMs, int* pa
  * pass, 2 = local (in-LDS) bucket sort of the 3-pass path, 3 = the 3-pass
  * path's fallback-only passes (they exit at once unless a bucket overflowed). */
 int thrs_profile_read_kind(int kind, double* ms, int* launches);
+/* Same, launch by launch in issue order: ms[i] for the first min(cap, *count)
+ * launches of `kind`, *count = all of them.  A gated launch that had nothing
+ * to do (the per-bucket fallback's launches when no bucket overflowed, the
+ * key-codec variants of the top passes when the planes ran) takes a few
+ * microseconds. */
+int thrs_profile_read_launches(int kind, double* ms, int cap, int* count);
+
+/* The path a sort with these arguments takes -- a host decision, no device
+ * work -- and the bytes it reads and writes in HBM when no bucket overflows
+ * (benchmark diagnostics; no reference counterpart). */
+enum { THRS_LOCALK_NONE = 0, THRS_LOCALK_16 = 1, THRS_LOCALK_32 = 2, THRS_LOCALK_PAIRS = 3, THRS_LOCALK_KV = 4,
+       THRS_LOCALK_COUNT16 = 5 };
+typedef struct thrs_path_info {
+  int32_t path;          /* 0 = one device pass per digit (LSD), 1 = bucket path          */
+  int32_t local;         /* the bucket path's local sort: THRS_LOCALK_*                     */
+  int32_t planes;        /* 1: u32 keys cross the top-digit passes as a u16 + u8 plane     */
+  int32_t devicePasses;  /* device-wide digit passes of one sort                           */
+  uint64_t minBytes;     /* HBM bytes read + written by one sort, histogram included      */
+  uint64_t localCap;     /* keys per local-sort chunk (a bigger bucket takes the fallback) */
+} thrs_path_info;
+int thrs_get_path_info(const thrs_config* config, const thrs_options* options, int pairs, uint32_t n, int startBits,
+                   int endBits, thrs_path_info* out);
 
 /* Rank path of the current device: 1 = one LDS atomic per key (gfx950
  * services conflicting lanes of a fully active wave in lane order; checked by
  * a one-time probe kernel per device), 0 = ballot match (always stable).
  * No reference counterpart. */
 int thrs_rank_mode(void);
+
+/* Diagnostic (tests, benchmarks): synchronises `stream` and reports what the
+ * LAST bucket-path sort on `temporaryBuffer` found: *mode = 0 every bucket fit
+ * its local sort, 1 some big chunks took the per-bucket fallback, 2 one bucket
+ * held every key; *bigChunks = the number of big chunks.  Meaningless after
+ * an LSD-path sort.  keyType / valueBytes / n: as that sort's. */
+int thrs_debug_bucket_mode(const void* temporaryBuffer, int keyType, int valueBytes, uint32_t n, hipStream_t stream,
+                           int* mode, int* bigChunks);
 
 /* Diagnostic: resident workgroups per CU of the 3-pass path's local bucket
  * sort kernel (4-byte keys), from the runtime's occupancy calculator. */

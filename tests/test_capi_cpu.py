@@ -125,3 +125,28 @@ def test_product_path_does_not_import_the_oracle():
             if f.endswith((".py", ".hip", ".hpp", ".cpp", ".h")):
                 text = open(os.path.join(dirpath, f)).read()
                 assert "import oracle" not in text and "from oracle" not in text and "liboracle" not in text, f
+
+
+def test_path_info_matches_the_configs():
+    """thrs_get_path_info: the host's path choice per BASELINE.json config (no
+    device work) and the HBM bytes that path must move."""
+    def info(kt, vt, n, pairs, s=0, e=None, **opt):
+        cfg = T.RadixSort.Config(keyType=kt, valueType=vt)
+        rs = T.RadixSort([], cfg, T.Options(**opt))
+        return rs.pathInfo(n, s, e if e is not None else 8 * T.bytesOf(kt), pairs)
+    U32, U64, F32 = T.KeyType.U32, T.KeyType.U64, T.KeyType.F32
+    c2 = info(U32, T.ValueType.U32, 1 << 30, False)
+    assert (c2["path"], c2["local"], c2["planes"], c2["device_passes"]) == ("bucket", "thrs_local16", True, 2)
+    assert c2["min_bytes"] == (4 + 7 + 5 + 6) * (1 << 30)           # hist 4, passes 4+3 and 3+2, local 2+4
+    c3 = info(U32, T.ValueType.U32, 1 << 30, True)
+    assert (c3["path"], c3["local"]) == ("bucket", "thrs_local_pairs")
+    c4 = info(F32, T.ValueType.U32, 1 << 28, False)
+    assert (c4["path"], c4["local"], c4["planes"], c4["local_cap"]) == ("bucket", "thrs_local16", False, 9216)
+    c5 = info(U64, T.ValueType.U64, 1 << 30, True)
+    assert (c5["path"], c5["local"], c5["local_cap"]) == ("bucket", "thrs_local_kv", 17408)
+    wide = info(U32, T.ValueType.U128, 1 << 30, True)
+    assert (wide["path"], wide["local"]) == ("bucket", "thrs_local_kv")
+    assert info(U32, T.ValueType.U32, 1 << 20, False)["path"] == "lsd"
+    assert info(U32, T.ValueType.U32, 1 << 20, False, path="bucket", s=0, e=24)["local"] == "thrs_local"
+    lsd = info(U32, T.ValueType.U32, 1 << 20, False, path="lsd")
+    assert lsd["min_bytes"] == 4 * (1 << 20) + 4 * 8 * (1 << 20)     # histogram + 4 passes of read + write

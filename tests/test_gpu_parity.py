@@ -445,3 +445,157 @@ def test_full_size_low_entropy(gpu, dist, kt, vb, n):
         r = TU.check_pairs(kt, vb, orig, keys, vals, n, 0, kb * 8)
         assert r["gather_mismatch"] == 0 and r["unstable"] == 0
         assert (r["index_sum"], r["index_xor"]) == TU.expected_index_fingerprint(n)
+
+
+@pytest.mark.parametrize("kt,vb", [(O.U32, 8), (O.U32, 16), (O.F32, 4), (O.F32, 8), (O.F32, 16), (O.U64, 4),
+                                   (O.U64, 16), (O.F64, 4), (O.F64, 16)])
+@pytest.mark.parametrize("desc", [False, True])
+def test_bucket_wide_payloads_vs_oracle(gpu, kt, vb, desc):
+    """f1 (SURVEY.md s8): sortPairs with 8/16-byte payloads (ValueType::U128,
+    tinyhipradixsort.hpp:779; K64V128, unittest.cpp:469-487) and f32 pairs on
+    the bucket path (forced for every size): thrs_local_kv / thrs_local_pairs
+    carry chunk positions and permute values -- and float keys, whose +0 and
+    -0 share one image -- through the LDS stage; 16-byte values move whole.
+    Big buckets take the per-bucket fallback."""
+    torch = gpu
+    rs = make_sorter(kt, vb, desc, path="bucket")
+    kb = O.KEY_BYTES[kt]
+    kdt = O.KEY_DTYPE[kt]
+    sign = np.array(1 << (8 * kb - 1), dtype=kdt)
+    dists = {
+        "uniform": lambda k: k,
+        "ties": lambda k: k & np.array(0xFF00FF00 if kb == 4 else 0xFFFF0000FF00FF00, dtype=kdt),
+        "signed_zero": lambda k: np.where(k & np.array(1, kdt), sign, np.array(0, kdt)).astype(kdt),
+        "lowbits": lambda k: k & np.array((1 << (8 * kb - 12)) - 1, dtype=kdt),   # 16 big buckets
+        "const": lambda k: np.full_like(k, k[0]),
+    }
+    j = 0
+    for name, f in dists.items():
+        for n in [1, 100, 17408, 17409, 70001, 300007]:
+            j += 1
+            keys = f(O.randomize_np(kt, O.splitmix64_stream(5151 * j + vb, n))).astype(kdt)
+            vals = (np.arange(n * vb // 4, dtype=np.uint32) * np.uint32(2654435761)).view(
+                {4: np.uint32, 8: np.uint64, 16: np.uint64}[vb])
+            if vb == 16:
+                vals = vals.reshape(n, 2)
+            k, v = gpu_sort(torch, rs, {"keys": keys, "values": vals}, kt, vb, 0, 8 * kb)
+            ek, ev = O.lsd_sort(kt, keys, vals, 0, 8 * kb, desc)
+            assert np.array_equal(k.view(kdt), ek.view(kdt)), (name, n)
+            assert np.array_equal(v, ev), (name, n)
+
+
+@pytest.mark.parametrize("desc", [False, True])
+@pytest.mark.parametrize("geom", ["auto", "small", "wide16"])
+def test_f32_keys_only_zero_chunk(gpu, desc, geom):
+    """f32 keys-only on the bucket path sort 16-bit items (thrs_local16): +0
+    and -0 share one image, so the chunk holding it takes the zeros' bit
+    patterns from the input in input order (fpKey.hpp:23-30: -0 -> +0, stable).
+    Mixed with the denormals and tiny normals that share the zero's bucket."""
+    torch = gpu
+    rs = make_sorter(O.F32, 0, desc, path="bucket", localGeometry=geom)
+    for j, n in enumerate([1, 64, 5000, 100003, 1 << 20]):
+        raw = O.splitmix64_stream(8080 + j, n).astype(np.uint32)
+        sel = raw % np.uint32(4)
+        small = raw >> np.uint32(18)                       # denormals 1 .. 2^14, positive or negative
+        keys = np.where(sel == 0, np.uint32(0x80000000), np.where(sel == 1, np.uint32(0),
+                        np.where(sel == 2, small, small | np.uint32(0x80000000)))).astype(np.uint32)
+        keys[::7] = O.randomize_np(O.F32, O.splitmix64_stream(99 + j, n))[::7]
+        k, _ = gpu_sort(torch, rs, {"keys": keys, "values": None}, O.F32, 0, 0, 32)
+        ek, _ = O.lsd_sort(O.F32, keys, None, 0, 32, desc)
+        assert np.array_equal(k.view(np.uint32), ek.view(np.uint32)), (n, geom)
+
+
+def _mode_after(torch, rs, keys, vals, kt, vb):
+    n = keys.shape[0]
+    kd = to_dev(torch, keys)
+    d = rs.getTemporaryBufferBytes(n)
+    tmp = torch.empty(d.getTemporaryBufferBytesForSortPairs(), dtype=torch.uint8, device="cuda")
+    if vb:
+        vd = to_dev(torch, vals)
+        rs.sortPairs(kd, vd, n, tmp, 0, 8 * O.KEY_BYTES[kt])
+    else:
+        vd = None
+        rs.sortKeys(kd, n, tmp, 0, 8 * O.KEY_BYTES[kt])
+    torch.cuda.synchronize()
+    rs.checkDeviceError(tmp)
+    mode = rs.debugBucketMode(tmp, n, bool(vb))
+    k = from_dev(kd, O.KEY_DTYPE[kt], (n,))
+    v = None if vd is None else from_dev(vd, vals.dtype, vals.shape)
+    return mode, k, v
+
+
+@pytest.mark.parametrize("kt,vb", [(O.U32, 0), (O.U32, 4), (O.F32, 0), (O.U64, 8), (O.U32, 16)])
+def test_per_bucket_fallback(gpu, kt, vb):
+    """Only buckets above the local capacity take device passes (thrs_fallback.hpp):
+    a quarter of the keys in one bucket next to uniform ones (one big chunk,
+    the others sorted locally), 16 distinct keys (both low passes are
+    identities, skipped), keys confined to 2^20 values (16 big chunks, both low
+    passes run).  Bit-exact vs the oracle, and the plan's mode says which ran."""
+    torch = gpu
+    rs = make_sorter(kt, vb, False, path="bucket")
+    kb = O.KEY_BYTES[kt]
+    kdt = O.KEY_DTYPE[kt]
+    n = 1 << 21
+    base = O.randomize_np(kt, O.splitmix64_stream(777 + vb, n)).astype(kdt)
+    few = O.randomize_np(kt, O.splitmix64_stream(31, 16)).astype(kdt)
+    cases = {
+        "one_big": np.where(np.arange(n) % 4 == 0, base[0], base).astype(kdt),
+        "few_unique": few[np.arange(n) % 16],
+        "low20": (base & np.array(0xFFFFF if kb == 4 else 0xFFFFFFFFFFFF, kdt)).astype(kdt),
+    }
+    cap = rs.pathInfo(n, 0, 8 * kb, bool(vb))["local_cap"]
+    for name, keys in cases.items():
+        # expected plan: buckets (top 16 image bits) above the local capacity
+        cnt = np.bincount((O.key_bits_np(kt, keys) >> np.uint64(8 * kb - 16)).astype(np.int64), minlength=65536)
+        ebig = int((cnt > cap).sum())
+        emode = 0 if ebig == 0 else (2 if int(cnt.max()) == n else 1)
+        assert ebig >= 1, name
+        vals = None
+        if vb:
+            vals = (np.arange(n * vb // 4, dtype=np.uint32) * np.uint32(40503)).view(
+                {4: np.uint32, 8: np.uint64, 16: np.uint64}[vb])
+            if vb == 16:
+                vals = vals.reshape(n, 2)
+        (mode, big), k, v = _mode_after(torch, rs, keys, vals, kt, vb)
+        ek, ev = O.lsd_sort(kt, keys, vals, 0, 8 * kb, False)
+        assert np.array_equal(k.view(kdt), ek.view(kdt)), name
+        if vb:
+            assert np.array_equal(v, ev), name
+        assert (mode, big) == (emode, ebig), (name, mode, big)
+
+
+@pytest.mark.parametrize("kt,vb", [(O.U32, 0), (O.U32, 4), (O.U64, 0), (O.U64, 8), (O.F32, 4)])
+@pytest.mark.parametrize("desc", [False, True])
+def test_key_range_keeps_buckets_local(gpu, kt, vb, desc):
+    """thrs_options.keyRange (the multi-GPU finish): keys confined to a narrow
+    image range [lo, hi] fill all 65536 buckets once the sort orders by
+    ((img - lo) << sh), so every bucket fits its local sort (mode 0) where
+    without the range 16 buckets overflow; same bytes as the oracle either way.
+    lo == hi (one key value) returns at once, leaving the input as it is."""
+    torch = gpu
+    kb = O.KEY_BYTES[kt]
+    kdt = O.KEY_DTYPE[kt]
+    n = 1 << 21
+    raw = O.randomize_np(kt, O.splitmix64_stream(4444 + vb, n)).astype(kdt)
+    if kt == O.F32:   # floats in [1, 2): one exponent, 2^23 mantissas
+        keys = ((raw & np.uint32(0x7FFFFF)) | np.uint32(0x3F800000)).astype(kdt)
+    else:
+        keys = (np.array(0x1234 << (8 * kb - 16), kdt) | (raw & np.array((1 << 20) - 1, kdt))).astype(kdt)
+    img = O.key_bits_np(kt, keys, desc)
+    lo, hi = int(img.min()), int(img.max())
+    vals = None
+    if vb:
+        vals = (np.arange(n * vb // 4, dtype=np.uint32) * np.uint32(2654435761)).view(
+            {4: np.uint32, 8: np.uint64}[vb])
+    ek, ev = O.lsd_sort(kt, keys, vals, 0, 8 * kb, desc)
+    for rng, want_mode in (((lo, hi), 0), (None, 1)):
+        rs = make_sorter(kt, vb, desc, path="bucket", keyRange=rng)
+        (mode, big), k, v = _mode_after(torch, rs, keys, vals, kt, vb)
+        assert np.array_equal(k.view(kdt), ek.view(kdt)), (rng, mode)
+        if vb:
+            assert np.array_equal(v, ev), rng
+        assert mode == want_mode, (rng, mode, big)
+    one = np.full(1000, keys[0], kdt)
+    rs = make_sorter(kt, vb, desc, keyRange=(int(img[0]), int(img[0])))
+    k, _ = gpu_sort(torch, rs, {"keys": one, "values": None if not vb else vals[:1000]}, kt, vb, 0, 8 * kb)
+    assert np.array_equal(k, one)

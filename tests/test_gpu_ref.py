@@ -82,12 +82,12 @@ def test_libthrs_equals_reference_kernels(refk, gpu, kt, vb, desc):
 
 @pytest.mark.parametrize("name", list(C.CASES))
 def test_reference_kernels_reproduce_golden(refk, gpu, name):
-    """The committed golden digests (first 16 iterations of each UTEST stream)
+    """The committed golden digests (all 128 iterations of each UTEST stream)
     are what the reference's own kernels output."""
     torch = gpu
     kind, kt, vb, desc, stream = C.CASES[name]
     rows = GOLDEN["cases"][name]
-    for i, item in enumerate(stream(16)):
+    for i, item in enumerate(stream(128)):
         keys, vals = item["keys"], item.get("values")
         n = keys.shape[0]
         s, e = (int(item["start"]), int(item["start"]) + 8) if kind == "window" else (0, O.KEY_BYTES[kt] * 8)

@@ -87,6 +87,13 @@ def lib() -> ctypes.CDLL:
                                         ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32)]
         L.thrs_profile_read_kind.argtypes = [i32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32)]
         L.thrs_rank_mode.restype = i32
+        L.thrs_profile_read_launches.argtypes = [i32, ctypes.POINTER(ctypes.c_double), i32, ctypes.POINTER(i32)]
+        L.thrs_profile_read_launches.restype = i32
+        L.thrs_get_path_info.argtypes = [ctypes.POINTER(_CConfig), ctypes.POINTER(_COptions), i32, u32, i32, i32,
+                                     ctypes.POINTER(_CPathInfo)]
+        L.thrs_get_path_info.restype = i32
+        L.thrs_debug_bucket_mode.argtypes = [vp, i32, i32, u32, vp, ctypes.POINTER(i32), ctypes.POINTER(i32)]
+        L.thrs_debug_bucket_mode.restype = i32
         for f in ("thrs_profile_enable", "thrs_profile_read", "thrs_profile_read_kind",
                   "thrs_get_temporary_buffer_bytes", "thrs_sort_keys", "thrs_sort_pairs", "thrs_sort_keys_ex",
                   "thrs_sort_pairs_ex", "thrs_check_device_error", "thrs_accumulate_device_error",
@@ -154,6 +161,11 @@ def take_device_error():
     current device that has finished, on any stream or thread
     (thrs_take_device_error; non-blocking, device-wide)."""
     _check(lib().thrs_take_device_error())
+
+
+class _CPathInfo(ctypes.Structure):
+    _fields_ = [("path", ctypes.c_int32), ("local", ctypes.c_int32), ("planes", ctypes.c_int32),
+                ("devicePasses", ctypes.c_int32), ("minBytes", ctypes.c_uint64), ("localCap", ctypes.c_uint64)]
 
 
 class _CTempDef(ctypes.Structure):
@@ -378,6 +390,26 @@ class RadixSort:
                                           int(prefixMask) & (2**64 - 1), int(prefixValue) & (2**64 - 1),
                                           int(bitLocation), _ptr(counts), _stream(stream)))
 
+    def pathInfo(self, numberOfInputs: int, startBits: int, endBits: int, pairs: bool) -> dict:
+        """The path such a sort takes and the HBM bytes it moves when no bucket
+        overflows (thrs_get_path_info; a host decision, no device work)."""
+        o = _CPathInfo()
+        _check(lib().thrs_get_path_info(ctypes.byref(self._c()), ctypes.byref(self.options._c()), int(bool(pairs)),
+                                    _n(numberOfInputs), int(startBits), int(endBits), ctypes.byref(o)))
+        local = {0: None, 1: "thrs_local16", 2: "thrs_local", 3: "thrs_local_pairs", 4: "thrs_local_kv",
+                 5: "thrs_local_count16"}[o.local]
+        return {"path": "bucket" if o.path else "lsd", "local": local, "planes": bool(o.planes),
+                "device_passes": o.devicePasses, "min_bytes": o.minBytes, "local_cap": o.localCap}
+
+    def debugBucketMode(self, temporaryBuffer, numberOfInputs: int, pairs: bool, stream=None) -> tuple:
+        """(mode, big chunks) the last bucket-path sort on temporaryBuffer found
+        (thrs_debug_bucket_mode; synchronising, diagnostics only)."""
+        m, b = ctypes.c_int(), ctypes.c_int()
+        vb = int(lib().thrs_value_bytes(int(self.m_config.valueType))) if pairs else 0
+        _check(lib().thrs_debug_bucket_mode(_ptr(temporaryBuffer), int(self.m_config.keyType), vb,
+                                            _n(numberOfInputs), _stream(stream), ctypes.byref(m), ctypes.byref(b)))
+        return m.value, b.value
+
     def checkDeviceError(self, temporaryBuffer, stream=None):
         """Synchronising: raises if a look-back spin bound was hit in the last
         sort on temporaryBuffer."""
@@ -394,12 +426,23 @@ def profile_enable(on: bool = True):
     _check(lib().thrs_profile_enable(int(on)))
 
 
+def profile_launches(kind: int) -> list:
+    """Per-launch milliseconds of one kind since profile_enable, in issue order
+    (thrs_profile_read_launches; synchronises the recorded events)."""
+    cnt = ctypes.c_int()
+    _check(lib().thrs_profile_read_launches(int(kind), None, 0, ctypes.byref(cnt)))
+    buf = (ctypes.c_double * max(1, cnt.value))()
+    _check(lib().thrs_profile_read_launches(int(kind), buf, cnt.value, ctypes.byref(cnt)))
+    return [buf[i] for i in range(cnt.value)]
+
+
 def profile_read() -> dict:
     """Synchronise recorded events; summed ms and launch counts since enable
     (hist = histogram + scan/plan, pass = device-wide digit passes, local =
-    the 3-pass path's in-LDS bucket sort)."""
+    the 3-pass path's in-LDS bucket sort, fallback = the per-bucket
+    fallback's launches)."""
     out = {}
-    for kind, name in ((0, "hist"), (1, "pass"), (2, "local")):
+    for kind, name in ((0, "hist"), (1, "pass"), (2, "local"), (3, "fallback")):
         ms, n = ctypes.c_double(), ctypes.c_int()
         _check(lib().thrs_profile_read_kind(kind, ctypes.byref(ms), ctypes.byref(n)))
         out[name + "_ms"] = ms.value

@@ -9,6 +9,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <type_traits>
 #include <vector>
 
 #include "thrs_host.hpp"
@@ -319,6 +320,22 @@ THRS_API int thrs_digit_histogram(const thrs_config* config, const void* keys, u
   return hipGetLastError() == hipSuccess ? THRS_SUCCESS : THRS_ERROR_HIP;
 }
 
+THRS_API int thrs_debug_bucket_mode(const void* tmp, int keyType, int valueBytes, uint32_t n, hipStream_t stream,
+                                    int* mode, int* bigChunks) {
+  if (!tmp || !mode || !bigChunks || !valid_key(keyType) ||
+      !(valueBytes == 0 || valueBytes == 4 || valueBytes == 8 || valueBytes == 16))
+    return THRS_ERROR_INVALID_VALUE;
+  const Plan plan = make_plan(keyType, valueBytes, n);
+  uint32_t meta[8] = {};
+  if (hipMemcpyAsync(meta, static_cast<const char*>(tmp) + plan.hybridOff + kMetaOff, sizeof(meta),
+                     hipMemcpyDeviceToHost, stream) != hipSuccess ||
+      hipStreamSynchronize(stream) != hipSuccess)
+    return THRS_ERROR_HIP;
+  *mode = (int)meta[kMetaMode];
+  *bigChunks = (int)meta[kMetaBigCount];
+  return THRS_SUCCESS;
+}
+
 THRS_API int thrs_check_device_error(void* tmp, hipStream_t stream) {
   if (!tmp) return THRS_ERROR_INVALID_VALUE;
   uint32_t err = 0;
@@ -364,6 +381,76 @@ THRS_API int thrs_profile_read_kind(int kind, double* ms, int* launches) {
   }
   if (ms) *ms = t;
   if (launches) *launches = c;
+  return THRS_SUCCESS;
+}
+
+THRS_API int thrs_profile_read_launches(int kind, double* ms, int cap, int* count) {
+  std::lock_guard<std::mutex> g(g_prof_mu);
+  int c = 0;
+  for (auto& r : g_prof) {
+    if (r.kind != kind) continue;
+    if (ms && c < cap) {
+      if (hipEventSynchronize(r.b) != hipSuccess) return THRS_ERROR_HIP;
+      float x = 0;
+      if (hipEventElapsedTime(&x, r.a, r.b) != hipSuccess) return THRS_ERROR_HIP;
+      ms[c] = x;
+    }
+    ++c;
+  }
+  if (count) *count = c;
+  return THRS_SUCCESS;
+}
+
+THRS_API int thrs_get_path_info(const thrs_config* cfg, const thrs_options* options, int pairs, uint32_t n,
+                            int startBits, int endBits, thrs_path_info* out) {
+  const thrs_options opt = options ? *options : thrs_options{};
+  if (!out || !cfg || !valid_key(cfg->keyType) || (pairs && !valid_value(cfg->valueType)) || !valid_options(opt))
+    return THRS_ERROR_INVALID_VALUE;
+  if (((endBits - startBits) % 8) != 0) return THRS_ERROR_BIT_RANGE;
+  const int kb = key_bytes_of(cfg->keyType), vb = pairs ? value_bytes_of(cfg->valueType) : 0;
+  int nPass = 0;
+  for (int i = 0; startBits + 8 * i < endBits; ++i)
+    if (startBits + 8 * i < kb * 8) ++nPass;
+  *out = thrs_path_info{};
+  if (n == 0 || nPass == 0) return THRS_SUCCESS;
+  const Plan plan = make_plan(cfg->keyType, vb, n);
+  PathSel P{};
+  auto sel = [&](auto kt) {
+    constexpr int KT = decltype(kt)::value;
+    switch (vb) {
+      case 0: P = select_path<KT, 0>(n, startBits, nPass, opt, plan, false); break;
+      case 4: P = select_path<KT, 4>(n, startBits, nPass, opt, plan, false); break;
+      case 8: P = select_path<KT, 8>(n, startBits, nPass, opt, plan, false); break;
+      default: P = select_path<KT, 16>(n, startBits, nPass, opt, plan, false); break;
+    }
+  };
+  switch (cfg->keyType) {
+    case THRS_KEY_U32: sel(std::integral_constant<int, 0>{}); break;
+    case THRS_KEY_U64: sel(std::integral_constant<int, 1>{}); break;
+    case THRS_KEY_F32: sel(std::integral_constant<int, 2>{}); break;
+    default: sel(std::integral_constant<int, 3>{}); break;
+  }
+  const uint64_t N = n, K = kb, V = vb;
+  out->path = P.bucket ? 1 : 0;
+  if (!P.bucket) {
+    out->devicePasses = nPass;
+    out->minBytes = N * K + (uint64_t)nPass * 2 * N * (K + V) + ((nPass & 1) ? 2 * N * (K + V) : 0);
+    return THRS_SUCCESS;
+  }
+  out->devicePasses = 2;
+  out->planes = P.planes ? 1 : 0;
+  out->localCap = P.cap;
+  out->local = P.count16 ? THRS_LOCALK_COUNT16
+               : P.local16 ? THRS_LOCALK_16
+               : P.local32 ? THRS_LOCALK_32
+               : (kb == 4 && vb == 4) ? THRS_LOCALK_PAIRS : THRS_LOCALK_KV;
+  // bucket histogram read; pass A (second digit) reads keys, writes KA per
+  // key; pass B reads KA, writes KB; the local sort reads KB, writes keys
+  const uint64_t KA = P.planes ? 3 : K, KBy = P.planes ? 2 : K;
+  uint64_t bytes = N * K + N * (K + V) + N * (KA + V) + N * (KA + V) + N * (KBy + V) + N * (KBy + V) + N * (K + V);
+  const bool floatKeys = cfg->keyType == THRS_KEY_F32 || cfg->keyType == THRS_KEY_F64;
+  if (floatKeys && vb) bytes += N * K;  // the local sort re-reads float keys to permute them
+  out->minBytes = bytes;
   return THRS_SUCCESS;
 }
 

@@ -69,7 +69,8 @@ struct Plan {
   uint64_t tileKeys;  // keys per tile of the pass kernel
   uint64_t nTiles;
   bool wideStatus;    // 64-bit look-back words (n >= 2^31)
-  uint64_t statusBytes;   // per-tile rows [nTiles][256]
+  uint64_t statusBytes;   // per-tile rows [nTiles + extra][256]
+  uint64_t statusUsedBytes;  // the rows the LSD / top-digit passes use (nTiles + kSegTilePad)
   uint64_t gaBytes;       // group aggregates [nGroups][256] u32 (kGroup > 0)
   uint64_t gpBytes;       // group prefixes   [nGroups][256] status words
   uint64_t setBytes;      // one look-back table set = status + ga + gp
@@ -77,9 +78,6 @@ struct Plan {
   uint64_t hybridOff;     // 3-pass path (thrs_hybrid.hpp): bucket histogram, chunk table, meta
   uint64_t bigMax;        // most big chunks the per-bucket fallback can meet (thrs_fallback.hpp)
   uint64_t bigHistOff;    // their low digits' counts [bigMax][key bytes - 2][256]
-  uint64_t fbRows;        // rows of one fallback look-back table: nTiles + bigMax
-  uint64_t fbOff;         // the two fallback look-back tables [2][fbRows][256] status words
-  uint64_t fbBytes;
   uint64_t hiPlaneOff;    // u32 keys without values: the bucket path's u8 plane (n bytes)
   uint64_t scratchBytes;  // header + 2 sets (ping-pong between passes) + 8 claim areas + hybrid area +
                           // fallback area [+ u8 plane]
@@ -117,8 +115,15 @@ inline Plan make_plan(int keyType, int valueBytesOrZero, uint32_t n) {
   p.tileKeys = tile_keys(p.kb, p.vb);
   p.nTiles = std::max<uint64_t>(1, ((uint64_t)n + p.tileKeys - 1) / p.tileKeys);
   p.wideStatus = (uint64_t)n >= (1ull << 31);
-  const uint64_t rows = p.nTiles + kSegTilePad;  // + the segmented pass's extra tile ids
+  // the per-bucket fallback (thrs_fallback.hpp): big chunks hold > kMinLocalCap
+  // keys each, and there are at most 65536 buckets
+  p.bigMax = std::min<uint64_t>(kBuckets, (uint64_t)n / (kMinLocalCap + 1) + 1);
+  // status rows: a tile id per tile, + the segmented passes' extra ids (each
+  // segment rounds up to a look-back group) or the fallback's (a partial tile
+  // per big chunk; the fallback passes use the same two table sets)
+  const uint64_t rows = p.nTiles + std::max<uint64_t>(kSegTilePad, p.bigMax);
   p.statusBytes = round_up(rows * kBins * (p.wideStatus ? 8 : 4), kAlign);
+  p.statusUsedBytes = round_up((p.nTiles + kSegTilePad) * kBins * (p.wideStatus ? 8 : 4), kAlign);
   const uint64_t nGroups = kGroup > 0 ? (rows + kGroup - 1) / kGroup : 0;
   p.gaBytes = round_up(nGroups * kBins * 4, kAlign);
   p.gpBytes = round_up(nGroups * kBins * (p.wideStatus ? 8 : 4), kAlign);
@@ -126,14 +131,8 @@ inline Plan make_plan(int keyType, int valueBytesOrZero, uint32_t n) {
   const uint64_t nXb = (p.nTiles + kXcdBlock - 1) / kXcdBlock + 16;  // table stride (see xb_claim)
   p.claimBytes = round_up((16 + 8 * nXb) * 4, kAlign);
   p.hybridOff = kHeaderBytes + 2 * p.setBytes + 8 * p.claimBytes;
-  // the per-bucket fallback (thrs_fallback.hpp): big chunks hold > kMinLocalCap
-  // keys each, and there are at most 65536 buckets
-  p.bigMax = std::min<uint64_t>(kBuckets, (uint64_t)n / (kMinLocalCap + 1) + 1);
   p.bigHistOff = p.hybridOff + kHybridBytes;
-  p.fbOff = p.bigHistOff + round_up(p.bigMax * (p.kb - 2) * kBins * 4, kAlign);
-  p.fbRows = p.nTiles + p.bigMax;  // one partial tile per big chunk at most
-  p.fbBytes = 2 * round_up(p.fbRows * kBins * (p.wideStatus ? 8 : 4), kAlign);
-  p.scratchBytes = p.fbOff + p.fbBytes;
+  p.scratchBytes = p.bigHistOff + round_up(p.bigMax * (p.kb - 2) * kBins * 4, kAlign);
   // the u8 plane of the planes codecs (thrs_kernels.hpp kCodecSplit): the u16
   // planes fill keyOut, which is all a sortKeys caller must allocate
   // (getTemporaryBufferBytesForSortKeys = pSumBuffer + keyOutBuffer).  Only
@@ -189,6 +188,105 @@ hipError_t allow_lds(F kernel, size_t bytes) {
 //                key), local sort.
 // Every hipFuncSetAttribute happens before the first enqueue, so a failure
 // there leaves the caller's buffers untouched.
+// The path one sort takes (host decision, no device work): run_sort and
+// thrs_path_info (thrs_capi.hip) share it.
+struct PathSel {
+  bool bucket, fullWindow, smallLocal, local16, wide16, small16, count16, local32, segTop, segA, planes, ranged, useXb;
+  int nLow;
+  uint32_t cap;
+};
+template <int KT, int VB>
+PathSel select_path(uint32_t n, int startBits, int nPass, const thrs_options& opt, const Plan& plan, bool partition) {
+  using U = typename KeyTraits<KT>::U;
+  const bool counts = partition;  // (a partition pass is one plain pass)
+  // Bucket path (thrs_hybrid.hpp, thrs_fallback.hpp): a bucket histogram,
+  // device passes for the window's TOP two digits only, then one in-LDS sort
+  // of every 16-bit bucket.  Key / value types and their local sorts:
+  //   4-byte keys, no values    any window with >= 3 digits: thrs_local16
+  //                             (16-bit items; full window) or thrs_local
+  //                             (32-bit items; windows, or when asked)
+  //   4-byte keys, 4-B values   full window: thrs_local_pairs (items carry
+  //                             positions; values -- and f32 keys -- permuted)
+  //   4-byte keys, 8/16-B vals  full window: thrs_local_kv
+  //   8-byte keys, any values   full window: thrs_local_kv
+  constexpr int KB = (int)sizeof(U);
+  constexpr bool kKeys4 = KB == 4 && VB == 0;
+  constexpr bool kKV = KB == 8 || VB >= 8;
+  const bool fullWindow = startBits == 0 && nPass * 8 >= (int)(8 * sizeof(U));
+  // Size window of the default (uniform keys: n / 65536 keys per bucket;
+  // docs/EXPERIMENTS.md row 29): the local sort costs about the same per chunk
+  // whatever its size, so below 2^28 the two passes it replaces are cheaper;
+  // above 2^30 + 2^26 the largest of 65536 uniform buckets (mean + ~4.5 sigma)
+  // outgrows the chunk capacity and big chunks would take the per-bucket
+  // fallback.  THRS_PATH_BUCKET forces the path for any n (tests).
+  // Local geometries: 9216-key chunks for n <= 2^29, 18432 above (17408 for
+  // thrs_local_kv: up to 2^30 + 2^24, the largest uniform bucket ~3 sigma
+  // below the capacity); 4-byte keys-only up to 2^31 + 2^25 in 34816-key
+  // chunks (Loc16Wide).
+  const uint64_t nn = n;
+  const bool sizeOk = nn >= (1ull << 28) && nn <= (1ull << 30) + (kKV ? (1ull << 24) : (1ull << 26));
+  const bool wideOk = kKeys4 && fullWindow && nn > (1ull << 30) + (1ull << 26) && nn <= (1ull << 31) + (1ull << 25);
+  const bool smallLocal = opt.localGeometry == THRS_LOCAL_SMALL ? true
+                          : opt.localGeometry != THRS_LOCAL_AUTO  // BIG, BIG32 and the 16-bit kernels
+                              ? false
+                              : nn <= (1ull << 29);
+  const bool bucket = !counts && nPass >= 3 &&
+                      (opt.path == THRS_PATH_BUCKET || (opt.path == THRS_PATH_AUTO && (sizeOk || wideOk))) &&
+                      (kKeys4 || fullWindow);
+  const int nLow = nPass - 2;
+  // 4-byte keys over the whole key: the local sort on 16-bit items
+  // (thrs_local16) over single-bucket chunks, unless 32-bit items are asked
+  const bool local16 = kKeys4 && bucket && fullWindow && opt.localGeometry != THRS_LOCAL_BIG32;
+  // ... in 34816-key chunks (explicitly, or by default above 2^30 + 2^26);
+  // 9216-key chunks for n <= 2^29 (or asked: SMALL)
+  const bool wide16 = local16 && (opt.localGeometry == THRS_LOCAL_WIDE16 ||
+                                  (opt.localGeometry == THRS_LOCAL_AUTO && nn > (1ull << 30) + (1ull << 26)));
+  const bool small16 = local16 && !wide16 && smallLocal;
+  // ... u32 only: sorted by counting (thrs_local_count16) when asked (it
+  // measured slower, docs/EXPERIMENTS.md row 56)
+  const bool count16 = local16 && KT == 0 && !wide16 && !small16 && opt.localGeometry == THRS_LOCAL_COUNT16;
+  const bool local32 = kKeys4 && bucket && !local16;
+  const bool segTop = opt.segmented != THRS_SEG_NONE;
+  const bool segA = opt.segmented == THRS_SEG_AUTO;
+  // u32 local16 with both top-digit passes segmented: the passes carry the
+  // keys as planes (thrs_kernels.hpp kCodecSplit / kCodecPlanes): keyOut (4n
+  // bytes) = lo u16[n] | lo2 u16[n], the u8 plane hi[n] at the end of the
+  // scratch (f32: the local sort needs the input's -0 bits)
+  const bool planes = local16 && KT == 0 && segA && opt.planes != THRS_PLANES_OFF &&
+                      plan.scratchBytes - plan.hiPlaneOff >= (uint64_t)n;
+  // the local sort's chunk capacity (a bigger bucket is a big chunk)
+  const uint32_t cap = kKV ? LocKV::CAP
+                       : local16 ? (wide16 ? Loc16Wide::CAP : small16 ? Loc16Small::CAP : Loc16::CAP)
+                                 : (smallLocal ? LocSmall::CAP : LocBig::CAP);
+  // The key range (thrs_options.keyRange, thrs_kernels.hpp KeyMap): for
+  // full-window sorts, except the 32-bit local sort (it sorts the keys
+  // themselves and pads with keys)
+  const bool ranged = opt.keyRange == 1 && fullWindow && !counts && !local32;
+  // XCD-block claims (thrs_pass_xb) pay off where runs are short and the
+  // grid is large: 4-byte keys without values, n >= 2^29 (docs/EXPERIMENTS.md
+  // row 19: +4-6% there, neutral at 2^28, -2..-6% for pairs / f32 at 2^28).
+  const bool useXb = opt.tileClaims == THRS_CLAIMS_XCD_BLOCKS ? true
+                     : opt.tileClaims == THRS_CLAIMS_TICKET ? false
+                                                            : (sizeof(U) == 4 && VB == 0 && n >= (1u << 29));
+  PathSel P;
+  P.bucket = bucket;
+  P.fullWindow = fullWindow;
+  P.smallLocal = smallLocal;
+  P.local16 = local16;
+  P.wide16 = wide16;
+  P.small16 = small16;
+  P.count16 = count16;
+  P.local32 = local32;
+  P.segTop = segTop;
+  P.segA = segA;
+  P.planes = planes;
+  P.ranged = ranged;
+  P.useXb = useXb;
+  P.nLow = nLow;
+  P.cap = cap;
+  return P;
+}
+
 #ifdef THRS_RUN_KT
 template <int KT, int VB, typename ST>
 int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, void* valOutBuf, int startBits, int nPass,
@@ -222,58 +320,16 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   VW* valOut = static_cast<VW*>(valOutBuf);
 
   const U orderMask = desc ? (U)~(U)0 : (U)0;
-  // 4-byte keys without values; u32 keys with 4-byte values over the whole
-  // key; 8-byte keys without values or with 8-byte values over the whole key
-  constexpr bool kBucket32 = sizeof(U) == 4 && (VB == 0 || (VB == 4 && KT == 0));
-  constexpr bool kBucket64 = sizeof(U) == 8 && (VB == 0 || VB == 8);
-  constexpr bool kBucketType = kBucket32 || kBucket64;
-  const bool fullWindow = startBits == 0 && nPass * 8 >= (int)(8 * sizeof(U));
-  // Size window of the default (uniform keys: n / 65536 keys per bucket;
-  // docs/EXPERIMENTS.md row 29): the local sort costs about the same per chunk
-  // whatever its size, so below 2^28 the two passes it replaces are cheaper;
-  // above 2^30 + 2^26 the largest of 65536 uniform buckets (mean + ~4.5 sigma)
-  // outgrows the chunk capacity and the fallback would pay for the bucket
-  // histogram in vain.  THRS_PATH_BUCKET forces the path for any n (tests).
-  // Local geometries (thrs_hybrid.hpp LocG): LocSmall (9216-key chunks,
-  // uniform buckets of 4-8K keys) for n <= 2^29, LocBig (18432) above.
-  const uint64_t nn = n;
-  // (8-byte keys: one 17408-slot chunk per bucket, so up to 2^30 + 2^24: the
-  // largest uniform bucket stays ~3 sigma below the capacity)
-  const bool sizeOk = nn >= (1ull << 28) && nn <= (1ull << 30) + (sizeof(U) == 8 ? (1ull << 24) : (1ull << 26));
-  // u32 keys without values over the whole key: up to 2^31 + 2^25 with the
-  // wide 16-bit local sort (Loc16Wide: 34816-key chunks)
-  const bool wideOk = KT == 0 && VB == 0 && fullWindow && nn > (1ull << 30) + (1ull << 26) &&
-                      nn <= (1ull << 31) + (1ull << 25);
-  const bool smallLocal = opt.localGeometry == THRS_LOCAL_SMALL ? true
-                          : opt.localGeometry != THRS_LOCAL_AUTO  // BIG, BIG32 and the 16-bit kernels
-                              ? false
-                              : nn <= (1ull << 29);
-  const bool bucket = kBucketType && !counts && nPass >= 3 &&
-                      (opt.path == THRS_PATH_BUCKET || (opt.path == THRS_PATH_AUTO && (sizeOk || wideOk))) &&
-                      ((kBucket32 && VB == 0) || fullWindow);
-  const int nLow = nPass - 2;
-  // u32 keys over the whole key, large chunks: the local sort on 16-bit items
-  // (thrs_hybrid.hpp thrs_local16) over single-bucket chunks
-  const bool local16 = bucket && KT == 0 && VB == 0 && fullWindow && !smallLocal &&
-                       opt.localGeometry != THRS_LOCAL_BIG32;
-  // ... sorted by counting (thrs_local_count16) or by two LSD rounds (thrs_local16)
-  // ... in 34816-key chunks (explicitly, or by default above 2^30 + 2^26)
-  const bool wide16 = local16 && (opt.localGeometry == THRS_LOCAL_WIDE16 ||
-                                  (opt.localGeometry == THRS_LOCAL_AUTO && nn > (1ull << 30) + (1ull << 26)));
-  // (counting only when asked: it measured slower, docs/EXPERIMENTS.md row 56)
-  const bool count16 = local16 && !wide16 && opt.localGeometry == THRS_LOCAL_COUNT16;
-  const bool segTop = opt.segmented != THRS_SEG_NONE;
-  const bool segA = opt.segmented == THRS_SEG_AUTO;
-  // local16 with both top-digit passes segmented: the passes carry the keys
-  // as planes (thrs_kernels.hpp kCodecSplit / kCodecPlanes): keyOut (4n bytes)
-  // = lo u16[n] | lo2 u16[n], the u8 plane hi[n] at the end of the scratch
-  const bool planes = local16 && segA && opt.planes != THRS_PLANES_OFF &&
-                      plan.scratchBytes - plan.hiPlaneOff >= (uint64_t)n;
-  // The key range (thrs_options.keyRange, thrs_kernels.hpp KeyMap): for
-  // full-window sorts, except the 32-bit local sort (it sorts the keys
-  // themselves and pads with keys)
-  const bool local32 = bucket && kBucket32 && VB == 0 && !local16;
-  const bool ranged = opt.keyRange == 1 && fullWindow && !counts && !local32;
+  constexpr int KB = (int)sizeof(U);
+  constexpr bool kKeys4 = KB == 4 && VB == 0;
+  constexpr bool kPairs4 = KB == 4 && VB == 4;
+  constexpr bool kKV = KB == 8 || VB >= 8;
+  const PathSel P = select_path<KT, VB>(n, startBits, nPass, opt, plan, counts != nullptr);
+  const bool bucket = P.bucket, smallLocal = P.smallLocal, local16 = P.local16, wide16 = P.wide16;
+  const bool small16 = P.small16, count16 = P.count16, local32 = P.local32, segTop = P.segTop, segA = P.segA;
+  const bool planes = P.planes, ranged = P.ranged, useXb = P.useXb;
+  const int nLow = P.nLow;
+  const uint32_t cap = P.cap;
   KeyMap<U> km{orderMask, (U)0, 0u};
   if (ranged) {
     const U span = (U)opt.rangeHi - (U)opt.rangeLo;  // > 0 (sort_impl returns at once for 0)
@@ -288,12 +344,6 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   const bool atomicRank = opt.rank == THRS_RANK_ATOMIC ? true
                           : opt.rank == THRS_RANK_BALLOT ? false
                                                          : probe_rank_mode(stream) != 0;
-  // XCD-block claims (thrs_pass_xb) pay off where runs are short and the
-  // grid is large: 4-byte keys without values, n >= 2^29 (docs/EXPERIMENTS.md
-  // row 19: +4-6% there, neutral at 2^28, -2..-6% for pairs / f32 at 2^28).
-  const bool useXb = opt.tileClaims == THRS_CLAIMS_XCD_BLOCKS ? true
-                     : opt.tileClaims == THRS_CLAIMS_TICKET ? false
-                                                            : (sizeof(U) == 4 && VB == 0 && n >= (1u << 29));
   uint32_t* sticky = sticky_dev(stream);
 
   // ---- kernels and their LDS opt-ins, before anything is enqueued
@@ -317,31 +367,28 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
       return THRS_ERROR_HIP;
     if (planes && (allow_lds(skSplit, lds) != hipSuccess || allow_lds(skPlanes, lds) != hipSuccess))
       return THRS_ERROR_HIP;
-    if constexpr (kBucket64) {
-      if (allow_lds(atomicRank ? thrs_local64<KT, VB, true> : thrs_local64<KT, VB, false>, Loc64::LDS) != hipSuccess)
+    if constexpr (kKV) {
+      if (allow_lds(atomicRank ? thrs_local_kv<KT, VB, true> : thrs_local_kv<KT, VB, false>, LocKV::LDS) != hipSuccess)
         return THRS_ERROR_HIP;
-    } else if constexpr (kBucketType) {
-      if (local16) {
-        if constexpr (KT == 0 && VB == 0) {
-          if (allow_lds(atomicRank ? thrs_local16<true, Loc16> : thrs_local16<false, Loc16>, Loc16::LDS) !=
-                  hipSuccess ||
-              allow_lds(atomicRank ? thrs_local16<true, Loc16Wide> : thrs_local16<false, Loc16Wide>,
-                        Loc16Wide::LDS) != hipSuccess ||
-              allow_lds(thrs_local_count16<true>, LocCount::LDS) != hipSuccess ||
-              allow_lds(thrs_local_count16<false>, LocCount::LDS) != hipSuccess)
-            return THRS_ERROR_HIP;
-        }
-      } else if constexpr (VB == 4) {
-        if (allow_lds(atomicRank ? thrs_local_pairs<true, LocBig> : thrs_local_pairs<false, LocBig>,
-                      LocBig::lds<U>()) != hipSuccess ||
-            allow_lds(atomicRank ? thrs_local_pairs<true, LocSmall> : thrs_local_pairs<false, LocSmall>,
-                      LocSmall::lds<U>()) != hipSuccess)
-          return THRS_ERROR_HIP;
-      } else {
-        if (allow_lds(atomicRank ? thrs_local<KT, true, LocBig> : thrs_local<KT, false, LocBig>, LocBig::lds<U>()) !=
-                hipSuccess ||
-            allow_lds(atomicRank ? thrs_local<KT, true, LocSmall> : thrs_local<KT, false, LocSmall>,
-                      LocSmall::lds<U>()) != hipSuccess)
+    } else if constexpr (kPairs4) {
+      if (allow_lds(atomicRank ? thrs_local_pairs<KT, true, LocBig> : thrs_local_pairs<KT, false, LocBig>,
+                    LocBig::lds<U>()) != hipSuccess ||
+          allow_lds(atomicRank ? thrs_local_pairs<KT, true, LocSmall> : thrs_local_pairs<KT, false, LocSmall>,
+                    LocSmall::lds<U>()) != hipSuccess)
+        return THRS_ERROR_HIP;
+    } else if constexpr (kKeys4) {
+      if (allow_lds(atomicRank ? thrs_local16<KT, true, Loc16> : thrs_local16<KT, false, Loc16>, Loc16::LDS) !=
+              hipSuccess ||
+          allow_lds(atomicRank ? thrs_local16<KT, true, Loc16Wide> : thrs_local16<KT, false, Loc16Wide>,
+                    Loc16Wide::LDS) != hipSuccess ||
+          allow_lds(atomicRank ? thrs_local<KT, true, LocBig> : thrs_local<KT, false, LocBig>, LocBig::lds<U>()) !=
+              hipSuccess ||
+          allow_lds(atomicRank ? thrs_local<KT, true, LocSmall> : thrs_local<KT, false, LocSmall>,
+                    LocSmall::lds<U>()) != hipSuccess)
+        return THRS_ERROR_HIP;
+      if constexpr (KT == 0) {
+        if (allow_lds(thrs_local_count16<true>, LocCount::LDS) != hipSuccess ||
+            allow_lds(thrs_local_count16<false>, LocCount::LDS) != hipSuccess)
           return THRS_ERROR_HIP;
       }
     }
@@ -370,10 +417,29 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   // both table sets (the top-digit passes use set nLow&1 and the other one,
   // and no launch before them dirties the other unless it also cleans it:
   // fallback passes clear their successor's rows), all 8 claim areas, joint.
-  if (bucket) {
-    if (hipMemsetAsync(scratch, 0, plan.hybridOff + kJointZero, stream) != hipSuccess) return THRS_ERROR_HIP;
-  } else if (hipMemsetAsync(scratch, 0, kHeaderBytes + plan.setBytes, stream) != hipSuccess) {
-    return THRS_ERROR_HIP;
+  // (one zeroing launch over up to three ranges: a set's status rows past
+  // statusUsedBytes serve only the per-bucket fallback, which zeroes them)
+  {
+    const uint64_t set0 = kHeaderBytes, set1 = kHeaderBytes + plan.setBytes;
+    ZeroRanges z{};
+    if (bucket) {
+      z.ptr[0] = scratch;
+      z.words[0] = (set0 + plan.statusUsedBytes) / 16;
+      z.ptr[1] = scratch + set0 + plan.statusBytes;  // set 0's group tables .. set 1's used rows
+      z.words[1] = (set1 + plan.statusUsedBytes - (set0 + plan.statusBytes)) / 16;
+      z.ptr[2] = scratch + set1 + plan.statusBytes;  // set 1's group tables, claim areas, bucket histogram
+      z.words[2] = (plan.hybridOff + kJointZero - (set1 + plan.statusBytes)) / 16;
+    } else {
+      z.ptr[0] = scratch;
+      z.words[0] = (set0 + plan.statusUsedBytes) / 16;
+      z.ptr[1] = scratch + set0 + plan.statusBytes;  // set 0's group tables
+      z.words[1] = (plan.gaBytes + plan.gpBytes) / 16;
+      if (useXb) {  // the XCD-block claim areas of every pass
+        z.ptr[2] = scratch + kHeaderBytes + 2 * plan.setBytes;
+        z.words[2] = (uint64_t)nPass * plan.claimBytes / 16;
+      }
+    }
+    hipLaunchKernelGGL(thrs_zero_ranges, dim3(std::min<uint32_t>(2048, 8 * cu_count())), dim3(256), 0, stream, z);
   }
   char* claim = scratch + kHeaderBytes + 2 * plan.setBytes;  // 8 per-pass claim areas
 
@@ -386,8 +452,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
       hipLaunchKernelGGL(thrs_hist_joint<KT>, dim3(hgrid), dim3(kHistThreads), kJointLds, stream,
                          static_cast<const U*>(keys), n, km, startBits + 8 * nLow, vec, joint,
                          reinterpret_cast<uint32_t*>(hyb + kSegHistAOff), reinterpret_cast<uint32_t*>(hyb + kRowHistOff));
-      const uint32_t cap = kBucket64 ? Loc64::CAP : smallLocal ? LocSmall::CAP : wide16 ? Loc16Wide::CAP : LocBig::CAP;
-      if (VB || local16 || kBucket64) {
+      if (!local32) {
         // single-bucket chunks: one workgroup per top digit
         hipLaunchKernelGGL(thrs_plan_rows, dim3(kBins), dim3(kPlanRowThreads), 0, stream, joint,
                            reinterpret_cast<const uint32_t*>(hyb + kRowHistOff),
@@ -399,7 +464,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
       } else {
         // chunks: whole buckets; neighbouring buckets below kLocCap/2 keys share one
         hipLaunchKernelGGL(thrs_plan, dim3(1), dim3(kPlanThreads), 0, stream, joint, n, base + nLow * kBins, chunkOff,
-                           chunkB0, meta, cap, (VB || local16 || kBucket64) ? -1 : smallLocal ? kLocSmallLogT : kLocLogT,
+                           chunkB0, meta, cap, smallLocal ? kLocSmallLogT : kLocLogT,
                            reinterpret_cast<uint32_t*>(hyb + kSegInfoOff), reinterpret_cast<uint32_t*>(hyb + kSegBaseOff),
                            (uint32_t)G::TILE, reinterpret_cast<const uint32_t*>(hyb + kSegHistAOff), (uint32_t)hgrid,
                            reinterpret_cast<uint32_t*>(hyb + kSegInfoAOff), reinterpret_cast<uint32_t*>(hyb + kSegBaseAOff),
@@ -414,8 +479,6 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
       return THRS_ERROR_HIP;
   }
 
-  if (useXb && !bucket && hipMemsetAsync(claim, 0, (size_t)nPass * plan.claimBytes, stream) != hipSuccess)
-    return THRS_ERROR_HIP;
 
   // pass p: digit at startBits + 8p, tables of set p&1; gate != nullptr runs
   // it only if bit *gate of gateMask is set (meta words written by thrs_plan)
@@ -457,7 +520,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   }
 
   // ---- bucket path: the two top digits, the local sort, the per-bucket fallback
-  if constexpr (kBucketType) {
+  {
     U* K = static_cast<U*>(keys);
     VW* V = static_cast<VW*>(vals);
     uint32_t* mode = meta + kMetaMode;
@@ -514,36 +577,39 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     {
       ProfScope prof(stream, 2);
       // never more workgroups than chunks can exist: <= 256 (one per top digit)
-      // + 2 per non-empty bucket, and <= the number of buckets
-      // (single-bucket chunks -- pairs, local16, 8-byte keys: thrs_plan makes
+      // + 2 per non-empty bucket, and <= the number of buckets (single-bucket
+      // chunks -- every local sort but the 32-bit one: thrs_plan_rows makes
       // every bucket a chunk, empty or not)
-      const bool singleChunks = VB || local16 || kBucket64;
-      const uint64_t maxChunks = singleChunks ? kBuckets : std::min<uint64_t>(kBuckets, 256 + 2 * (uint64_t)n);
-      auto launch_local = [&](auto geom) {
-        using LG = decltype(geom);
-        const size_t llds = LG::template lds<U>();
-        if constexpr (kBucket64) {
-          (void)llds;
-        } else if constexpr (VB == 4) {
-          auto lk = atomicRank ? thrs_local_pairs<true, LG> : thrs_local_pairs<false, LG>;
-          hipLaunchKernelGGL(lk, dim3((uint32_t)maxChunks), dim3(LG::THREADS), llds, stream,
-                             reinterpret_cast<uint32_t*>(K), reinterpret_cast<uint32_t*>(V), km32,
-                             chunkOff, chunkB0, meta);
-        } else {
+      const uint64_t maxChunks = !local32 ? kBuckets : std::min<uint64_t>(kBuckets, 256 + 2 * (uint64_t)n);
+      const dim3 lgrid((uint32_t)maxChunks);
+      if constexpr (kKV) {
+        auto lk = atomicRank ? thrs_local_kv<KT, VB, true> : thrs_local_kv<KT, VB, false>;
+        hipLaunchKernelGGL(lk, lgrid, dim3(LocKV::THREADS), LocKV::LDS, stream, K, V, km, chunkOff, chunkB0, meta);
+      } else if constexpr (kPairs4) {
+        auto launch_pairs = [&](auto geom) {
+          using LG = decltype(geom);
+          auto lk = atomicRank ? thrs_local_pairs<KT, true, LG> : thrs_local_pairs<KT, false, LG>;
+          hipLaunchKernelGGL(lk, lgrid, dim3(LG::THREADS), LG::template lds<U>(), stream,
+                             reinterpret_cast<uint32_t*>(K), reinterpret_cast<uint32_t*>(V), km32, chunkOff, chunkB0,
+                             meta);
+        };
+        if (smallLocal) launch_pairs(LocSmall{});
+        else launch_pairs(LocBig{});
+      } else if constexpr (kKeys4) {
+        auto launch16 = [&](auto geom) {
+          using LG = decltype(geom);
+          auto lk = atomicRank ? thrs_local16<KT, true, LG> : thrs_local16<KT, false, LG>;
+          hipLaunchKernelGGL(lk, lgrid, dim3(LG::THREADS), LG::LDS, stream, reinterpret_cast<uint32_t*>(K), km32,
+                             chunkOff, chunkB0, meta, planes ? static_cast<const uint16_t*>(lo2P) : nullptr);
+        };
+        auto launch32 = [&](auto geom) {
+          using LG = decltype(geom);
           auto lk = atomicRank ? thrs_local<KT, true, LG> : thrs_local<KT, false, LG>;
-          hipLaunchKernelGGL(lk, dim3((uint32_t)maxChunks), dim3(LG::THREADS), llds, stream, K, km, startBits,
-                             nLow, chunkOff, chunkB0, meta, g_lstamps);
-        }
-      };
-      if constexpr (kBucket64) {
-        auto lk = atomicRank ? thrs_local64<KT, VB, true> : thrs_local64<KT, VB, false>;
-        hipLaunchKernelGGL(lk, dim3((uint32_t)maxChunks), dim3(Loc64::THREADS), Loc64::LDS, stream,
-                           reinterpret_cast<uint64_t*>(K), reinterpret_cast<uint64_t*>(V),
-                           KeyMap<uint64_t>{(uint64_t)km.mask, (uint64_t)km.lo, km.sh},
-                           chunkOff, chunkB0, meta);
-      } else if (local16) {
-        if constexpr (KT == 0 && VB == 0) {
-          if (count16) {
+          hipLaunchKernelGGL(lk, lgrid, dim3(LG::THREADS), LG::template lds<U>(), stream, K, km, startBits, nLow,
+                             chunkOff, chunkB0, meta, g_lstamps);
+        };
+        if (count16) {
+          if constexpr (KT == 0) {
             // persistent: one 128-KiB workgroup per CU walks the chunks
             const uint32_t cgrid = (uint32_t)std::min<uint64_t>(maxChunks, (uint64_t)cu_count());
             // planes off (or mode 1, big chunks): the items are the keys
@@ -552,22 +618,18 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
             hipLaunchKernelGGL(lk, dim3(cgrid), dim3(LocCount::THREADS), LocCount::LDS, stream,
                                reinterpret_cast<uint32_t*>(K), n, km32, chunkOff, chunkB0, meta,
                                static_cast<const uint16_t*>(lo2P), joint);
-          } else if (wide16) {
-            auto lk = atomicRank ? thrs_local16<true, Loc16Wide> : thrs_local16<false, Loc16Wide>;
-            hipLaunchKernelGGL(lk, dim3((uint32_t)maxChunks), dim3(Loc16Wide::THREADS), Loc16Wide::LDS, stream,
-                               reinterpret_cast<uint32_t*>(K), km32, chunkOff, chunkB0, meta,
-                               planes ? static_cast<const uint16_t*>(lo2P) : nullptr);
-          } else {
-            auto lk = atomicRank ? thrs_local16<true, Loc16> : thrs_local16<false, Loc16>;
-            hipLaunchKernelGGL(lk, dim3((uint32_t)maxChunks), dim3(Loc16::THREADS), Loc16::LDS, stream,
-                               reinterpret_cast<uint32_t*>(K), km32, chunkOff, chunkB0, meta,
-                               planes ? static_cast<const uint16_t*>(lo2P) : nullptr);
           }
+        } else if (wide16) {
+          launch16(Loc16Wide{});
+        } else if (small16) {
+          launch16(Loc16Small{});
+        } else if (local16) {
+          launch16(Loc16{});
+        } else if (smallLocal) {
+          launch32(LocSmall{});
+        } else {
+          launch32(LocBig{});
         }
-      } else if (smallLocal) {
-        launch_local(LocSmall{});
-      } else {
-        launch_local(LocBig{});
       }
     }
     // ---- the per-bucket fallback (thrs_fallback.hpp): big chunks only,
@@ -578,17 +640,17 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
       uint32_t* bigPos = reinterpret_cast<uint32_t*>(hyb + kBigPosOff);
       uint32_t* bigTile = reinterpret_cast<uint32_t*>(hyb + kBigTileOff);
       uint32_t* bigHist = reinterpret_cast<uint32_t*>(scratch + plan.bigHistOff);
-      ST* fb0 = reinterpret_cast<ST*>(scratch + plan.fbOff);
-      ST* fb1 = reinterpret_cast<ST*>(scratch + plan.fbOff + plan.fbBytes / 2);
+      // (the low passes reuse both look-back table sets: zeroed by thrs_big_plan)
       hipLaunchKernelGGL(thrs_big_plan, dim3(std::min<uint32_t>(256, cu_count())), dim3(kBigPlanThreads), 0, stream,
                          chunkOff, meta, bigB, bigPos, bigTile, (uint32_t)G::TILE, reinterpret_cast<uint4*>(bigHist),
-                         nLow, reinterpret_cast<uint4*>(fb0), (uint64_t)(plan.fbBytes / 16));
+                         nLow, reinterpret_cast<uint4*>(scratch + kHeaderBytes), (uint64_t)(2 * plan.setBytes / 16));
       hipLaunchKernelGGL(thrs_big_hist<KT>, dim3(cu_count()), dim3(kHistThreads),
                          (size_t)nLow * kBins * kBigCopies * 4, stream, static_cast<const U*>(keys), km, startBits, nLow,
                          chunkOff, meta, bigB, bigPos, bigHist);
       for (int p = 0; p < nLow; ++p)
         hipLaunchKernelGGL(kernelBig, dim3(gridBig), dim3(G::THREADS), lds, stream, K, keyOut, V, valOut, km,
-                           startBits + 8 * p, p, nLow, chunkOff, meta, bigB, bigPos, bigTile, bigHist, fb0, fb1, err);
+                           startBits + 8 * p, p, nLow, chunkOff, meta, bigB, bigPos, bigTile, bigHist, status[0], status[1],
+                           err);
       hipLaunchKernelGGL((thrs_big_copy<U, VW>), dim3(2048), dim3(256), 0, stream, K, keyOut, VB ? V : nullptr, valOut,
                          chunkOff, meta, bigB, bigPos);
     }

@@ -653,12 +653,6 @@ constexpr uint32_t kLocCap = LocBig::CAP;  // 18432 keys
 constexpr int kLocLogT = 12, kLocSmallLogT = 11;
 template <typename U> constexpr size_t local_lds_bytes() { return LocBig::lds<U>(); }
 
-// raw 4-byte key whose getKeyBits image is y (inverse of KeyTraits::bits, for
-// images that do not come from -0)
-template <int KT> __device__ __forceinline__ uint32_t unbits32(uint32_t y) {
-  if constexpr (KT == 2) return (y & 0x80000000u) ? (y ^ 0x80000000u) : ~y;
-  else return y;
-}
 
 struct LocChunk {
   uint32_t start, size, b0;
@@ -949,6 +943,8 @@ template <int W, int K, int WPE_ = 6, int LB_ = K> struct Loc16G {
   __device__ static uint32_t at(uint32_t s) { return (s >> 6) * ROW + (s & 63u); }
 };
 using Loc16 = Loc16G<8, 36>;
+// n <= 2^29: 9216-key chunks (uniform buckets of <= 8K keys), 6 WGs per CU
+using Loc16Small = Loc16G<4, 36, 6>;
 static_assert(Loc16::CAP == LocBig::CAP, "same chunk capacity as the 32-bit geometry (thrs_plan's cap)");
 // Wide chunks for u32 keys-only sorts above 2^30 + 2^26, whose uniform
 // buckets (n / 65536 keys) outgrow Loc16's 18432 slots: 34816 keys (8 waves x
@@ -963,7 +959,66 @@ static_assert(Loc16::CAP == LocBig::CAP, "same chunk capacity as the 32-bit geom
 #endif
 using Loc16Wide = Loc16G<THRS_WIDE_W, THRS_WIDE_K, 4, THRS_WIDE_K / 2>;
 
-template <bool ATOMIC_RANK, typename LG>
+// f32 keys, the chunk holding the zero image Z (at most one per sort): its
+// sorted 16-bit items are in the stage; the keys with image Z are +0 or -0,
+// occupy the output slots [s0, s0 + z) (s0 = the chunk's items below Z) and
+// keep their input order there (stable).  The input keys (still in place)
+// give each zero its rank among the zeros and its sign, as bits in the
+// counters' LDS (free after the rounds); the write-out takes the zeros' bit
+// patterns from there and rebuilds every other key.
+template <typename LG>
+__device__ __attribute__((noinline)) void loc16_write_zero_chunk(uint32_t* __restrict__ keys, KeyMap<uint32_t> km,
+                                                                 uint32_t start, uint32_t size, uint32_t hiBits,
+                                                                 unsigned char* smem) {
+  constexpr int KPT = LG::KPT;
+  constexpr uint32_t CHUNK = 64 * KPT;
+  static_assert(LG::CAP / 32 + LG::WAVES + 1 <= (uint32_t)LG::WAVES * kBins, "sign bits fit the counters' LDS");
+  const uint16_t* stage = reinterpret_cast<const uint16_t*>(smem);
+  uint32_t* negBits = reinterpret_cast<uint32_t*>(smem + LG::STAGE_BYTES);  // [CAP / 32]
+  uint32_t* s_wz = negBits + LG::CAP / 32;                                   // [WAVES]: zeros per wave
+  uint32_t* s_s0 = s_wz + LG::WAVES;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint32_t zlo = kimg<2>(km, 0u) & 0xFFFFu;
+  for (uint32_t i = tid; i < LG::CAP / 32 + LG::WAVES + 1; i += LG::THREADS) negBits[i] = 0;
+  lds_barrier();
+  const uint32_t* src = keys + start + w * CHUNK + lane;
+  const int32_t lim = (int32_t)size - (int32_t)(w * CHUNK + lane);
+  uint32_t nz = 0, below = 0;
+  for (int j = 0; j < KPT; ++j) {  // input position w*CHUNK + 64j + lane: the stable order
+    const bool in = j * 64 < lim;
+    const uint32_t raw = in ? src[j * 64] : 1u;
+    below += (in && (kimg<2>(km, raw) & 0xFFFFu) < zlo) ? 1u : 0u;
+    nz += (uint32_t)__builtin_popcountll(__ballot(in && (raw & 0x7FFFFFFFu) == 0));
+  }
+  if (lane == 0) s_wz[w] = nz;
+  atomicAdd(s_s0, below);
+  lds_barrier();
+  uint32_t q = 0;
+  for (uint32_t ww = 0; ww < w; ++ww) q += s_wz[ww];
+  for (int j = 0; j < KPT; ++j) {
+    const bool in = j * 64 < lim;
+    const uint32_t raw = in ? src[j * 64] : 1u;
+    const uint64_t m = __ballot(in && (raw & 0x7FFFFFFFu) == 0);
+    const uint32_t r = q + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    if (in && raw == 0x80000000u) atomicOr(&negBits[r >> 5], 1u << (r & 31));
+    q += (uint32_t)__builtin_popcountll(m);
+  }
+  lds_barrier();
+  uint32_t z = 0;
+  for (int ww = 0; ww < LG::WAVES; ++ww) z += s_wz[ww];
+  const uint32_t s0 = *s_s0;
+  const uint16_t* stw = stage + w * KPT * LG::ROW + lane;
+  uint32_t* dst = keys + start + w * CHUNK + lane;
+  for (int j = 0; j < KPT; ++j) {
+    if (j * 64 < lim) {
+      const uint32_t slot = w * CHUNK + 64 * j + lane, r = slot - s0;
+      dst[j * 64] = r < z ? (((negBits[r >> 5] >> (r & 31)) & 1u) ? 0x80000000u : 0u)
+                          : kinv<2>(km, hiBits | (uint32_t)stw[j * LG::ROW]);
+    }
+  }
+}
+
+template <int KT, bool ATOMIC_RANK, typename LG>
 __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(LG::WPE))) void thrs_local16(uint32_t* __restrict__ keys, KeyMap<uint32_t> km,
                                                             const uint32_t* __restrict__ chunkOff,
                                                             const uint32_t* __restrict__ chunkB0,
@@ -1021,8 +1076,8 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(LG:
 #pragma unroll
       for (int jj = 0; jj < LB; jj += 2) {
         const int j = h + jj;
-        const uint32_t a = (j * 64 < lim) ? (kimg<0>(km, raw[jj]) & 0xFFFFu) : 0xFFFFu;
-        const uint32_t b = (j + 1 < KPT && (j + 1) * 64 < lim) ? (kimg<0>(km, raw[jj + 1]) & 0xFFFFu) : 0xFFFFu;
+        const uint32_t a = (j * 64 < lim) ? (kimg<KT>(km, raw[jj]) & 0xFFFFu) : 0xFFFFu;
+        const uint32_t b = (j + 1 < KPT && (j + 1) * 64 < lim) ? (kimg<KT>(km, raw[jj + 1]) & 0xFFFFu) : 0xFFFFu;
         it[j >> 1] = a | (b << 16);
       }
     }
@@ -1111,6 +1166,14 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(LG:
       }
     }
   }
+  if constexpr (KT == 2) {
+    // f32: +0 and -0 share one image Z, so the chunk of Z's bucket takes its
+    // zeros' bit patterns from the input, in input order (their stable order)
+    if ((kimg<2>(km, 0u) >> 16) == chunkB0[c]) {
+      loc16_write_zero_chunk<LG>(keys, km, start, size, hiBits, smem);
+      return;
+    }
+  }
   // every stage read first (in bounds for all lanes), then the lane-conditional
   // stores: a read inside the condition would be waited for one at a time
 #pragma unroll
@@ -1120,7 +1183,7 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(LG:
     for (int jj = 0; jj < LB; ++jj) o[jj] = stw[(h + jj) * LG::ROW];
 #pragma unroll
     for (int jj = 0; jj < LB; ++jj)
-      if ((h + jj) * 64 < lim) src[(h + jj) * 64] = kinv_int(km, hiBits | o[jj]);
+      if ((h + jj) * 64 < lim) src[(h + jj) * 64] = kinv<KT>(km, hiBits | o[jj]);
   }
 }
 
@@ -1333,16 +1396,16 @@ __global__ __launch_bounds__(LocCount::THREADS) void thrs_local_count16(
 }
 
 // ------------------------------------------------------ local sort, pairs
-// sortPairs with u32 keys and 4-byte values over the whole key (startBits 0,
+// sortPairs with u32 / f32 keys and 4-byte values over the whole key (startBits 0,
 // 32 bits): chunks are single buckets (thrs_plan single mode), so a key is
 // (bucket << 16 | low16) in image space and needs only its low 16 bits plus
 // its chunk position to be carried: item = low16 << 16 | position (positions
 // < 18432 < 2^16).  The rounds sort the items by their top 16 bits, exactly
 // as the keys-only rounds (stable, lane-ordered rank); then the keys are
 // rebuilt from the bucket and written, and the values are permuted through
-// the same LDS stage by the carried positions.  (f32 keys stay on the LSD
-// path: +0 and -0 share one image and could not be rebuilt bit-exactly.)
-template <bool ATOMIC_RANK, typename LG>
+// the same LDS stage by the carried positions.  f32 keys (+0 and -0 share one
+// image, so they cannot be rebuilt bit-exactly) are permuted the same way.
+template <int KT, bool ATOMIC_RANK, typename LG>
 __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(4))) void thrs_local_pairs(
     uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, KeyMap<uint32_t> km,
     const uint32_t* __restrict__ chunkOff, const uint32_t* __restrict__ chunkB0, const uint32_t* __restrict__ meta) {
@@ -1373,7 +1436,7 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(4))
 #pragma unroll
   for (int j = 0; j < KPT; ++j) {
     const uint32_t pos = myOff + j * 64;
-    it[j] = (j * 64 < lim) ? ((kimg<0>(km, it[j]) << 16) | pos) : 0xFFFF0000u;  // padding: digits 255
+    it[j] = (j * 64 < lim) ? ((kimg<KT>(km, it[j]) << 16) | pos) : 0xFFFF0000u;  // padding: digits 255
   }
   loc_rounds<0, ATOMIC_RANK, LG>(it, ch, KeyMap<uint32_t>{0u, 0u, 0u}, 16, 2, smem, nullptr);
   pin(reinterpret_cast<uint32_t&>(lim));
@@ -1398,7 +1461,7 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(4))
       const int j = j0 + jj;
       if (j < KPT) {
         id[j / 2] |= (j * 64 < lim ? (o[jj] & 0xFFFFu) : 0u) << (16 * (j & 1));
-        if (j * 64 < lim) ksrc[j * 64] = kinv_int(km, hiImg | (o[jj] >> 16));
+        if (KT == 0 && j * 64 < lim) ksrc[j * 64] = kinv_int(km, hiImg | (o[jj] >> 16));
       }
     }
   }
@@ -1417,65 +1480,95 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(4))
     for (int jj = 0; jj < BR; ++jj)
       if (j0 + jj < KPT && (j0 + jj) * 64 < lim) vsrc[(j0 + jj) * 64] = o[jj];
   }
+  if constexpr (KT == 2) {
+    // f32 keys travel by position like the values (+0 and -0 share one image)
+    load_run<KPT>(it, keys + ch.start, myOff, ch.size, avail);
+    lds_barrier();  // every value read from the stage
+#pragma unroll
+    for (int j = 0; j < KPT; ++j)
+      if (j * 64 < lim) stage[w * CHUNK + j * 64 + lane] = it[j];
+    lds_barrier();
+#pragma unroll
+    for (int j0 = 0; j0 < KPT; j0 += BR) {
+      uint32_t o[BR];
+#pragma unroll
+      for (int jj = 0; jj < BR; ++jj)
+        if (j0 + jj < KPT) o[jj] = stage[(id[(j0 + jj) / 2] >> (16 * ((j0 + jj) & 1))) & 0xFFFFu];
+#pragma unroll
+      for (int jj = 0; jj < BR; ++jj)
+        if (j0 + jj < KPT && (j0 + jj) * 64 < lim) ksrc[(j0 + jj) * 64] = o[jj];
+    }
+  }
 }
 
-// ------------------------------------------------ local sort, 64-bit keys
-// u64 / f64 keys over the whole key (startBits 0, 64 bits), optionally with
-// 8-byte values: the bucket path's two device passes group the keys by their
-// top 16 bits; each single-bucket chunk then takes SIX in-LDS rounds on the
-// low 48 bits.  Item = low48(image) << 16 | chunk position (positions <
-// 17408 < 2^16), so the rounds sort by item bits 16..63 (stable, the same
-// count / scan / lane-ordered rank / scatter / reload as loc_rounds), and the
-// carried position permutes what cannot be rebuilt from the item: the values,
-// and f64 keys (+0 and -0 share one image).  u64 keys are rebuilt from the
-// bucket id and the item.  One workgroup of 16 waves x 17 items = 17408
-// slots: 136 KiB of 8-byte stage + 16 KiB of per-wave counters, one per CU.
-struct Loc64 {
+// ------------------------------------ local sort, carried positions (wide)
+// Full-window sorts whose keys or values cannot take the 16-bit or 32-bit
+// item kernels above: 8-byte keys (u64 / f64) with no, 4-, 8- or 16-byte
+// values, and 4-byte keys (u32 / f32) with 8- or 16-byte values.  Chunks are
+// single buckets (the top 16 bits of the image).  Item = the image's bits
+// below the bucket << 16 | chunk position (positions < 17408 < 2^16): 32-bit
+// items and two in-LDS rounds for 4-byte keys, 64-bit items and six rounds
+// for 8-byte keys -- stable count / scan / lane-ordered rank / scatter /
+// reload as loc_rounds.  The carried position then permutes, through the
+// LDS stage, what cannot be rebuilt from the item: the values, and float
+// keys (+0 and -0 share one image).  u32 / u64 keys are rebuilt from the
+// bucket and the item.  16-byte values are loaded and stored whole (one
+// 16-B access per lane, full lines) and pass the 8-byte stage in two halves.
+// One workgroup of 16 waves x 17 items = 17408 slots: 136 KiB of 8-byte
+// stage + 16 KiB of per-wave counters, one per CU.
+struct LocKV {
   static constexpr int WAVES = 16, KPT = 17, THREADS = 64 * WAVES;
   static constexpr uint32_t CAP = (uint32_t)THREADS * KPT;  // 17408
   static constexpr size_t LDS = (size_t)CAP * 8 + (size_t)WAVES * kBins * 4;
 };
-static_assert(Loc64::CAP < 65536, "positions are carried in 16 bits");
+static_assert(LocKV::CAP < 65536, "positions are carried in 16 bits");
 
 template <int KT, int VB, bool ATOMIC_RANK>
-__global__ __launch_bounds__(Loc64::THREADS) void thrs_local64(uint64_t* __restrict__ keys,
-                                                              uint64_t* __restrict__ vals, KeyMap<uint64_t> km,
-                                                              const uint32_t* __restrict__ chunkOff,
-                                                              const uint32_t* __restrict__ chunkB0,
-                                                              const uint32_t* __restrict__ meta) {
-  static_assert(KT == 1 || KT == 3, "64-bit keys");
-  static_assert(VB == 0 || VB == 8, "no values or 8-byte values");
-  constexpr int KPT = Loc64::KPT, W = Loc64::WAVES;
+__global__ __launch_bounds__(LocKV::THREADS) void thrs_local_kv(typename KeyTraits<KT>::U* __restrict__ keys,
+                                                                typename ValueWord<VB>::T* __restrict__ vals,
+                                                                KeyMap<typename KeyTraits<KT>::U> km,
+                                                                const uint32_t* __restrict__ chunkOff,
+                                                                const uint32_t* __restrict__ chunkB0,
+                                                                const uint32_t* __restrict__ meta) {
+  using U = typename KeyTraits<KT>::U;
+  constexpr int KB = (int)sizeof(U);
+  using Item = typename std::conditional<KB == 4, uint32_t, uint64_t>::type;
+  static_assert(KB == 8 || VB >= 8, "4-byte keys with 0 / 4-byte values: thrs_local16 / thrs_local / thrs_local_pairs");
+  constexpr int KPT = LocKV::KPT, W = LocKV::WAVES;
   constexpr uint32_t CHUNK = 64 * KPT;
-  constexpr bool PERMUTE_KEYS = KT == 3;  // f64: keys travel by position (their -0 is not rebuilt)
+  constexpr int ROUNDS = KB == 4 ? 2 : 6;
+  constexpr bool PERMUTE_KEYS = KT == 2 || KT == 3;  // floats travel by position (their -0 is not rebuilt)
   const uint32_t c = blockIdx.x;
   if (c >= meta[kMetaChunks]) return;
   const uint32_t start = chunkOff[c], size = chunkOff[c + 1] - start;
-  if (size == 0 || size > Loc64::CAP) return;  // big chunk: the per-bucket fallback sorts it
-  const uint64_t hiImg = (uint64_t)chunkB0[c] << 48;  // the bucket: the image's top 16 bits
+  if (size == 0 || size > LocKV::CAP) return;  // big chunk: the per-bucket fallback sorts it
+  const U hiImg = (U)chunkB0[c] << (8 * KB - 16);  // the bucket: the image's top 16 bits
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  uint64_t* stage = reinterpret_cast<uint64_t*>(smem);
-  uint32_t* s_cnt = reinterpret_cast<uint32_t*>(smem + (size_t)Loc64::CAP * 8);  // [W][256]
+  Item* stage = reinterpret_cast<Item*>(smem);
+  uint32_t* s_cnt = reinterpret_cast<uint32_t*>(smem + (size_t)LocKV::CAP * 8);  // [W][256]
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6);
   uint32_t* cnt = s_cnt + w * kBins;
-  const uint64_t* stw = stage + w * CHUNK + lane;
+  const Item* stw = stage + w * CHUNK + lane;
   const uint32_t myOff = w * CHUNK + lane;
   int32_t lim = (int32_t)size - (int32_t)myOff;
   pin(reinterpret_cast<uint32_t&>(lim));
   const int32_t limw = __builtin_amdgcn_readfirstlane((int32_t)size - (int32_t)(w * CHUNK));
   const int nItems = limw <= 0 ? 0 : min(KPT, (limw + 63) >> 6);  // items j with j*64 < limw
 
-  // items: low 48 bits of the image and the position; padding (past the
+  // items: the image below the bucket and the position; padding (past the
   // chunk) has every digit 255 and sorts last (stable: it sits at the end)
-  uint64_t it[KPT];
-  load_run<KPT>(it, keys + start, myOff, size, limw);
+  Item it[KPT];
+  {
+    U raw[KPT];
+    load_run<KPT>(raw, keys + start, myOff, size, limw);
 #pragma unroll
-  for (int j = 0; j < KPT; ++j) {
-    const uint64_t img = kimg<KT>(km, it[j]);
-    it[j] = (j * 64 < lim) ? ((img << 16) | (uint64_t)(myOff + j * 64)) : ~0xFFFFull;
+    for (int j = 0; j < KPT; ++j) {
+      const U img = kimg<KT>(km, raw[j]);
+      it[j] = (j * 64 < lim) ? (((Item)img << 16) | (Item)(myOff + j * 64)) : (Item)~(Item)0xFFFF;
+    }
   }
-  for (int r = 0; r < 6; ++r) {
+  for (int r = 0; r < ROUNDS; ++r) {
     const int shift = 16 + 8 * r;
     auto digit_of = [&](int j) -> uint32_t { return (uint32_t)(it[j] >> shift) & 0xFFu; };
 #pragma unroll
@@ -1535,7 +1628,7 @@ __global__ __launch_bounds__(Loc64::THREADS) void thrs_local64(uint64_t* __restr
     if (wfull) rank_scatter(std::true_type{});
     else rank_scatter(std::false_type{});
     lds_barrier();
-    if (r < 5) {
+    if (r + 1 < ROUNDS) {
       if (wfull) {
 #pragma unroll
         for (int j = 0; j < KPT; ++j) it[j] = stw[j * 64];
@@ -1550,35 +1643,62 @@ __global__ __launch_bounds__(Loc64::THREADS) void thrs_local64(uint64_t* __restr
   // first (in bounds for all lanes), then the lane-conditional stores
 #pragma unroll
   for (int j = 0; j < KPT; ++j) it[j] = stw[j * 64];
-  uint64_t* kdst = keys + start + myOff;
+  U* kdst = keys + start + myOff;
   if constexpr (!PERMUTE_KEYS) {
 #pragma unroll
     for (int j = 0; j < KPT; ++j)
-      if (j * 64 < lim) kdst[j * 64] = kinv_int(km, hiImg | (it[j] >> 16));  // u64: getKeyBits is the identity
+      if (j * 64 < lim) kdst[j * 64] = kinv_int(km, (U)(hiImg | (U)(it[j] >> 16)));  // integer keys: rebuilt
   }
-  if constexpr (PERMUTE_KEYS || VB == 8) {
-    // carried positions; then each permuted array goes through the stage
-    uint32_t pos[(KPT + 1) / 2];
+  // carried positions, two 16-bit halves per register
+  uint32_t pos[(KPT + 1) / 2];
 #pragma unroll
-    for (int j = 0; j < (KPT + 1) / 2; ++j) pos[j] = 0;
+  for (int j = 0; j < (KPT + 1) / 2; ++j) pos[j] = 0;
 #pragma unroll
-    for (int j = 0; j < KPT; ++j) pos[j / 2] |= (uint32_t)(it[j] & 0xFFFFu) << (16 * (j & 1));
-    auto permute = [&](uint64_t* arr) {
-      uint64_t x[KPT];
-      load_run<KPT>(x, arr + start, myOff, size, limw);
-      lds_barrier();  // every stage read of the previous step is done
+  for (int j = 0; j < KPT; ++j) pos[j / 2] |= (uint32_t)(it[j] & 0xFFFFu) << (16 * (j & 1));
+  auto pos_of = [&](int j) -> uint32_t { return (pos[j / 2] >> (16 * (j & 1))) & 0xFFFFu; };
+  // out[j] = in[pos_of(j)] through the stage, for T of 4 or 8 bytes
+  auto permute = [&](auto* arr) {
+    using T = typename std::remove_pointer<decltype(arr)>::type;
+    T* st = reinterpret_cast<T*>(smem);
+    T x[KPT];
+    load_run<KPT>(x, arr + start, myOff, size, limw);
+    lds_barrier();  // every stage read of the previous step is done
 #pragma unroll
-      for (int j = 0; j < KPT; ++j)
-        if (j < nItems) stage[myOff + j * 64] = x[j];
-      lds_barrier();
+    for (int j = 0; j < KPT; ++j)
+      if (j < nItems) st[myOff + j * 64] = x[j];
+    lds_barrier();
 #pragma unroll
-      for (int j = 0; j < KPT; ++j) x[j] = stage[(pos[j / 2] >> (16 * (j & 1))) & 0xFFFFu];
+    for (int j = 0; j < KPT; ++j) x[j] = st[pos_of(j)];
 #pragma unroll
-      for (int j = 0; j < KPT; ++j)
-        if (j * 64 < lim) arr[start + myOff + j * 64] = x[j];
-    };
-    if constexpr (PERMUTE_KEYS) permute(keys);
-    if constexpr (VB == 8) permute(vals);
+    for (int j = 0; j < KPT; ++j)
+      if (j * 64 < lim) arr[start + myOff + j * 64] = x[j];
+  };
+  if constexpr (PERMUTE_KEYS) permute(keys);
+  if constexpr (VB == 4 || VB == 8) permute(vals);
+  if constexpr (VB == 16) {
+    // whole 16-byte values in registers; the halves pass the stage in turn
+    uint4 x[KPT];
+    load_run<KPT>(x, reinterpret_cast<const uint4*>(vals) + start, myOff, size, limw);
+    uint64_t* st = reinterpret_cast<uint64_t*>(smem);
+    uint64_t o[KPT];
+    lds_barrier();
+#pragma unroll
+    for (int j = 0; j < KPT; ++j)
+      if (j < nItems) st[myOff + j * 64] = ((uint64_t)x[j].y << 32) | x[j].x;
+    lds_barrier();
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) o[j] = st[pos_of(j)];
+    lds_barrier();
+#pragma unroll
+    for (int j = 0; j < KPT; ++j)
+      if (j < nItems) st[myOff + j * 64] = ((uint64_t)x[j].w << 32) | x[j].z;
+    lds_barrier();
+    uint4* vdst = reinterpret_cast<uint4*>(vals) + start + myOff;
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) {
+      const uint64_t h = st[pos_of(j)];
+      if (j * 64 < lim) vdst[j * 64] = make_uint4((uint32_t)o[j], (uint32_t)(o[j] >> 32), (uint32_t)h, (uint32_t)(h >> 32));
+    }
   }
 }
 

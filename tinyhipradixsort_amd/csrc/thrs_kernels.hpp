@@ -85,6 +85,16 @@ __device__ __forceinline__ typename KeyTraits<KT>::U kimg(const KeyMap<typename 
 template <typename U> __device__ __forceinline__ U kinv_int(const KeyMap<U>& m, U y) {
   return ((y >> m.sh) + m.lo) ^ m.mask;
 }
+// raw 4-byte key whose getKeyBits image is y (inverse of KeyTraits::bits, for
+// images that do not come from -0: -0 and +0 have one image, this gives +0)
+template <int KT> __device__ __forceinline__ uint32_t unbits32(uint32_t y) {
+  if constexpr (KT == 2) return (y & 0x80000000u) ? (y ^ 0x80000000u) : ~y;
+  else return y;
+}
+// the 4-byte key whose image (under m) is y
+template <int KT> __device__ __forceinline__ uint32_t kinv(const KeyMap<uint32_t>& m, uint32_t y) {
+  return unbits32<KT>(kinv_int(m, y));
+}
 
 // value payloads: 4, 8 or 16 bytes moved as opaque words
 template <int VB> struct ValueWord;
@@ -1400,6 +1410,21 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
                                                      shift, myBase, status, nullptr, errFlag, chain + t, chain, g, smem,
                                                      nullptr, k, v, NoMid{}, hiPlane);
     lds_barrier();  // stage, s_gofs and s_misc are reused by the next tile
+  }
+}
+
+// Zeroing of up to three 16-byte-aligned ranges in one launch (the scratch
+// header and look-back tables at the start of every sort).
+struct ZeroRanges {
+  char* ptr[3];
+  uint64_t words[3];  // 16-byte words
+};
+__global__ __launch_bounds__(256) void thrs_zero_ranges(ZeroRanges z) {
+  const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x, stride = (uint64_t)gridDim.x * 256;
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    uint4* p = reinterpret_cast<uint4*>(z.ptr[r]);
+    for (uint64_t i = g; i < z.words[r]; i += stride) p[i] = make_uint4(0, 0, 0, 0);
   }
 }
 
