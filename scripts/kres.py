@@ -22,7 +22,7 @@ for line in sys.stdin:
 dem = subprocess.run(["c++filt"], input="\n".join(r["name"] for r in rows), capture_output=True,
                      text=True).stdout.splitlines()
 for r, d in zip(rows, dem):
-    d = d.replace("thrs_dev::", "").replace("unsigned int", "u32")
+    d = d.replace("(anonymous namespace)::", "").replace("thrs_dev::", "").replace("unsigned int", "u32")
     d = d.split("(")[0]
     if flt and flt not in d:
         continue
