@@ -176,7 +176,10 @@ int thrs_digit_histogram(const thrs_config* config, const void* keys, uint32_t n
  * bound is hit the sort's output is wrong and the failure is recorded in the
  * sort's own `temporaryBuffer` (until the next sort that uses it), and ORed
  * into a per-device sticky word in host memory.  A sort never fails because
- * of an EARLIER sort: each caller checks its own sort, either way below.
+ * of an EARLIER sort: each caller checks its own sort, either way below.  A
+ * sort with nothing to do (n > 0 but an empty or identity bit window, or a
+ * keyRange holding one key) launches no kernel and clears the word, so its
+ * check reports success.
  *   thrs_check_device_error         synchronises `stream`; returns
  *                                   THRS_ERROR_LOOKBACK_TIMEOUT if the last sort
  *                                   on `temporaryBuffer` failed;

@@ -181,19 +181,26 @@ int sort_impl(const thrs_config* cfg, const thrs_options* options, void* keys, v
   if (cfg->sortOrder != THRS_ORDER_ASCENDING && cfg->sortOrder != THRS_ORDER_DESCENDING) return THRS_ERROR_INVALID_VALUE;
   if (((endBits - startBits) % 8) != 0) return THRS_ERROR_BIT_RANGE;  // tinyhipradixsort.hpp:856
   if (startBits < 0) return THRS_ERROR_INVALID_VALUE;
-  if (n == 0 || startBits >= endBits) return THRS_SUCCESS;
+  // a sort with nothing to do launches nothing; its temporary buffer (sized
+  // for n > 0, so it holds the header) reports no device failure afterwards
+  auto noop = [&]() -> int {
+    if (n == 0 || !tmp) return THRS_SUCCESS;
+    return hipMemsetAsync(static_cast<char*>(tmp) + kErrOff, 0, 4, stream) == hipSuccess ? THRS_SUCCESS
+                                                                                         : THRS_ERROR_HIP;
+  };
+  if (n == 0 || startBits >= endBits) return noop();
   const int kb = key_bytes_of(cfg->keyType);
   const int width = kb * 8;
   int nPass = 0;  // passes that read at least one key bit; the rest are identities
   for (int i = 0; startBits + 8 * i < endBits; ++i)
     if (startBits + 8 * i < width) ++nPass;
-  if (nPass == 0) return THRS_SUCCESS;
+  if (nPass == 0) return noop();
   if (!keys || !tmp || (pairs && !vals)) return THRS_ERROR_INVALID_VALUE;
   const int vb = pairs ? value_bytes_of(cfg->valueType) : 0;
   if (opt.keyRange == 1) {
     if (kb == 4 && opt.rangeHi > 0xFFFFFFFFull) return THRS_ERROR_INVALID_VALUE;
     // every key has one image: the stable sort is the identity (full window)
-    if (opt.rangeLo == opt.rangeHi && startBits == 0 && endBits >= width) return THRS_SUCCESS;
+    if (opt.rangeLo == opt.rangeHi && startBits == 0 && endBits >= width) return noop();
   }
   const Plan plan = make_plan(cfg->keyType, vb, n);
   const bool desc = cfg->sortOrder == THRS_ORDER_DESCENDING;
