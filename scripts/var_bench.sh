@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B of libthrs variant builds (make variants -> exp/variants/): for each
 # "WORKLOAD:variant" argument (variant "base" = the in-tree libthrs.so), one
-# short bench.py run; prints ms/step, avg pass, hist and local kernel ms.
+# short bench.py run; prints ms/step and per-kind ms/sort / launches.
 cd ${GRAFT_REPO_ROOT:-/root/repo}
 mkdir -p gpurun_out
 for a in "$@"; do
@@ -11,5 +11,6 @@ for a in "$@"; do
     > gpurun_out/var_${wl}_$v.json 2>gpurun_out/var_${wl}_$v.err || { echo "FAIL $a"; tail -3 gpurun_out/var_${wl}_$v.err; exit 1; }
   python3 -c "
 import json; d=json.load(open('gpurun_out/var_${wl}_$v.json')); r=d['roofline']
-print('$wl $v', d['ms_per_step'], r['avg_launch_ms'], r['hist_avg_ms'], (r.get('local') or {}).get('avg_launch_ms'))"
+k=r['kinds']
+print('$wl $v', d['ms_per_step'], ' '.join(f\"{n}={v['ms_per_sort']}/{v['launches_per_sort']}\" for n,v in k.items()))"
 done
