@@ -19,7 +19,9 @@
 //                   big chunk (bigHist[chunk][pass][256]); the last workgroup
 //                   decides per low pass whether it RUNS -- a pass whose
 //                   digit is one value in every big chunk is the identity
-//                   (16 distinct keys: both low passes) -- and the parity
+//                   (16 distinct keys: both low passes; counted as they
+//                   happen: the count add that completes a bin to its
+//                   chunk's size marks that chunk single) -- and the parity
 //                   (which buffer holds the big chunks) of each running pass
 //   thrs_pass_big   one launch per low digit: persistent, ticket tile claims
 //                   over the concatenated big chunks' tiles (monotone tickets:
@@ -113,7 +115,7 @@ __global__ __launch_bounds__(kHistThreads) void thrs_big_hist(
   using U = typename KeyTraits<KT>::U;
   if (meta[kMetaFallback] == 0) return;
   extern __shared__ __attribute__((aligned(16))) uint32_t s_h[];  // [nLow][256][kBigCopies]
-  __shared__ uint32_t s_run, s_last;
+  __shared__ uint32_t s_last;
   const uint32_t tid = threadIdx.x, G = gridDim.x;
   const uint32_t words = (uint32_t)nLow * kBins * kBigCopies;
   for (uint32_t i = tid; i < words; i += kHistThreads) s_h[i] = 0;
@@ -125,7 +127,7 @@ __global__ __launch_bounds__(kHistThreads) void thrs_big_hist(
   if (lo < hi) {
     for (uint32_t c = big_find(bigPos, M, lo); c < M && bigPos[c] < hi; ++c) {
       const uint32_t p0 = bigPos[c], a = max(lo, p0), b = min(hi, bigPos[c + 1]);
-      const uint32_t start = chunkOff[bigB[c]];
+      const uint32_t start = chunkOff[bigB[c]], size = bigPos[c + 1] - p0;
       for (uint32_t x = a + tid; x < b; x += kHistThreads) {
         const U img = kimg<KT>(km, keys[start + (x - p0)]);
         for (int p = 0; p < nLow; ++p) {
@@ -141,7 +143,10 @@ __global__ __launch_bounds__(kHistThreads) void thrs_big_hist(
           sum += s_h[i * kBigCopies + k];
           s_h[i * kBigCopies + k] = 0;
         }
-        if (sum) atomicAdd(&bigHist[(uint64_t)c * nLow * kBins + i], sum);
+        // the add that completes a bin to the chunk's size finds the chunk
+        // single-valued on that digit (one such add per chunk and pass)
+        if (sum && atomicAdd(&bigHist[(uint64_t)c * nLow * kBins + i], sum) + sum == size)
+          atomicAdd(&meta[kMetaBigSingle + i / kBins], 1u);
       }
       __syncthreads();
     }
@@ -149,24 +154,14 @@ __global__ __launch_bounds__(kHistThreads) void thrs_big_hist(
   // the last workgroup to finish plans the low passes
   __threadfence();
   if (tid == 0) s_last = atomicAdd(&meta[kMetaBigDone], 1u) == G - 1;
-  if (tid == 0) s_run = 0;
   __syncthreads();
-  if (!s_last) return;
+  if (!s_last || tid != 0) return;
   __threadfence();
   // pass p runs unless its digit is a single value in every big chunk
-  for (uint32_t q = tid; q < M * (uint32_t)nLow; q += kHistThreads) {
-    const uint32_t c = q / nLow, p = q % nLow;
-    const uint32_t size = bigPos[c + 1] - bigPos[c];
-    const uint32_t* h = bigHist + (uint64_t)c * nLow * kBins + (uint64_t)p * kBins;
-    bool single = false;
-    for (uint32_t d = 0; d < kBins && !single; ++d) single = load_agent(&h[d]) == size;
-    if (!single) atomicOr(&s_run, 1u << p);
-  }
-  __syncthreads();
-  if (tid == 0) {
+  {
     uint32_t par = 0;
     for (int p = 0; p < nLow; ++p) {
-      const uint32_t run = (s_run >> p) & 1u;
+      const uint32_t run = load_agent(&meta[kMetaBigSingle + p]) < M;
       meta[kMetaBigPass + p] = run | (par << 1);
       par ^= run;
     }

@@ -54,6 +54,7 @@ enum {
   kMetaBigCopy = 6,  // 1: an odd number of low passes ran -- big chunks end in the temp buffer
   kMetaBigPass = 8,  // [8]: per low pass p, bit 0 = runs (not the identity for every big chunk), bit 1 = parity
   kMetaBigTicket = 16,  // [8]: per low pass p, its tile ticket
+  kMetaBigSingle = 24,  // [6]: per low pass p, big chunks whose digit p is one value
 };
 // gate masks of the gated launches: bit v set = run when the gate word is v
 constexpr uint32_t kGateMode0 = 1u << 0, kGateMode1 = 1u << 1, kGateMode2 = 1u << 2;  // on meta[kMetaMode]
@@ -934,31 +935,17 @@ __global__ __launch_bounds__(LG::THREADS) void thrs_local(typename KeyTraits<KT>
 // at (s / 64) * 66 + s % 64.  Structured inputs scatter with regular strides
 // (sorted keys: a wave's 64 slots ~288 apart, all on 2 of the 32 store banks);
 // the pad spreads them.  A wave's 64 consecutive slots stay contiguous.
-// C1 > 0: the first (low-byte) round is not stable -- keys-only items that
-// share a low byte differ in their high byte, which the second round orders,
-// or are equal -- and counts / ranks into C1 copies of the 256 counters,
-// shared by the workgroup's waves, copy (lane % C1): no two lanes of a 32-lane
-// LDS group meet on one bank unless they share lane % C1 and the digit's
-// low bits, where the per-wave counters of the stable round see the random
-// digits' bank conflicts.  C1 = 0: both rounds stable (per-wave counters).
-#ifndef THRS_LOC16_C1
-#define THRS_LOC16_C1 16
-#endif
-template <int W, int K, int WPE_ = 6, int LB_ = K, int C1_ = THRS_LOC16_C1> struct Loc16G {
-  static constexpr int WAVES = W, KPT = K, THREADS = 64 * W, NP = (K + 1) / 2, WPE = WPE_, LB = LB_, C1 = C1_;
+template <int W, int K, int WPE_ = 6, int LB_ = K> struct Loc16G {
+  static constexpr int WAVES = W, KPT = K, THREADS = 64 * W, NP = (K + 1) / 2, WPE = WPE_, LB = LB_;
   static constexpr uint32_t CAP = (uint32_t)THREADS * K;
   static constexpr uint32_t ROW = 66;                                // u16 slots per 64 items
   static constexpr size_t STAGE_BYTES = (size_t)(CAP / 64) * ROW * 2;
-  static constexpr uint32_t CNT_WORDS = (uint32_t)W * kBins > (uint32_t)C1 * kBins ? (uint32_t)W * kBins
-                                                                                     : (uint32_t)C1 * kBins;
-  static constexpr size_t LDS = STAGE_BYTES + (size_t)CNT_WORDS * 4;
-  static_assert(C1 == 0 || (C1 & (C1 - 1)) == 0, "copies: a power of two");
-  static_assert(C1 == 0 || ((uint32_t)C1 * kBins) % THREADS == 0, "the copies' scan splits evenly");
+  static constexpr size_t LDS = STAGE_BYTES + (size_t)W * kBins * 4;
   __device__ static uint32_t at(uint32_t s) { return (s >> 6) * ROW + (s & 63u); }
 };
 using Loc16 = Loc16G<8, 36>;
 // n <= 2^29: 9216-key chunks (uniform buckets of <= 8K keys), 6 WGs per CU
-using Loc16Small = Loc16G<4, 36, 6, 36, (THRS_LOC16_C1 > 8 ? 8 : THRS_LOC16_C1)>;
+using Loc16Small = Loc16G<4, 36, 6, 36>;
 static_assert(Loc16::CAP == LocBig::CAP, "same chunk capacity as the 32-bit geometry (thrs_plan's cap)");
 // Wide chunks for u32 keys-only sorts above 2^30 + 2^26, whose uniform
 // buckets (n / 65536 keys) outgrow Loc16's 18432 slots: 34816 keys (8 waves x
@@ -971,7 +958,7 @@ static_assert(Loc16::CAP == LocBig::CAP, "same chunk capacity as the 32-bit geom
 #ifndef THRS_WIDE_W
 #define THRS_WIDE_W 8
 #endif
-using Loc16Wide = Loc16G<THRS_WIDE_W, THRS_WIDE_K, 4, THRS_WIDE_K / 2, (THRS_LOC16_C1 > 8 ? 8 : THRS_LOC16_C1)>;
+using Loc16Wide = Loc16G<THRS_WIDE_W, THRS_WIDE_K, 4, THRS_WIDE_K / 2>;
 
 // f32 keys, the chunk holding the zero image Z (at most one per sort): its
 // sorted 16-bit items are in the stage; the keys with image Z are +0 or -0,
@@ -1098,83 +1085,7 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(LG:
   }
   auto item = [&](int j) -> uint32_t { return (it[j >> 1] >> ((j & 1) * 16)) & 0xFFFFu; };
 
-  if constexpr (LG::C1 > 0) {
-    // ---- round 0, not stable: C1 counter copies shared by the waves
-    constexpr int C1 = LG::C1, E = C1 * kBins / LG::THREADS;  // counters per thread in the scan
-    uint32_t* c1 = s_cnt;                                       // [256][C1]
-    auto digit0 = [&](int j) -> uint32_t { return (it[j >> 1] >> ((j & 1) * 16)) & 0xFFu; };
-    uint32_t* mine = c1 + (lane & (C1 - 1));
-    for (uint32_t i = tid; i < (uint32_t)C1 * kBins; i += LG::THREADS) c1[i] = 0;
-    lds_barrier();
-    const bool wfull = nItems == KPT;
-    if (wfull) {
-#pragma unroll
-      for (int j = 0; j < KPT; ++j)
-        __hip_atomic_fetch_add(&mine[digit0(j) * C1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    } else {
-#pragma unroll
-      for (int j = 0; j < KPT; ++j)
-        if (j < nItems) __hip_atomic_fetch_add(&mine[digit0(j) * C1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    lds_barrier();
-    {  // exclusive scan of the counters in (digit, copy) order: thread t owns E consecutive ones
-      uint32_t* s_wt = reinterpret_cast<uint32_t*>(smem);  // stage words: free until the scatter
-      uint32_t v[E], tot = 0;
-#pragma unroll
-      for (int e = 0; e < E; ++e) {
-        v[e] = c1[tid * E + e];
-        tot += v[e];
-      }
-      const uint32_t inc = wave_incl_scan(tot, lane);
-      if (lane == 63) s_wt[w] = inc;
-      lds_barrier();
-      uint32_t run = inc - tot;
-      for (uint32_t ww = 0; ww < w; ++ww) run += s_wt[ww];
-#pragma unroll
-      for (int e = 0; e < E; ++e) {
-        c1[tid * E + e] = run;
-        run += v[e];
-      }
-    }
-    lds_barrier();
-    constexpr int RB = THRS_LOC_RB;
-    auto rank_scatter0 = [&](auto fullc) __attribute__((always_inline)) {
-      constexpr bool FULL = decltype(fullc)::value;
-#pragma unroll
-      for (int j0 = 0; j0 < KPT; j0 += RB) {
-        uint32_t sl[RB];
-#pragma unroll
-        for (int jj = 0; jj < RB; ++jj) {
-          const int j = j0 + jj;
-          if (j < KPT && (FULL || j < nItems))
-            sl[jj] = __hip_atomic_fetch_add(&mine[digit0(j) * C1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-#pragma unroll
-        for (int jj = 0; jj < RB; ++jj)
-          if (j0 + jj < KPT && (FULL || j0 + jj < nItems)) stage[LG::at(sl[jj])] = (uint16_t)item(j0 + jj);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    };
-    if (wfull) rank_scatter0(std::true_type{});
-    else rank_scatter0(std::false_type{});
-    lds_barrier();
-    if (limw >= (int32_t)CHUNK) {  // reload in slot order (see below)
-#pragma unroll
-      for (int j = 0; j < KPT; j += 2) {
-        const uint32_t a = stw[j * LG::ROW];
-        const uint32_t b = (j + 1 < KPT) ? (uint32_t)stw[(j + 1) * LG::ROW] : 0xFFFFu;
-        it[j >> 1] = a | (b << 16);
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < KPT; j += 2) {
-        const uint32_t a = (j * 64 < limw) ? (uint32_t)stw[j * LG::ROW] : 0xFFFFu;
-        const uint32_t b = (j + 1 < KPT && (j + 1) * 64 < limw) ? (uint32_t)stw[(j + 1) * LG::ROW] : 0xFFFFu;
-        it[j >> 1] = a | (b << 16);
-      }
-    }
-  }
-  for (int r = LG::C1 > 0 ? 1 : 0; r < 2; ++r) {
+  for (int r = 0; r < 2; ++r) {
     const int shift = 8 * r;
     auto digit_of = [&](int j) -> uint32_t { return (it[j >> 1] >> ((j & 1) * 16 + shift)) & 0xFFu; };
 #pragma unroll
