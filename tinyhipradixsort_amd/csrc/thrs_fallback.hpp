@@ -104,6 +104,7 @@ __global__ __launch_bounds__(kBigPlanThreads) void thrs_big_plan(
 
 // LDS digit counts of the low passes: [pass][256][kBigCopies]
 constexpr int kBigCopies = 8;
+constexpr int kBigUnroll = 8;
 constexpr int kBigMaxLow = 6;  // 8-byte keys: 8 digits - the two top ones
 constexpr size_t kBigHistLds = (size_t)kBigMaxLow * kBins * kBigCopies * 4;
 
@@ -128,13 +129,25 @@ __global__ __launch_bounds__(kHistThreads) void thrs_big_hist(
     for (uint32_t c = big_find(bigPos, M, lo); c < M && bigPos[c] < hi; ++c) {
       const uint32_t p0 = bigPos[c], a = max(lo, p0), b = min(hi, bigPos[c + 1]);
       const uint32_t start = chunkOff[bigB[c]], size = bigPos[c + 1] - p0;
-      for (uint32_t x = a + tid; x < b; x += kHistThreads) {
-        const U img = kimg<KT>(km, keys[start + (x - p0)]);
+      const U* src = keys + start;  // chunk position x - p0
+      auto count = [&](U raw) {
+        const U img = kimg<KT>(km, raw);
         for (int p = 0; p < nLow; ++p) {
           const uint32_t d = (uint32_t)(img >> (startBits + 8 * p)) & 0xFFu;
           __hip_atomic_fetch_add(&my[(p * kBins + d) * kBigCopies], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
+      };
+      // kBigUnroll loads in flight per thread (one at a time leaves the
+      // workgroup latency-bound: ~1/3 of the read bandwidth)
+      uint32_t x = a + tid;
+      for (; x + (kBigUnroll - 1) * kHistThreads < b; x += kBigUnroll * kHistThreads) {
+        U r[kBigUnroll];
+#pragma unroll
+        for (int u = 0; u < kBigUnroll; ++u) r[u] = src[x - p0 + u * kHistThreads];
+#pragma unroll
+        for (int u = 0; u < kBigUnroll; ++u) count(r[u]);
       }
+      for (; x < b; x += kHistThreads) count(src[x - p0]);
       __syncthreads();
       for (uint32_t i = tid; i < (uint32_t)nLow * kBins; i += kHistThreads) {
         uint32_t sum = 0;
