@@ -1523,6 +1523,7 @@ struct LocKV {
   static constexpr size_t LDS = (size_t)CAP * 8 + (size_t)WAVES * kBins * 4;
 };
 static_assert(LocKV::CAP < 65536, "positions are carried in 16 bits");
+constexpr int kTieScan = 32;  // thrs_local_kv: longest tie run the fix-up walks
 
 template <int KT, int VB, bool ATOMIC_RANK>
 __global__ __launch_bounds__(LocKV::THREADS) void thrs_local_kv(typename KeyTraits<KT>::U* __restrict__ keys,
@@ -1569,12 +1570,13 @@ __global__ __launch_bounds__(LocKV::THREADS) void thrs_local_kv(typename KeyTrai
       it[j] = (j * 64 < lim) ? (((Item)img << 16) | (Item)(myOff + j * 64)) : (Item)~(Item)0xFFFF;
     }
   }
-  for (int r = 0; r < ROUNDS; ++r) {
-    const int shift = 16 + 8 * r;
+  const bool wfull = nItems == KPT;  // whole wave: no per-item tests (see loc_rounds)
+  // one stable round on the item bits [shift, shift + 8): count, scan, rank,
+  // scatter into the stage (sorted order)
+  auto round = [&](int shift) __attribute__((always_inline)) {
     auto digit_of = [&](int j) -> uint32_t { return (uint32_t)(it[j] >> shift) & 0xFFu; };
 #pragma unroll
     for (int i = 0; i < kBins / 64; ++i) cnt[i * 64 + lane] = 0;
-    const bool wfull = nItems == KPT;  // whole wave: no per-item tests (see loc_rounds)
     if (wfull) {
 #pragma unroll
       for (int j = 0; j < KPT; ++j)
@@ -1629,16 +1631,73 @@ __global__ __launch_bounds__(LocKV::THREADS) void thrs_local_kv(typename KeyTrai
     if (wfull) rank_scatter(std::true_type{});
     else rank_scatter(std::false_type{});
     lds_barrier();
-    if (r + 1 < ROUNDS) {
-      if (wfull) {
+  };
+  auto reload = [&]() __attribute__((always_inline)) {  // items of this lane's slots (past the chunk: padding)
+    if (wfull) {
 #pragma unroll
-        for (int j = 0; j < KPT; ++j) it[j] = stw[j * 64];
-      } else {
+      for (int j = 0; j < KPT; ++j) it[j] = stw[j * 64];
+    } else {
 #pragma unroll
-        for (int j = 0; j < KPT; ++j)
-          if (j < nItems) it[j] = stw[j * 64];
+      for (int j = 0; j < KPT; ++j)
+        if (j < nItems) it[j] = stw[j * 64];
+    }
+  };
+  auto lsd = [&]() __attribute__((always_inline)) {  // every digit below the bucket
+    for (int r = 0; r < ROUNDS; ++r) {
+      round(16 + 8 * r);
+      if (r + 1 < ROUNDS) reload();
+    }
+  };
+  if constexpr (KB == 8) {
+    // Two rounds on the 16 bits below the bucket (item bits 48..63), then
+    // each run of items sharing those bits (random keys: ~1 item in 4 is in
+    // one, mostly pairs) is insertion-sorted in place in the stage by its
+    // first slot's thread, on the whole item (the remaining 32 key bits, then
+    // the position: stable) -- 2 rounds + a fix-up instead of 6.  Runs are
+    // disjoint, and a thread reading a neighbouring run mid-sort still sees
+    // that run's 16 bits.  A run longer than kTieScan makes the workgroup
+    // restore the input order (slot = position) and take the six rounds.
+    __shared__ uint32_t s_over;
+    if (tid == 0) s_over = 0;  // (the rounds' barriers order this before any set)
+    round(48);
+    reload();
+    round(56);
+    auto pre_of = [&](uint32_t slot) -> uint32_t { return (uint32_t)(stage[slot] >> 48); };
+    bool over = false;
+    for (uint32_t h = tid; h + 1 < size; h += LocKV::THREADS) {
+      const uint32_t pre = pre_of(h);
+      if ((h > 0 && pre_of(h - 1) == pre) || pre_of(h + 1) != pre) continue;  // not a run's first slot
+      uint32_t e = h + 2;
+      while (e < size && e - h <= (uint32_t)kTieScan && pre_of(e) == pre) ++e;
+      if (e - h > (uint32_t)kTieScan) {
+        over = true;
+        continue;
+      }
+      for (uint32_t i = h + 1; i < e; ++i) {
+        const Item x = stage[i];
+        uint32_t j = i;
+        for (; j > h && stage[j - 1] > x; --j) stage[j] = stage[j - 1];
+        stage[j] = x;
       }
     }
+    if (over) s_over = 1;  // (every writer stores 1)
+    lds_barrier();
+    if (s_over != 0) {
+      // back to the input order (the position field), then the six rounds
+#pragma unroll
+      for (int j = 0; j < KPT; ++j) it[j] = stw[j * 64];
+      lds_barrier();
+#pragma unroll
+      for (int j = 0; j < KPT; ++j)
+        if (myOff + 64 * j < size) stage[(uint32_t)(it[j] & 0xFFFFu)] = it[j];
+      lds_barrier();
+#pragma unroll
+      for (int j = 0; j < KPT; ++j)
+        if (j < nItems) it[j] = (j * 64 < lim) ? stw[j * 64] : (Item)~(Item)0xFFFF;
+      lsd();
+    }
+  } else {
+    lsd();
   }
   // sorted items: this lane's output slots myOff + 64j; every stage read
   // first (in bounds for all lanes), then the lane-conditional stores
