@@ -484,6 +484,48 @@ def test_bucket_wide_payloads_vs_oracle(gpu, kt, vb, desc):
             assert np.array_equal(v, ev), (name, n)
 
 
+@pytest.mark.parametrize("kt,vb", [(O.U64, 0), (O.U64, 8), (O.F64, 8), (O.U64, 16)])
+@pytest.mark.parametrize("desc", [False, True])
+def test_local_kv_tie_runs(gpu, kt, vb, desc):
+    """thrs_local_kv on 8-byte keys sorts each chunk by the 16 bits below the
+    bucket (two rounds), then insertion-sorts every run of items sharing those
+    bits on the rest of the key and the position; a run longer than 32 items
+    sends the chunk back to input order and six rounds.  Keys here fill 256
+    buckets of ~16K keys (near the 17408-key chunk capacity) with those 16
+    bits drawn from 4096 values (runs of ~4: the fix-up), from 64 values (runs
+    of ~256: the six rounds), constant, or with whole keys repeated in runs."""
+    torch = gpu
+    rs = make_sorter(kt, vb, desc, path="bucket")
+    kdt = O.KEY_DTYPE[kt]
+    n = 1 << 22
+    r = O.splitmix64_stream(777 + vb + 2 * desc, 2 * n)
+    top = (r[:n] >> np.uint64(56)) << np.uint64(48)          # 256 buckets (the image's top 16 bits
+    low = r[n:] & np.uint64(0xFFFFFFFF)                       # differ only in their top byte)
+    cases = {
+        "runs4": top | ((r[n:] >> np.uint64(40)) & np.uint64(0xFFF)) << np.uint64(32) | low,
+        "runs256": top | ((r[n:] >> np.uint64(40)) & np.uint64(0x3F)) << np.uint64(32) | low,
+        "const16": top | np.uint64(0x1234) << np.uint64(32) | low,
+        "dupkeys": top | ((r[n:] >> np.uint64(40)) & np.uint64(0xFFF)) << np.uint64(32) | (low & np.uint64(3)),
+    }
+    for name, keys in cases.items():
+        keys = keys.astype(np.uint64)
+        if kt == O.F64:   # finite doubles with the same bit structure (exponent below all-ones)
+            keys = keys & np.uint64(0xFFEFFFFFFFFFFFFF)
+        keys = keys.view(kdt)
+        vals = None
+        if vb:
+            vals = (np.arange(n * vb // 4, dtype=np.uint32) * np.uint32(2654435761)).view(
+                {4: np.uint32, 8: np.uint64, 16: np.uint64}[vb])
+            if vb == 16:
+                vals = vals.reshape(n, 2)
+        (mode, big), k, v = _mode_after(torch, rs, keys, vals, kt, vb)
+        ek, ev = O.lsd_sort(kt, keys, vals, 0, 64, desc)
+        assert mode == 0, (name, mode, big)     # every chunk sorted locally
+        assert np.array_equal(k.view(kdt), ek.view(kdt)), name
+        if vb:
+            assert np.array_equal(v, ev), name
+
+
 @pytest.mark.parametrize("desc", [False, True])
 @pytest.mark.parametrize("geom", ["auto", "small", "wide16"])
 def test_f32_keys_only_zero_chunk(gpu, desc, geom):
