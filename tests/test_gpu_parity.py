@@ -499,8 +499,10 @@ def test_local_kv_tie_runs(gpu, kt, vb, desc):
     kdt = O.KEY_DTYPE[kt]
     n = 1 << 22
     r = O.splitmix64_stream(777 + vb + 2 * desc, 2 * n)
-    top = (r[:n] >> np.uint64(56)) << np.uint64(48)          # 256 buckets (the image's top 16 bits
-    low = r[n:] & np.uint64(0xFFFFFFFF)                       # differ only in their top byte)
+    # 256 buckets: the image's top 16 bits differ in bits 53..60 only (bit 52
+    # clear: f64 keys are finite)
+    top = (r[:n] >> np.uint64(56)) << np.uint64(53)
+    low = r[n:] & np.uint64(0xFFFFFFFF)
     cases = {
         "runs4": top | ((r[n:] >> np.uint64(40)) & np.uint64(0xFFF)) << np.uint64(32) | low,
         "runs256": top | ((r[n:] >> np.uint64(40)) & np.uint64(0x3F)) << np.uint64(32) | low,
@@ -508,10 +510,7 @@ def test_local_kv_tie_runs(gpu, kt, vb, desc):
         "dupkeys": top | ((r[n:] >> np.uint64(40)) & np.uint64(0xFFF)) << np.uint64(32) | (low & np.uint64(3)),
     }
     for name, keys in cases.items():
-        keys = keys.astype(np.uint64)
-        if kt == O.F64:   # finite doubles with the same bit structure (exponent below all-ones)
-            keys = keys & np.uint64(0xFFEFFFFFFFFFFFFF)
-        keys = keys.view(kdt)
+        keys = keys.astype(np.uint64).view(kdt)
         vals = None
         if vb:
             vals = (np.arange(n * vb // 4, dtype=np.uint32) * np.uint32(2654435761)).view(
