@@ -1699,6 +1699,12 @@ __global__ __launch_bounds__(LocKV::THREADS) void thrs_local_kv(typename KeyTrai
   } else {
     lsd();
   }
+  // 4- / 8-byte values (integer keys): their loads are issued now and land
+  // during the key write-out
+  constexpr bool PREFETCH = (VB == 4 || VB == 8) && !PERMUTE_KEYS;
+  using VW = typename ValueWord<VB>::T;
+  VW xv[PREFETCH ? KPT : 1];
+  if constexpr (PREFETCH) load_run<KPT>(xv, vals + start, myOff, size, limw);
   // sorted items: this lane's output slots myOff + 64j; every stage read
   // first (in bounds for all lanes), then the lane-conditional stores
 #pragma unroll
@@ -1717,11 +1723,15 @@ __global__ __launch_bounds__(LocKV::THREADS) void thrs_local_kv(typename KeyTrai
   for (int j = 0; j < KPT; ++j) pos[j / 2] |= (uint32_t)(it[j] & 0xFFFFu) << (16 * (j & 1));
   auto pos_of = [&](int j) -> uint32_t { return (pos[j / 2] >> (16 * (j & 1))) & 0xFFFFu; };
   // out[j] = in[pos_of(j)] through the stage, for T of 4 or 8 bytes
-  auto permute = [&](auto* arr) {
+  auto permute = [&](auto* arr, auto pre) {
     using T = typename std::remove_pointer<decltype(arr)>::type;
     T* st = reinterpret_cast<T*>(smem);
     T x[KPT];
-    load_run<KPT>(x, arr + start, myOff, size, limw);
+    if constexpr (std::is_same<decltype(pre), std::nullptr_t>::value) load_run<KPT>(x, arr + start, myOff, size, limw);
+    else {
+#pragma unroll
+      for (int j = 0; j < KPT; ++j) x[j] = pre[j];
+    }
     lds_barrier();  // every stage read of the previous step is done
 #pragma unroll
     for (int j = 0; j < KPT; ++j)
@@ -1733,8 +1743,9 @@ __global__ __launch_bounds__(LocKV::THREADS) void thrs_local_kv(typename KeyTrai
     for (int j = 0; j < KPT; ++j)
       if (j * 64 < lim) arr[start + myOff + j * 64] = x[j];
   };
-  if constexpr (PERMUTE_KEYS) permute(keys);
-  if constexpr (VB == 4 || VB == 8) permute(vals);
+  if constexpr (PERMUTE_KEYS) permute(keys, nullptr);
+  if constexpr (PREFETCH) permute(vals, xv);
+  else if constexpr (VB == 4 || VB == 8) permute(vals, nullptr);
   if constexpr (VB == 16) {
     // whole 16-byte values in registers; the halves pass the stage in turn
     uint4 x[KPT];

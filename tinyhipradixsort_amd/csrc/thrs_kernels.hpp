@@ -540,7 +540,7 @@ template <> struct PassCfg<4, 0> {
 #define THRS_K8V4_CFG 16, 16, 8, 4
 #endif
 #ifndef THRS_K8V8_CFG
-#define THRS_K8V8_CFG 8, 8, 1, 4
+#define THRS_K8V8_CFG 16, 16, 4, 4
 #endif
 #ifndef THRS_K8V16_CFG
 #define THRS_K8V16_CFG 16, 8, 8, 4
