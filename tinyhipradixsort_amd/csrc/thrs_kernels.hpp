@@ -531,19 +531,19 @@ template <> struct PassCfg<4, 0> {
 #define THRS_K4V8_CFG 16, 16, 8, 4
 #endif
 #ifndef THRS_K4V16_CFG
-#define THRS_K4V16_CFG 16, 8, 8, 4
+#define THRS_K4V16_CFG 16, 8, 4, 4
 #endif
 #ifndef THRS_K8V0_CFG
-#define THRS_K8V0_CFG 8, 16, 1, 4
+#define THRS_K8V0_CFG 16, 16, 2, 4
 #endif
 #ifndef THRS_K8V4_CFG
 #define THRS_K8V4_CFG 16, 16, 8, 4
 #endif
 #ifndef THRS_K8V8_CFG
-#define THRS_K8V8_CFG 16, 16, 4, 4
+#define THRS_K8V8_CFG 16, 16, 2, 4
 #endif
 #ifndef THRS_K8V16_CFG
-#define THRS_K8V16_CFG 16, 8, 8, 4
+#define THRS_K8V16_CFG 16, 8, 4, 4
 #endif
 #define THRS_PASS_CFG(KB_, VB_, MACRO)                                           \
   template <> struct PassCfg<KB_, VB_> {                                          \
