@@ -525,25 +525,25 @@ template <> struct PassCfg<4, 0> {
   static constexpr int WAVES = CFG[0], KPT = CFG[1], ROUNDS = CFG[2], WPE = CFG[3];
 };
 #ifndef THRS_K4V4_CFG
-#define THRS_K4V4_CFG 16, 16, 2, 4
+#define THRS_K4V4_CFG 16, 16, 1, 4
 #endif
 #ifndef THRS_K4V8_CFG
-#define THRS_K4V8_CFG 16, 16, 8, 4
+#define THRS_K4V8_CFG 16, 16, 4, 4
 #endif
 #ifndef THRS_K4V16_CFG
-#define THRS_K4V16_CFG 16, 8, 4, 4
+#define THRS_K4V16_CFG 16, 8, 2, 4
 #endif
 #ifndef THRS_K8V0_CFG
 #define THRS_K8V0_CFG 16, 16, 2, 4
 #endif
 #ifndef THRS_K8V4_CFG
-#define THRS_K8V4_CFG 16, 16, 8, 4
+#define THRS_K8V4_CFG 16, 16, 4, 4
 #endif
 #ifndef THRS_K8V8_CFG
 #define THRS_K8V8_CFG 16, 16, 2, 4
 #endif
 #ifndef THRS_K8V16_CFG
-#define THRS_K8V16_CFG 16, 8, 4, 4
+#define THRS_K8V16_CFG 16, 8, 2, 4
 #endif
 #define THRS_PASS_CFG(KB_, VB_, MACRO)                                           \
   template <> struct PassCfg<KB_, VB_> {                                          \
