@@ -517,7 +517,7 @@ template <typename ST> struct GroupTables {
 // (tiles completed per us) x (cross-XCD visibility latency, ~1-2 us under load)
 // and every step reads one 1 KiB status row.
 #ifndef THRS_K4V0_CFG
-#define THRS_K4V0_CFG 8, 32, 1, 4
+#define THRS_K4V0_CFG 16, 32, 1, 4
 #endif
 template <int KB, int VB> struct PassCfg;
 template <> struct PassCfg<4, 0> {
