@@ -244,7 +244,7 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
     g.nTiles = chain + (size + T - 1) / T;
     load_tile<KT, VB>(kin, vin, keyStart, valid, k, v);
     pass_tile<KT, VB, ST, ATOMIC_RANK, NoMid, kCodecKeys, false>(kin, kout, vin, vout, keyStart, valid, km, shift,
-                                                                myBase, status, statusNext, errFlag, tile, chain, g,
+                                                                myBase, start + size, status, statusNext, errFlag, tile, chain, g,
                                                                 smem, nullptr, k, v, NoMid{});
     lds_barrier();  // stage, s_gofs, s_misc and s_w are reused by the next tile
   }

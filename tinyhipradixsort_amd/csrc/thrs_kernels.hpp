@@ -588,6 +588,16 @@ __device__ __forceinline__ uint32_t xcc_id() {
   return x;
 }
 
+// Output start of a tile's digit-d run of cnt keys, base + total, clamped so
+// the run ends by outEnd.  Only a look-back that gave up (error word set:
+// the sort's bytes are garbage and the caller is told) or stale tables after
+// one can put a run past the end; it is still never written out of bounds.
+__device__ __forceinline__ uint32_t clamp_run(uint32_t base, uint32_t total, uint32_t cnt, uint32_t outEnd) {
+  const uint64_t pos = (uint64_t)base + total;
+  const uint64_t hi = outEnd >= cnt ? (uint64_t)(outEnd - cnt) : 0u;
+  return (uint32_t)(pos < hi ? pos : hi);
+}
+
 // Two-level look-back for digit d of one tile (THRS_GROUP > 0).  issue()
 // sends one round of status loads (this group's earlier tile rows + a window
 // of group rows); finish() consumes rounds until the walk ends, writes the
@@ -662,7 +672,7 @@ struct GroupWalk {
     }
     return stall;
   }
-  __device__ __forceinline__ void finish(uint32_t realTot, uint32_t myBase, uint32_t localStart,
+  __device__ __forceinline__ void finish(uint32_t realTot, uint32_t myBase, uint32_t outEnd, uint32_t localStart,
                                          uint32_t* s_gofs, uint32_t* s_misc, uint32_t* errFlag,
                                          uint64_t* __restrict__ stamps) {
 #ifdef THRS_STAMPS
@@ -707,7 +717,7 @@ struct GroupWalk {
 #else
     (void)s_misc;
 #endif
-    s_gofs[d] = myBase + total - localStart;
+    s_gofs[d] = clamp_run(myBase, total, realTot, outEnd) - localStart;
     if (tile == gend - 1) {
       store_agent(grp->gp + (uint64_t)g * kBins + d, Status<ST>::pre(total + realTot));
     }
@@ -799,7 +809,7 @@ __device__ __forceinline__ void pass_tile(
     const typename KeyTraits<KT>::U* __restrict__ keysIn, typename KeyTraits<KT>::U* __restrict__ keysOut,
     const typename ValueWord<VB>::T* __restrict__ valsIn, typename ValueWord<VB>::T* __restrict__ valsOut,
     uint64_t keyStart, uint32_t valid, KeyMap<typename KeyTraits<KT>::U> km, int shift, uint32_t myBase,
-    ST* __restrict__ status, ST* __restrict__ statusNext, uint32_t* __restrict__ errFlag, uint32_t tile,
+    uint32_t outEnd, ST* __restrict__ status, ST* __restrict__ statusNext, uint32_t* __restrict__ errFlag, uint32_t tile,
     uint32_t chainStart, const GroupTables<ST>& grp, unsigned char* smem, uint64_t* __restrict__ stamps,
     typename KeyTraits<KT>::U (&k)[PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::KPT],
     typename ValueWord<VB>::T (&v)[VB ? PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::KPT : 1], Mid mid,
@@ -1009,7 +1019,7 @@ __device__ __forceinline__ void pass_tile(
   // ---- D: decoupled look-back for digit d, kLookWindow rows per round trip;
   // a not-yet-published word stops the window and is re-polled.
   if constexpr (kGroup > 0 && GROUPED) {
-    if (tid < 256) gw.finish(realTot, myBase, localStart, s_gofs, s_misc, errFlag, stamps);
+    if (tid < 256) gw.finish(realTot, myBase, outEnd, localStart, s_gofs, s_misc, errFlag, stamps);
 #ifdef THRS_STAMPS
     if (stamps && lane == 0 && w < 4) {  // slots 12..15: waves 0..3 arrive at the post-walk barrier
       uint32_t dep = s_gofs[d & 255];
@@ -1062,7 +1072,7 @@ __device__ __forceinline__ void pass_tile(
       }
 #endif
     }
-    s_gofs[d] = myBase + excl - localStart;
+    s_gofs[d] = clamp_run(myBase, excl, realTot, outEnd) - localStart;
   }
   lds_barrier();
   THRS_STAMP(5);
@@ -1211,7 +1221,7 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
   typename ValueWord<VB>::T v[VB ? G::KPT : 1];
   load_tile<KT, VB>(keysIn, valsIn, (uint64_t)tile * G::TILE, tile_valid<G::TILE>(n, tile), k, v);
   pass_tile<KT, VB, ST, ATOMIC_RANK>(keysIn, keysOut, valsIn, valsOut, (uint64_t)tile * G::TILE,
-                                     tile_valid<G::TILE>(n, tile), km, shift, myBase, status,
+                                     tile_valid<G::TILE>(n, tile), km, shift, myBase, n, status,
                                      statusNext, errFlag, tile, 0, grp, smem, stamps, k, v, NoMid{});
 }
 
@@ -1322,7 +1332,7 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
     if (tile == kXbDone) break;
     load_tile<KT, VB>(keysIn, valsIn, (uint64_t)tile * G::TILE, tile_valid<G::TILE>(n, tile), k, v);
     pass_tile<KT, VB, ST, ATOMIC_RANK>(keysIn, keysOut, valsIn, valsOut, (uint64_t)tile * G::TILE,
-                                       tile_valid<G::TILE>(n, tile), km, shift, myBase, status,
+                                       tile_valid<G::TILE>(n, tile), km, shift, myBase, n, status,
                                        statusNext, errFlag, tile, 0, grp, smem, stamps, k, v, NoMid{});
     lds_barrier();  // stage, s_gofs and s_misc[0] are reused by the next tile
   }
@@ -1407,7 +1417,7 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
     const uint32_t myBase = segBase[seg * kBins + (tid & 255u)];
     load_tile<KT, VB, CODEC>(keysIn, valsIn, keyStart, valid, k, v, hiPlane);
     pass_tile<KT, VB, ST, ATOMIC_RANK, NoMid, CODEC>(keysIn, keysOut, valsIn, valsOut, keyStart, valid, km,
-                                                     shift, myBase, status, nullptr, errFlag, chain + t, chain, g, smem,
+                                                     shift, myBase, segPos[kSegs], status, nullptr, errFlag, chain + t, chain, g, smem,
                                                      nullptr, k, v, NoMid{}, hiPlane);
     lds_barrier();  // stage, s_gofs and s_misc are reused by the next tile
   }
