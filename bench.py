@@ -277,6 +277,9 @@ def build_roofline(prof, steps, n, kb, vb, pinfo, elapsed, global_keys, world, w
         kinds[KIND_NAMES[k]] = {"ms_per_sort": round(sum(eff) / steps, 4), "launches_per_sort": round(len(eff) / steps, 2),
                                 "avg_launch_ms": round(sum(eff) / len(eff), 4) if eff else None,
                                 "gated_noops_per_sort": round((len(ms) - len(eff)) / steps, 2)}
+        per = len(eff) // steps if eff and len(eff) % steps == 0 else 0
+        if per > 1:   # the same launches every sort: each one's average, in launch order
+            kinds[KIND_NAMES[k]]["by_launch_ms"] = [round(sum(eff[i::per]) / steps, 4) for i in range(per)]
     cand = {k: v for k, v in kinds.items() if k in ("pass", "local", "fallback") and v["avg_launch_ms"]}
     if not cand:
         return None
