@@ -419,16 +419,22 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   // fallback passes clear their successor's rows), all 8 claim areas, joint.
   // (one zeroing launch over up to three ranges: a set's status rows past
   // statusUsedBytes serve only the per-bucket fallback, which zeroes them)
+  // Bucket path: the look-back tables are zeroed by thrs_hist_joint (`tables`)
+  ZeroRanges tables{};
   {
     const uint64_t set0 = kHeaderBytes, set1 = kHeaderBytes + plan.setBytes;
     ZeroRanges z{};
     if (bucket) {
-      z.ptr[0] = scratch;
-      z.words[0] = (set0 + plan.statusUsedBytes) / 16;
-      z.ptr[1] = scratch + set0 + plan.statusBytes;  // set 0's group tables .. set 1's used rows
-      z.words[1] = (set1 + plan.statusUsedBytes - (set0 + plan.statusBytes)) / 16;
-      z.ptr[2] = scratch + set1 + plan.statusBytes;  // set 1's group tables, claim areas, bucket histogram
-      z.words[2] = (plan.hybridOff + kJointZero - (set1 + plan.statusBytes)) / 16;
+      z.ptr[0] = scratch;  // header
+      z.words[0] = kHeaderBytes / 16;
+      z.ptr[1] = scratch + set1 + plan.setBytes;  // claim areas, bucket histogram, meta
+      z.words[1] = (plan.hybridOff + kJointZero - (set1 + plan.setBytes)) / 16;
+      tables.ptr[0] = scratch + set0;  // set 0's used rows
+      tables.words[0] = plan.statusUsedBytes / 16;
+      tables.ptr[1] = scratch + set0 + plan.statusBytes;  // set 0's group tables .. set 1's used rows
+      tables.words[1] = (set1 + plan.statusUsedBytes - (set0 + plan.statusBytes)) / 16;
+      tables.ptr[2] = scratch + set1 + plan.statusBytes;  // set 1's group tables
+      tables.words[2] = (plan.setBytes - plan.statusBytes) / 16;
     } else {
       z.ptr[0] = scratch;
       z.words[0] = (set0 + plan.statusUsedBytes) / 16;
@@ -451,7 +457,8 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     if (bucket) {
       hipLaunchKernelGGL(thrs_hist_joint<KT>, dim3(hgrid), dim3(kHistThreads), kJointLds, stream,
                          static_cast<const U*>(keys), n, km, startBits + 8 * nLow, vec, joint,
-                         reinterpret_cast<uint32_t*>(hyb + kSegHistAOff), reinterpret_cast<uint32_t*>(hyb + kRowHistOff));
+                         reinterpret_cast<uint32_t*>(hyb + kSegHistAOff), reinterpret_cast<uint32_t*>(hyb + kRowHistOff),
+                         tables);
       if (!local32) {
         // single-bucket chunks: one workgroup per top digit
         hipLaunchKernelGGL(thrs_plan_rows, dim3(kBins), dim3(kPlanRowThreads), 0, stream, joint,

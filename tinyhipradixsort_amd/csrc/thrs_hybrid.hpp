@@ -96,13 +96,23 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
                                                                 int bucketShift, int vec,
                                                                 uint32_t* __restrict__ joint,
                                                                 uint32_t* __restrict__ segHist /* [8][256] */,
-                                                                uint32_t* __restrict__ rowHist /* [256] */) {
+                                                                uint32_t* __restrict__ rowHist /* [256] */,
+                                                                ZeroRanges tables) {
   using U = typename KeyTraits<KT>::U;
   extern __shared__ __attribute__((aligned(16))) uint32_t s_joint[];
   uint32_t* s_d2 = s_joint + kJointWords;
   uint32_t* s_log = s_d2 + kBins;
   uint32_t* s_logN = s_log + kCarryLog;
   const uint32_t tid = threadIdx.x;
+  {  // the top-digit passes' look-back tables (first read after this kernel):
+     // their zero stores ride along with this read-bound kernel
+    const uint64_t g = (uint64_t)blockIdx.x * kHistThreads + tid, stride = (uint64_t)gridDim.x * kHistThreads;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      uint4* p = reinterpret_cast<uint4*>(tables.ptr[r]);
+      for (uint64_t i = g; i < tables.words[r]; i += stride) p[i] = make_uint4(0, 0, 0, 0);
+    }
+  }
   for (uint32_t i = tid; i < kJointWords + kBins; i += kHistThreads) s_joint[i] = 0;
   if (tid == 0) *s_logN = 0;
   __syncthreads();
