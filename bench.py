@@ -84,6 +84,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--quiet", action="store_true")
     p.add_argument("--lib", default=None, help="experiments: a variant build of libthrs.so (make variants)")
+    p.add_argument("--opt", default="", help="experiments: thrs_options fields, e.g. planes=off,path=lsd")
     p.add_argument("--force-dist", action="store_true",
                    help="run the bucket-exchange path even at world size 1 (RCCL smoke test)")
     p.add_argument("--scaling", default="auto", choices=["auto", "strong", "weak"],
@@ -387,7 +388,8 @@ def main():
     if not use_dist:
         cfg = T.RadixSort.Config(keyType=T.KeyType(kt), valueType={0: T.ValueType.U32, 4: T.ValueType.U32,
                                                                    8: T.ValueType.U64, 16: T.ValueType.U128}[vb])
-        rs = T.RadixSort([], cfg)
+        opts = T.Options(**dict(kv.split("=", 1) for kv in args.opt.split(",") if kv))
+        rs = T.RadixSort([], cfg, opts)
         tdef = rs.getTemporaryBufferBytes(n)
         tmp_bytes = tdef.getTemporaryBufferBytesForSortPairs() if vb else tdef.getTemporaryBufferBytesForSortKeys()
         tmp = torch.empty(tmp_bytes, dtype=torch.uint8, device="cuda")
@@ -559,7 +561,8 @@ def main():
     # to do (< GATED_NOOP_MS) are not launches of the kernel's work
     cfg_info = T.RadixSort.Config(keyType=T.KeyType(kt), valueType={0: T.ValueType.U32, 4: T.ValueType.U32,
                                                                      8: T.ValueType.U64, 16: T.ValueType.U128}[vb])
-    pinfo = T.RadixSort([], cfg_info).pathInfo(n, 0, kb * 8, bool(vb)) if not use_dist else None
+    pinfo = T.RadixSort([], cfg_info, T.Options(**dict(kv.split("=", 1) for kv in args.opt.split(",") if kv))).pathInfo(
+        n, 0, kb * 8, bool(vb)) if not use_dist else None
     roof = build_roofline(prof, steps, n, kb, vb, pinfo, elapsed, global_keys, world, wl)
 
     cpu = None
