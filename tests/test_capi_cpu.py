@@ -76,12 +76,12 @@ def test_temporary_buffer_layout(kt, vt, n):
     assert d.getOutputValueBuffer(1000) == 1000 + d.pSumBuffer + d.keyOutBuffer
     # scratch (look-back status words) stays a modest fraction of the payload
     # (the reference's pSum region is 4*256*ceil(n/2048) = n/2 bytes, hpp:839),
-    # plus a fixed ~2.9 MiB: the 3-pass path's bucket histograms (one per XCD)
-    # and chunk table and the segmented pass's extra look-back rows; u32 keys:
-    # + the bucket path's u8 plane (n bytes: its two u16 planes fill keyOut)
+    # plus a fixed ~1.1 MiB: the 3-pass path's bucket histogram and chunk table
+    # and the segmented pass's extra look-back rows; u32 keys: + the bucket
+    # path's u8 plane (n bytes: its two u16 planes fill keyOut)
     plane = -(-n // 256) * 256 if kt == T.KeyType.U32 else 0
     if n >= (1 << 20):
-        assert d.pSumBuffer < 0.3 * d.keyOutBuffer + plane + (13 << 20) // 4
+        assert d.pSumBuffer < 0.3 * d.keyOutBuffer + plane + (3 << 20) // 2
 
 
 def test_argument_validation_needs_no_device():

@@ -83,15 +83,10 @@ struct Plan {
                           // fallback area [+ u8 plane]
 };
 
-// hybrid area: u32 joint[8][65536] | segHistA[8][256] | rowHist[256] |
-// meta[64] (all zeroed up front) | chunkOff[65537] | chunkB0[65537] | segment
-// tables of the two top-digit passes.  joint: one bucket histogram per XCD
-// (thrs_hist_joint adds in its XCD's L2; thrs_plan_rows sums them into copy 0)
-#ifndef THRS_JOINT_XCD
-#define THRS_JOINT_XCD 1
-#endif
-constexpr uint64_t kJointCopies = 8;
-constexpr uint64_t kJointBytes = kJointCopies * kBuckets * 4;
+// hybrid area: u32 joint[65536] | segHistA[8][256] | rowHist[256] | meta[64]
+// (all zeroed up front) | chunkOff[65537] | chunkB0[65537] | segment tables
+// of the two top-digit passes
+constexpr uint64_t kJointBytes = kBuckets * 4;
 constexpr uint64_t kSegHistAOff = kJointBytes;                    // per position segment: second-digit counts
 constexpr uint64_t kRowHistOff = kSegHistAOff + kSegs * 256 * 4;  // top-digit counts (thrs_hist_joint)
 constexpr uint64_t kMetaOff = kRowHistOff + 256 * 4;              // zero: thrs_plan_rows raises its flags atomically
@@ -463,7 +458,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
       hipLaunchKernelGGL(thrs_hist_joint<KT>, dim3(hgrid), dim3(kHistThreads), kJointLds, stream,
                          static_cast<const U*>(keys), n, km, startBits + 8 * nLow, vec, joint,
                          reinterpret_cast<uint32_t*>(hyb + kSegHistAOff), reinterpret_cast<uint32_t*>(hyb + kRowHistOff),
-                         tables, (local32 || !THRS_JOINT_XCD) ? 0u : (uint32_t)kBuckets);
+                         tables);
       if (!local32) {
         // single-bucket chunks: one workgroup per top digit
         hipLaunchKernelGGL(thrs_plan_rows, dim3(kBins), dim3(kPlanRowThreads), 0, stream, joint,
@@ -472,7 +467,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                            chunkOff, chunkB0, meta, reinterpret_cast<uint32_t*>(hyb + kSegInfoOff),
                            reinterpret_cast<uint32_t*>(hyb + kSegBaseOff), (uint32_t)G::TILE, (uint32_t)hgrid,
                            reinterpret_cast<uint32_t*>(hyb + kSegInfoAOff), reinterpret_cast<uint32_t*>(hyb + kSegBaseAOff),
-                           reinterpret_cast<uint32_t*>(hyb + kBigBOff), THRS_JOINT_XCD ? (uint32_t)kBuckets : 0u);
+                           reinterpret_cast<uint32_t*>(hyb + kBigBOff));
       } else {
         // chunks: whole buckets; neighbouring buckets below kLocCap/2 keys share one
         hipLaunchKernelGGL(thrs_plan, dim3(1), dim3(kPlanThreads), 0, stream, joint, n, base + nLow * kBins, chunkOff,

@@ -97,7 +97,7 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
                                                                 uint32_t* __restrict__ joint,
                                                                 uint32_t* __restrict__ segHist /* [8][256] */,
                                                                 uint32_t* __restrict__ rowHist /* [256] */,
-                                                                ZeroRanges tables, uint32_t jointStride) {
+                                                                ZeroRanges tables) {
   using U = typename KeyTraits<KT>::U;
   extern __shared__ __attribute__((aligned(16))) uint32_t s_joint[];
   uint32_t* s_d2 = s_joint + kJointWords;
@@ -115,14 +115,6 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
   }
   for (uint32_t i = tid; i < kJointWords + kBins; i += kHistThreads) s_joint[i] = 0;
   if (tid == 0) *s_logN = 0;
-  // jointStride > 0: this XCD's copy of the bucket histogram, added to in the
-  // XCD's own L2 (workgroup-scope atomics: every workgroup of one XCD shares
-  // that L2; the end of the kernel writes it back), summed by thrs_plan_rows
-  uint32_t* jx = joint + (jointStride ? (xcc_id() & 7u) * jointStride : 0u);
-  auto joint_add = [&](uint32_t b, uint32_t c) {
-    if (jointStride) __hip_atomic_fetch_add(&jx[b], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    else atomicAdd(&joint[b], c);
-  };
   __syncthreads();
   const uint64_t len = hj_len(n, gridDim.x);
   const uint64_t lo = min((uint64_t)n, (uint64_t)blockIdx.x * len), hi = min((uint64_t)n, lo + len);
@@ -151,7 +143,7 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
       if (slot < kCarryLog) {
         s_log[slot] = b;
       } else {
-        joint_add(b, 0x8000u);
+        atomicAdd(&joint[b], 0x8000u);
         atomicAdd(&segH[b & 255u], 0x8000u);
         atomicAdd(&rowHist[b >> 8], 0x8000u);
       }
@@ -267,14 +259,14 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
       first = first && !(x == b && u < t);
     }
     if (first) {
-      joint_add(b, mult * 0x8000u);
+      atomicAdd(&joint[b], mult * 0x8000u);
       atomicAdd(&segH[b & 255u], mult * 0x8000u);
       atomicAdd(&rowHist[b >> 8], mult * 0x8000u);
     }
   }
   for (uint32_t i = tid; i < kBuckets; i += kHistThreads) {
     const uint32_t c = (s_joint[i >> 1] >> ((i & 1u) << 4)) & 0xFFFFu;
-    if (c) joint_add(i, c);
+    if (c) atomicAdd(&joint[i], c);
   }
   // the range's second-digit counts (column sums; lanes d, d+1 share a word)
   static_assert(kHistThreads == 4 * kBins, "four top-digit quarters per second digit");
@@ -319,12 +311,11 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
 // tables and the chunk count.
 constexpr int kPlanRowThreads = 256;
 __global__ __launch_bounds__(kPlanRowThreads) void thrs_plan_rows(
-    uint32_t* __restrict__ joint, const uint32_t* __restrict__ rowHist, const uint32_t* __restrict__ segHistA,
+    const uint32_t* __restrict__ joint, const uint32_t* __restrict__ rowHist, const uint32_t* __restrict__ segHistA,
     uint32_t n, uint32_t cap, uint32_t* __restrict__ baseTop /* [2][256]: second, top */,
     uint32_t* __restrict__ chunkOff, uint32_t* __restrict__ chunkB0, uint32_t* __restrict__ meta,
     uint32_t* __restrict__ segInfo, uint32_t* __restrict__ segBase, uint32_t tileKeys, uint32_t histGrid,
-    uint32_t* __restrict__ segInfoA, uint32_t* __restrict__ segBaseA, uint32_t* __restrict__ bigB,
-    uint32_t jointStride) {
+    uint32_t* __restrict__ segInfoA, uint32_t* __restrict__ segBaseA, uint32_t* __restrict__ bigB) {
   __shared__ uint32_t s_w[2][4], s_base, s_b2[kBins];
   const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6, r = blockIdx.x;
   // 256-thread exclusive scan (4 waves)
@@ -346,12 +337,7 @@ __global__ __launch_bounds__(kPlanRowThreads) void thrs_plan_rows(
   const uint32_t rowTot = rowHist[t];
   const uint32_t rowEx = scan256(rowTot, 0, nullptr);
   if (t == r) s_base = rowEx;
-  uint32_t x = joint[kBins * r + t];
-  if (jointStride) {  // the per-XCD copies (thrs_hist_joint): summed into copy 0 for later readers
-#pragma unroll
-    for (uint32_t c = 1; c < 8; ++c) x += joint[c * jointStride + kBins * r + t];
-    joint[kBins * r + t] = x;
-  }
+  const uint32_t x = joint[kBins * r + t];
   const uint32_t pre = scan256(x, 1, nullptr);  // (its barrier also publishes s_base)
   const uint32_t base = s_base;
   chunkOff[kBins * r + t] = base + pre;
