@@ -1535,6 +1535,120 @@ struct LocKV {
 static_assert(LocKV::CAP < 65536, "positions are carried in 16 bits");
 constexpr int kTieScan = 32;  // thrs_local_kv: longest tie run the fix-up walks
 
+// One stable LDS round of thrs_local_kv on the item bits [shift, shift + 8)
+// of it[] (32- or 64-bit items): count (per-wave counters), scan, lane-ordered
+// rank, scatter into st (sorted order).  Items past nItems of the wave are
+// not there; the counters sit after the 64-bit stage.
+template <bool ATOMIC_RANK, typename Item>
+__device__ __forceinline__ void kv_round(Item (&it)[LocKV::KPT], Item* st, int shift, unsigned char* smem, int nItems) {
+  constexpr int KPT = LocKV::KPT, W = LocKV::WAVES;
+  uint32_t* s_cnt = reinterpret_cast<uint32_t*>(smem + (size_t)LocKV::CAP * 8);  // [W][256]
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  uint32_t* cnt = s_cnt + w * kBins;
+  const bool wfull = nItems == KPT;  // whole wave: no per-item tests (see loc_rounds)
+  auto digit_of = [&](int j) -> uint32_t { return (uint32_t)(it[j] >> shift) & 0xFFu; };
+#pragma unroll
+  for (int i = 0; i < kBins / 64; ++i) cnt[i * 64 + lane] = 0;
+  if (wfull) {
+#pragma unroll
+    for (int j = 0; j < KPT; ++j)
+      __hip_atomic_fetch_add(&cnt[digit_of(j)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  } else {
+#pragma unroll
+    for (int j = 0; j < KPT; ++j)
+      if (j < nItems) __hip_atomic_fetch_add(&cnt[digit_of(j)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  lds_barrier();
+  {  // digit totals over the waves -> block exclusive scan -> per-wave running offsets
+    uint32_t* s_wt = reinterpret_cast<uint32_t*>(smem);  // stage words: reloaded into registers before each round
+    uint32_t cw[W], tot = 0, inc = 0;
+    if (tid < kBins) {
+#pragma unroll
+      for (int ww = 0; ww < W; ++ww) {
+        cw[ww] = s_cnt[ww * kBins + tid];
+        tot += cw[ww];
+      }
+      inc = wave_incl_scan(tot, lane);
+      if (lane == 63) s_wt[w] = inc;
+    }
+    lds_barrier();
+    if (tid < kBins) {
+      const uint32_t w0 = s_wt[0], w1 = s_wt[1], w2 = s_wt[2];
+      uint32_t run = inc - tot + (w > 0 ? w0 : 0u) + (w > 1 ? w1 : 0u) + (w > 2 ? w2 : 0u);
+#pragma unroll
+      for (int ww = 0; ww < W; ++ww) {
+        s_cnt[ww * kBins + tid] = run;
+        run += cw[ww];
+      }
+    }
+  }
+  lds_barrier();
+  constexpr int RB = 9;
+  auto rank_scatter = [&](auto fullc) __attribute__((always_inline)) {
+    constexpr bool FULL = decltype(fullc)::value;
+#pragma unroll
+    for (int j0 = 0; j0 < KPT; j0 += RB) {
+      uint32_t sl[RB];
+#pragma unroll
+      for (int jj = 0; jj < RB; ++jj) {
+        const int j = j0 + jj;
+        if (j < KPT && (FULL || j < nItems)) sl[jj] = wave_rank<ATOMIC_RANK>(cnt, digit_of(j), lane, false);
+      }
+#pragma unroll
+      for (int jj = 0; jj < RB; ++jj)
+        if (j0 + jj < KPT && (FULL || j0 + jj < nItems)) st[sl[jj]] = it[j0 + jj];
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  if (wfull) rank_scatter(std::true_type{});
+  else rank_scatter(std::false_type{});
+  lds_barrier();
+}
+
+// thrs_local_kv, 8-byte keys, a tie run longer than kTieScan: from the
+// 32-bit items sorted by the 16 bits below the bucket (stage st) and the
+// image's low 32 bits (low[position]), back to input order as 64-bit items
+// (the image's low 48 bits << 16 | position) in the same LDS seen as one
+// 64-bit stage, then six rounds; leaves the sorted items in that stage.  A
+// call (not inlined): the caller's live registers (prefetched values) are
+// saved around it instead of squeezing the six rounds.
+template <bool ATOMIC_RANK>
+__device__ __noinline__ void kv8_six_rounds(unsigned char* smem, uint32_t size) {
+  constexpr int KPT = LocKV::KPT;
+  constexpr uint32_t CHUNK = 64 * KPT;
+  const uint32_t* st = reinterpret_cast<const uint32_t*>(smem);
+  const uint32_t* low = st + LocKV::CAP;
+  uint64_t* st64 = reinterpret_cast<uint64_t*>(smem);
+  const uint32_t lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t myOff = w * CHUNK + lane;
+  const int32_t lim = (int32_t)size - (int32_t)myOff;
+  const int32_t limw = __builtin_amdgcn_readfirstlane((int32_t)size - (int32_t)(w * CHUNK));
+  const int nItems = limw <= 0 ? 0 : min(KPT, (limw + 63) >> 6);
+  uint64_t it[KPT];
+#pragma unroll
+  for (int j = 0; j < KPT; ++j) {
+    const uint32_t v = st[myOff + j * 64];
+    it[j] = ((uint64_t)(v >> 16) << 48) | ((uint64_t)low[v & 0xFFFFu] << 16) | (v & 0xFFFFu);
+  }
+  lds_barrier();
+#pragma unroll
+  for (int j = 0; j < KPT; ++j)  // back to the input order (the position field)
+    if (myOff + 64 * j < size) st64[(uint32_t)(it[j] & 0xFFFFu)] = it[j];
+  lds_barrier();
+#pragma unroll
+  for (int j = 0; j < KPT; ++j)
+    if (j < nItems) it[j] = (j * 64 < lim) ? st64[myOff + j * 64] : ~(uint64_t)0xFFFF;
+  for (int r = 0; r < 6; ++r) {
+    kv_round<ATOMIC_RANK>(it, st64, 16 + 8 * r, smem, nItems);
+    if (r < 5) {
+#pragma unroll
+      for (int j = 0; j < KPT; ++j)
+        if (j < nItems) it[j] = st64[myOff + j * 64];
+    }
+  }
+}
+
 template <int KT, int VB, bool ATOMIC_RANK>
 __global__ __launch_bounds__(LocKV::THREADS) void thrs_local_kv(typename KeyTraits<KT>::U* __restrict__ keys,
                                                                 typename ValueWord<VB>::T* __restrict__ vals,
@@ -1546,9 +1660,8 @@ __global__ __launch_bounds__(LocKV::THREADS) void thrs_local_kv(typename KeyTrai
   constexpr int KB = (int)sizeof(U);
   using Item = typename std::conditional<KB == 4, uint32_t, uint64_t>::type;
   static_assert(KB == 8 || VB >= 8, "4-byte keys with 0 / 4-byte values: thrs_local16 / thrs_local / thrs_local_pairs");
-  constexpr int KPT = LocKV::KPT, W = LocKV::WAVES;
+  constexpr int KPT = LocKV::KPT;
   constexpr uint32_t CHUNK = 64 * KPT;
-  constexpr int ROUNDS = KB == 4 ? 2 : 6;
   constexpr bool PERMUTE_KEYS = KT == 2 || KT == 3;  // floats travel by position (their -0 is not rebuilt)
   const uint32_t c = blockIdx.x;
   if (c >= meta[kMetaChunks]) return;
@@ -1556,123 +1669,95 @@ __global__ __launch_bounds__(LocKV::THREADS) void thrs_local_kv(typename KeyTrai
   if (size == 0 || size > LocKV::CAP) return;  // big chunk: the per-bucket fallback sorts it
   const U hiImg = (U)chunkB0[c] << (8 * KB - 16);  // the bucket: the image's top 16 bits
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  Item* stage = reinterpret_cast<Item*>(smem);
-  uint32_t* s_cnt = reinterpret_cast<uint32_t*>(smem + (size_t)LocKV::CAP * 8);  // [W][256]
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  uint32_t* cnt = s_cnt + w * kBins;
-  const Item* stw = stage + w * CHUNK + lane;
   const uint32_t myOff = w * CHUNK + lane;
   int32_t lim = (int32_t)size - (int32_t)myOff;
   pin(reinterpret_cast<uint32_t&>(lim));
   const int32_t limw = __builtin_amdgcn_readfirstlane((int32_t)size - (int32_t)(w * CHUNK));
   const int nItems = limw <= 0 ? 0 : min(KPT, (limw + 63) >> 6);  // items j with j*64 < limw
 
-  // items: the image below the bucket and the position; padding (past the
-  // chunk) has every digit 255 and sorts last (stable: it sits at the end)
-  Item it[KPT];
-  {
-    U raw[KPT];
-    load_run<KPT>(raw, keys + start, myOff, size, limw);
-#pragma unroll
-    for (int j = 0; j < KPT; ++j) {
-      const U img = kimg<KT>(km, raw[j]);
-      it[j] = (j * 64 < lim) ? (((Item)img << 16) | (Item)(myOff + j * 64)) : (Item)~(Item)0xFFFF;
-    }
-  }
   const bool wfull = nItems == KPT;  // whole wave: no per-item tests (see loc_rounds)
-  // one stable round on the item bits [shift, shift + 8): count, scan, rank,
-  // scatter into the stage (sorted order)
-  auto round = [&](int shift) __attribute__((always_inline)) {
-    auto digit_of = [&](int j) -> uint32_t { return (uint32_t)(it[j] >> shift) & 0xFFu; };
-#pragma unroll
-    for (int i = 0; i < kBins / 64; ++i) cnt[i * 64 + lane] = 0;
+  auto round = [&](auto& it, auto* st, int shift) __attribute__((always_inline)) {
+    kv_round<ATOMIC_RANK>(it, st, shift, smem, nItems);
+  };
+  auto reload = [&](auto& it, const auto* st) __attribute__((always_inline)) {  // this lane's slots (past the chunk: padding)
     if (wfull) {
 #pragma unroll
-      for (int j = 0; j < KPT; ++j)
-        __hip_atomic_fetch_add(&cnt[digit_of(j)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      for (int j = 0; j < KPT; ++j) it[j] = st[myOff + j * 64];
     } else {
 #pragma unroll
       for (int j = 0; j < KPT; ++j)
-        if (j < nItems) __hip_atomic_fetch_add(&cnt[digit_of(j)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (j < nItems) it[j] = st[myOff + j * 64];
     }
-    lds_barrier();
-    {  // digit totals over the waves -> block exclusive scan -> per-wave running offsets
-      uint32_t* s_wt = reinterpret_cast<uint32_t*>(smem);  // stage words: free until the scatter
-      uint32_t cw[W], tot = 0, inc = 0;
-      if (tid < kBins) {
-#pragma unroll
-        for (int ww = 0; ww < W; ++ww) {
-          cw[ww] = s_cnt[ww * kBins + tid];
-          tot += cw[ww];
-        }
-        inc = wave_incl_scan(tot, lane);
-        if (lane == 63) s_wt[w] = inc;
-      }
-      lds_barrier();
-      if (tid < kBins) {
-        const uint32_t w0 = s_wt[0], w1 = s_wt[1], w2 = s_wt[2];
-        uint32_t run = inc - tot + (w > 0 ? w0 : 0u) + (w > 1 ? w1 : 0u) + (w > 2 ? w2 : 0u);
-#pragma unroll
-        for (int ww = 0; ww < W; ++ww) {
-          s_cnt[ww * kBins + tid] = run;
-          run += cw[ww];
-        }
-      }
-    }
-    lds_barrier();
-    constexpr int RB = 9;
-    auto rank_scatter = [&](auto fullc) __attribute__((always_inline)) {
-      constexpr bool FULL = decltype(fullc)::value;
-#pragma unroll
-      for (int j0 = 0; j0 < KPT; j0 += RB) {
-        uint32_t sl[RB];
-#pragma unroll
-        for (int jj = 0; jj < RB; ++jj) {
-          const int j = j0 + jj;
-          if (j < KPT && (FULL || j < nItems)) sl[jj] = wave_rank<ATOMIC_RANK>(cnt, digit_of(j), lane, false);
-        }
-#pragma unroll
-        for (int jj = 0; jj < RB; ++jj)
-          if (j0 + jj < KPT && (FULL || j0 + jj < nItems)) stage[sl[jj]] = it[j0 + jj];
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    };
-    if (wfull) rank_scatter(std::true_type{});
-    else rank_scatter(std::false_type{});
-    lds_barrier();
   };
-  auto reload = [&]() __attribute__((always_inline)) {  // items of this lane's slots (past the chunk: padding)
-    if (wfull) {
-#pragma unroll
-      for (int j = 0; j < KPT; ++j) it[j] = stw[j * 64];
-    } else {
+  // 4- / 8-byte values with integer keys: loaded now, used after the sort
+  // (the loads land while the workgroup works in LDS)
+  constexpr bool PREFETCH = (VB == 4 || VB == 8) && !PERMUTE_KEYS;
+  using VW = typename ValueWord<VB>::T;
+  VW xv[PREFETCH ? KPT : 1];
+  // the sorted chunk, per output slot myOff + 64j: the image below the
+  // bucket, and the input position
+  Item img[KPT];
+  uint32_t pos[(KPT + 1) / 2];
+  if constexpr (KB == 4) {
+    // items: the image's low 16 bits << 16 | position; padding (past the
+    // chunk) sorts last (stable: it sits at the end)
+    uint32_t it[KPT];
+    {
+      U raw[KPT];
+      load_run<KPT>(raw, keys + start, myOff, size, limw);
+      if constexpr (PREFETCH) load_run<KPT>(xv, vals + start, myOff, size, limw);
 #pragma unroll
       for (int j = 0; j < KPT; ++j)
-        if (j < nItems) it[j] = stw[j * 64];
+        it[j] = (j * 64 < lim) ? ((uint32_t)kimg<KT>(km, raw[j]) << 16) | (myOff + j * 64) : 0xFFFF0000u;
     }
-  };
-  auto lsd = [&]() __attribute__((always_inline)) {  // every digit below the bucket
-    for (int r = 0; r < ROUNDS; ++r) {
-      round(16 + 8 * r);
-      if (r + 1 < ROUNDS) reload();
-    }
-  };
-  if constexpr (KB == 8) {
-    // Two rounds on the 16 bits below the bucket (item bits 48..63), then
-    // each run of items sharing those bits (random keys: ~1 item in 4 is in
-    // one, mostly pairs) is insertion-sorted in place in the stage by its
-    // first slot's thread, on the whole item (the remaining 32 key bits, then
-    // the position: stable) -- 2 rounds + a fix-up instead of 6.  Runs are
-    // disjoint, and a thread reading a neighbouring run mid-sort still sees
-    // that run's 16 bits.  A run longer than kTieScan makes the workgroup
-    // restore the input order (slot = position) and take the six rounds.
+    uint32_t* st = reinterpret_cast<uint32_t*>(smem);
+    round(it, st, 16);
+    reload(it, st);
+    round(it, st, 24);
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) it[j] = st[myOff + j * 64];
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) img[j] = it[j] >> 16;
+#pragma unroll
+    for (int j = 0; j < (KPT + 1) / 2; ++j) pos[j] = 0;
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) pos[j / 2] |= (it[j] & 0xFFFFu) << (16 * (j & 1));
+  } else {
+    // 8-byte keys.  Items are 32-bit: the 16 image bits below the bucket
+    // (bits 32..47) << 16 | position; the image's low 32 bits wait in LDS
+    // (low[position]).  Two rounds sort by those 16 bits; then each run of
+    // items sharing them (random keys: ~1 item in 4 is in one, mostly pairs)
+    // is insertion-sorted in place by its first slot's thread on (low bits,
+    // position): stable.  Runs are disjoint, and a thread reading a
+    // neighbouring run mid-sort still sees that run's 16 bits.  A run longer
+    // than kTieScan makes the workgroup restore the input order and take six
+    // rounds on 64-bit items (the image's low 48 bits << 16 | position), in
+    // the same LDS seen as one 64-bit stage.
+    uint32_t* st = reinterpret_cast<uint32_t*>(smem);
+    uint32_t* low = st + LocKV::CAP;
+    uint64_t* st64 = reinterpret_cast<uint64_t*>(smem);
     __shared__ uint32_t s_over;
     if (tid == 0) s_over = 0;  // (the rounds' barriers order this before any set)
-    round(48);
-    reload();
-    round(56);
-    auto pre_of = [&](uint32_t slot) -> uint32_t { return (uint32_t)(stage[slot] >> 48); };
+    uint32_t it[KPT];
+    {
+      U raw[KPT];
+      load_run<KPT>(raw, keys + start, myOff, size, limw);
+      if constexpr (PREFETCH) load_run<KPT>(xv, vals + start, myOff, size, limw);
+#pragma unroll
+      for (int j = 0; j < KPT; ++j) {
+        const uint64_t im = kimg<KT>(km, raw[j]);
+        const uint32_t p = myOff + j * 64;
+        if (j * 64 < lim) low[p] = (uint32_t)im;
+        it[j] = (j * 64 < lim) ? ((uint32_t)(im >> 32) << 16) | p : 0xFFFF0000u | p;
+      }
+    }
+    round(it, st, 16);
+    reload(it, st);
+    round(it, st, 24);
+    auto pre_of = [&](uint32_t slot) -> uint32_t { return st[slot] >> 16; };
+    auto key_of = [&](uint32_t v) -> uint64_t { return ((uint64_t)low[v & 0xFFFFu] << 16) | (v & 0xFFFFu); };
     bool over = false;
     for (uint32_t h = tid; h + 1 < size; h += LocKV::THREADS) {
       const uint32_t pre = pre_of(h);
@@ -1684,53 +1769,44 @@ __global__ __launch_bounds__(LocKV::THREADS) void thrs_local_kv(typename KeyTrai
         continue;
       }
       for (uint32_t i = h + 1; i < e; ++i) {
-        const Item x = stage[i];
+        const uint32_t x = st[i];
+        const uint64_t kx = key_of(x);
         uint32_t j = i;
-        for (; j > h && stage[j - 1] > x; --j) stage[j] = stage[j - 1];
-        stage[j] = x;
+        for (; j > h && key_of(st[j - 1]) > kx; --j) st[j] = st[j - 1];
+        st[j] = x;
       }
     }
     if (over) s_over = 1;  // (every writer stores 1)
     lds_barrier();
-    if (s_over != 0) {
-      // back to the input order (the position field), then the six rounds
+    if (s_over == 0) {
 #pragma unroll
-      for (int j = 0; j < KPT; ++j) it[j] = stw[j * 64];
-      lds_barrier();
+      for (int j = 0; j < KPT; ++j) it[j] = st[myOff + j * 64];
 #pragma unroll
-      for (int j = 0; j < KPT; ++j)
-        if (myOff + 64 * j < size) stage[(uint32_t)(it[j] & 0xFFFFu)] = it[j];
-      lds_barrier();
+      for (int j = 0; j < KPT; ++j) img[j] = ((uint64_t)(it[j] >> 16) << 32) | low[it[j] & 0xFFFFu];
 #pragma unroll
-      for (int j = 0; j < KPT; ++j)
-        if (j < nItems) it[j] = (j * 64 < lim) ? stw[j * 64] : (Item)~(Item)0xFFFF;
-      lsd();
+      for (int j = 0; j < (KPT + 1) / 2; ++j) pos[j] = 0;
+#pragma unroll
+      for (int j = 0; j < KPT; ++j) pos[j / 2] |= (it[j] & 0xFFFFu) << (16 * (j & 1));
+    } else {
+      kv8_six_rounds<ATOMIC_RANK>(smem, size);  // (a call: its registers are its own)
+#pragma unroll
+      for (int j = 0; j < KPT; ++j) {
+        const uint64_t v = st64[myOff + j * 64];
+        img[j] = v >> 16;
+      }
+#pragma unroll
+      for (int j = 0; j < (KPT + 1) / 2; ++j) pos[j] = 0;
+#pragma unroll
+      for (int j = 0; j < KPT; ++j) pos[j / 2] |= (uint32_t)(st64[myOff + j * 64] & 0xFFFFu) << (16 * (j & 1));
     }
-  } else {
-    lsd();
   }
-  // 4- / 8-byte values (integer keys): their loads are issued now and land
-  // during the key write-out
-  constexpr bool PREFETCH = (VB == 4 || VB == 8) && !PERMUTE_KEYS;
-  using VW = typename ValueWord<VB>::T;
-  VW xv[PREFETCH ? KPT : 1];
-  if constexpr (PREFETCH) load_run<KPT>(xv, vals + start, myOff, size, limw);
-  // sorted items: this lane's output slots myOff + 64j; every stage read
-  // first (in bounds for all lanes), then the lane-conditional stores
-#pragma unroll
-  for (int j = 0; j < KPT; ++j) it[j] = stw[j * 64];
   U* kdst = keys + start + myOff;
   if constexpr (!PERMUTE_KEYS) {
 #pragma unroll
     for (int j = 0; j < KPT; ++j)
-      if (j * 64 < lim) kdst[j * 64] = kinv_int(km, (U)(hiImg | (U)(it[j] >> 16)));  // integer keys: rebuilt
+      if (j * 64 < lim) kdst[j * 64] = kinv_int(km, (U)(hiImg | (U)img[j]));  // integer keys: rebuilt
   }
-  // carried positions, two 16-bit halves per register
-  uint32_t pos[(KPT + 1) / 2];
-#pragma unroll
-  for (int j = 0; j < (KPT + 1) / 2; ++j) pos[j] = 0;
-#pragma unroll
-  for (int j = 0; j < KPT; ++j) pos[j / 2] |= (uint32_t)(it[j] & 0xFFFFu) << (16 * (j & 1));
+  // carried positions: two 16-bit halves per register
   auto pos_of = [&](int j) -> uint32_t { return (pos[j / 2] >> (16 * (j & 1))) & 0xFFFFu; };
   // out[j] = in[pos_of(j)] through the stage, for T of 4 or 8 bytes
   auto permute = [&](auto* arr, auto pre) {
