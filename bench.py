@@ -85,6 +85,8 @@ def parse():
     p.add_argument("--quiet", action="store_true")
     p.add_argument("--lib", default=None, help="experiments: a variant build of libthrs.so (make variants)")
     p.add_argument("--opt", default="", help="experiments: thrs_options fields, e.g. planes=off,path=lsd")
+    p.add_argument("--unchecked", action="store_true",
+                   help="experiments only: skip the output check (timing a deliberately incomplete variant build)")
     p.add_argument("--force-dist", action="store_true",
                    help="run the bucket-exchange path even at world size 1 (RCCL smoke test)")
     p.add_argument("--scaling", default="auto", choices=["auto", "strong", "weak"],
@@ -454,10 +456,10 @@ def main():
         rs.checkDeviceError(tmp)      # raises on a look-back / claim timeout in any timed step
         # correctness of the last timed step (outside the timed region)
         last = steps - 1
-        bad = TU.count_unsorted(kt, keys[last], n, 0, kb * 8)
+        bad = 0 if args.unchecked else TU.count_unsorted(kt, keys[last], n, 0, kb * 8)
         if bad:
             raise SystemExit(f"bench: output of the last step is not sorted ({bad} inversions)")
-        if vb:
+        if vb and not args.unchecked:
             chk = TU.check_pairs(kt, vb, keys_in0, keys[last], vals[last], n, 0, kb * 8)
             if chk["gather_mismatch"] or chk["unstable"]:
                 raise SystemExit(f"bench: pairs output of the last step is wrong: {chk}")

@@ -11,7 +11,7 @@ for a in "$@"; do
   lib=""; [ "$v" != base ] && lib="--lib exp/variants/libthrs_$v.so"
   tag=$v${o:+_$(echo $o | tr ',=' '__')}
   timeout -k 10 200 python -u bench.py --workload $wl --steps 5 --warmup 1 --cpu-baseline off --vendor off --ref-gpu off $lib \
-    ${o:+--opt $o} > gpurun_out/var_${wl}_$tag.json 2>gpurun_out/var_${wl}_$tag.err || { echo "FAIL $a"; tail -3 gpurun_out/var_${wl}_$tag.err; exit 1; }
+    ${o:+--opt $o} ${VB_EXTRA:-} > gpurun_out/var_${wl}_$tag.json 2>gpurun_out/var_${wl}_$tag.err || { echo "FAIL $a"; tail -3 gpurun_out/var_${wl}_$tag.err; exit 1; }
   python3 -c "
 import json; d=json.load(open('gpurun_out/var_${wl}_$tag.json')); r=d['roofline']
 k=r['kinds']

@@ -101,6 +101,9 @@ constexpr uint64_t kSegBaseAOff = kSegInfoAOff + 512;
 constexpr uint64_t kBigBOff = kSegBaseAOff + kSegs * 256 * 4;
 constexpr uint64_t kBigPosOff = kBigBOff + round_up_c((kBuckets + 1) * 4, 256);
 constexpr uint64_t kBigTileOff = kBigPosOff + round_up_c((kBuckets + 1) * 4, 256);
+#ifndef THRS_KV2
+#define THRS_KV2 1
+#endif
 constexpr uint64_t kKvBailOff = kBigTileOff + round_up_c((kBuckets + 1) * 4, 256);  // thrs_local_kv2 hand-over list
 constexpr uint64_t kHybridBytes = kKvBailOff + round_up_c(kBuckets * 4, 256);
 // the smallest local-sort capacity (LocSmall): a big chunk holds more keys
@@ -597,7 +600,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
       // every bucket a chunk, empty or not)
       const uint64_t maxChunks = !local32 ? kBuckets : std::min<uint64_t>(kBuckets, 256 + 2 * (uint64_t)n);
       const dim3 lgrid((uint32_t)maxChunks);
-      if constexpr (kKV && sizeof(U) == 8 && VB <= 8) {
+      if constexpr (kKV && sizeof(U) == 8 && VB <= 8 && THRS_KV2) {
         // two 76-KiB workgroups per CU; chunks with long tie runs are handed
         // to the 152-KiB kernel (persistent over the list, ~5 us when empty)
         uint32_t* kvBail = reinterpret_cast<uint32_t*>(hyb + kKvBailOff);

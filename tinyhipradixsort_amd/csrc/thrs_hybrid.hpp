@@ -2118,7 +2118,10 @@ __global__ __launch_bounds__(LocKV2::THREADS) __attribute__((amdgpu_waves_per_eu
   typename ValueWord<VB>::T* vc = vals + start;
   auto ld = [](const auto* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
   bool over = false;
-  for (uint32_t h = tid; h + 1 < size; h += LocKV2::THREADS) {
+#ifndef THRS_KV2_TIEFIX
+#define THRS_KV2_TIEFIX 1
+#endif
+  for (uint32_t h = tid; THRS_KV2_TIEFIX && h + 1 < size; h += LocKV2::THREADS) {
     const uint32_t pre = st[h];
     if ((h > 0 && st[h - 1] == pre) || st[h + 1] != pre) continue;  // not a run's first slot
     uint32_t e = h + 2;
