@@ -303,8 +303,12 @@ def build_roofline(prof, steps, n, kb, vb, pinfo, elapsed, global_keys, world, w
     # whole sort: B_alg = P*2*N*(K+V) for P 8-bit digits, the
     # work of P LSD passes whatever path ran ...
     passes = kb
+    # (an LSD-equivalent rate: the bucket path moves fewer bytes than P LSD
+    # passes, so it can exceed the HBM peak -- then it is no fraction of a
+    # roofline and is withheld; sort_min_frac below is the roofline figure)
     roof["sort_alg_GBps"] = round(passes * 2 * global_keys * (kb + vb) / step_s / 1e9, 1)
-    roof["sort_frac_of_peak"] = round(roof["sort_alg_GBps"] / PEAK_HBM_GBS / max(1, world), 4)
+    frac_alg = roof["sort_alg_GBps"] / PEAK_HBM_GBS / max(1, world)
+    roof["sort_frac_of_peak"] = round(frac_alg, 4) if frac_alg <= 1.0 else None
     # ... and on the bytes the path that ran must move at least (thrs_path_info)
     if pinfo:
         roof["path"] = pinfo

@@ -101,11 +101,7 @@ constexpr uint64_t kSegBaseAOff = kSegInfoAOff + 512;
 constexpr uint64_t kBigBOff = kSegBaseAOff + kSegs * 256 * 4;
 constexpr uint64_t kBigPosOff = kBigBOff + round_up_c((kBuckets + 1) * 4, 256);
 constexpr uint64_t kBigTileOff = kBigPosOff + round_up_c((kBuckets + 1) * 4, 256);
-#ifndef THRS_KV2
-#define THRS_KV2 1
-#endif
-constexpr uint64_t kKvBailOff = kBigTileOff + round_up_c((kBuckets + 1) * 4, 256);  // thrs_local_kv2 hand-over list
-constexpr uint64_t kHybridBytes = kKvBailOff + round_up_c(kBuckets * 4, 256);
+constexpr uint64_t kHybridBytes = kBigTileOff + round_up_c((kBuckets + 1) * 4, 256);
 // the smallest local-sort capacity (LocSmall): a big chunk holds more keys
 constexpr uint64_t kMinLocalCap = LocSmall::CAP;
 // tile ids of the segmented pass: each of the 8 segments adds at most one
@@ -374,13 +370,6 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     if constexpr (kKV) {
       if (allow_lds(atomicRank ? thrs_local_kv<KT, VB, true> : thrs_local_kv<KT, VB, false>, LocKV::LDS) != hipSuccess)
         return THRS_ERROR_HIP;
-      if constexpr (sizeof(U) == 8 && VB <= 8) {
-        if (allow_lds(atomicRank ? thrs_local_kv2<KT, VB, true> : thrs_local_kv2<KT, VB, false>, LocKV2::LDS) !=
-                hipSuccess ||
-            allow_lds(atomicRank ? thrs_local_kv<KT, VB, true, true> : thrs_local_kv<KT, VB, false, true>,
-                      LocKV::LDS) != hipSuccess)
-          return THRS_ERROR_HIP;
-      }
     } else if constexpr (kPairs4) {
       if (allow_lds(atomicRank ? thrs_local_pairs<KT, true, LocBig> : thrs_local_pairs<KT, false, LocBig>,
                     LocBig::lds<U>()) != hipSuccess ||
@@ -600,20 +589,9 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
       // every bucket a chunk, empty or not)
       const uint64_t maxChunks = !local32 ? kBuckets : std::min<uint64_t>(kBuckets, 256 + 2 * (uint64_t)n);
       const dim3 lgrid((uint32_t)maxChunks);
-      if constexpr (kKV && sizeof(U) == 8 && VB <= 8 && THRS_KV2) {
-        // two 76-KiB workgroups per CU; chunks with long tie runs are handed
-        // to the 152-KiB kernel (persistent over the list, ~5 us when empty)
-        uint32_t* kvBail = reinterpret_cast<uint32_t*>(hyb + kKvBailOff);
-        auto lk2 = atomicRank ? thrs_local_kv2<KT, VB, true> : thrs_local_kv2<KT, VB, false>;
-        hipLaunchKernelGGL(lk2, lgrid, dim3(LocKV2::THREADS), LocKV2::LDS, stream, K, V, km, chunkOff, chunkB0, meta,
-                           kvBail);
-        auto lkl = atomicRank ? thrs_local_kv<KT, VB, true, true> : thrs_local_kv<KT, VB, false, true>;
-        hipLaunchKernelGGL(lkl, dim3(cu_count()), dim3(LocKV::THREADS), LocKV::LDS, stream, K, V, km, chunkOff,
-                           chunkB0, meta, kvBail);
-      } else if constexpr (kKV) {
+      if constexpr (kKV) {
         auto lk = atomicRank ? thrs_local_kv<KT, VB, true> : thrs_local_kv<KT, VB, false>;
-        hipLaunchKernelGGL(lk, lgrid, dim3(LocKV::THREADS), LocKV::LDS, stream, K, V, km, chunkOff, chunkB0, meta,
-                           nullptr);
+        hipLaunchKernelGGL(lk, lgrid, dim3(LocKV::THREADS), LocKV::LDS, stream, K, V, km, chunkOff, chunkB0, meta);
       } else if constexpr (kPairs4) {
         auto launch_pairs = [&](auto geom) {
           using LG = decltype(geom);

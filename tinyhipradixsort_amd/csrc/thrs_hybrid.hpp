@@ -55,7 +55,6 @@ enum {
   kMetaBigPass = 8,  // [8]: per low pass p, bit 0 = runs (not the identity for every big chunk), bit 1 = parity
   kMetaBigTicket = 16,  // [8]: per low pass p, its tile ticket
   kMetaBigSingle = 24,  // [6]: per low pass p, big chunks whose digit p is one value
-  kMetaKvBail = 32,     // thrs_local_kv2: chunks handed to thrs_local_kv (a tie run too long / too many ties)
 };
 // gate masks of the gated launches: bit v set = run when the gate word is v
 constexpr uint32_t kGateMode0 = 1u << 0, kGateMode1 = 1u << 1, kGateMode2 = 1u << 2;  // on meta[kMetaMode]
@@ -1650,16 +1649,13 @@ __device__ __noinline__ void kv8_six_rounds(unsigned char* smem, uint32_t size) 
   }
 }
 
-// LIST: persistent over the chunks thrs_local_kv2 handed over (list[0 ..
-// meta[kMetaKvBail])), one workgroup per CU; else chunk c = blockIdx.x.
-template <int KT, int VB, bool ATOMIC_RANK, bool LIST = false>
+template <int KT, int VB, bool ATOMIC_RANK>
 __global__ __launch_bounds__(LocKV::THREADS) void thrs_local_kv(typename KeyTraits<KT>::U* __restrict__ keys,
                                                                 typename ValueWord<VB>::T* __restrict__ vals,
                                                                 KeyMap<typename KeyTraits<KT>::U> km,
                                                                 const uint32_t* __restrict__ chunkOff,
                                                                 const uint32_t* __restrict__ chunkB0,
-                                                                const uint32_t* __restrict__ meta,
-                                                                const uint32_t* __restrict__ list) {
+                                                                const uint32_t* __restrict__ meta) {
   using U = typename KeyTraits<KT>::U;
   constexpr int KB = (int)sizeof(U);
   using Item = typename std::conditional<KB == 4, uint32_t, uint64_t>::type;
@@ -1667,13 +1663,10 @@ __global__ __launch_bounds__(LocKV::THREADS) void thrs_local_kv(typename KeyTrai
   constexpr int KPT = LocKV::KPT;
   constexpr uint32_t CHUNK = 64 * KPT;
   constexpr bool PERMUTE_KEYS = KT == 2 || KT == 3;  // floats travel by position (their -0 is not rebuilt)
-  const uint32_t nList = LIST ? meta[kMetaKvBail] : 1u;
-#pragma unroll 1
-  for (uint32_t li = LIST ? blockIdx.x : 0u; li < nList; li += LIST ? gridDim.x : 1u) {
-  const uint32_t c = LIST ? list[li] : blockIdx.x;
-  if (!LIST && c >= meta[kMetaChunks]) return;
+  const uint32_t c = blockIdx.x;
+  if (c >= meta[kMetaChunks]) return;
   const uint32_t start = chunkOff[c], size = chunkOff[c + 1] - start;
-  if (size == 0 || size > LocKV::CAP) return;  // big chunk: the per-bucket fallback sorts it (never listed)
+  if (size == 0 || size > LocKV::CAP) return;  // big chunk: the per-bucket fallback sorts it
   const U hiImg = (U)chunkB0[c] << (8 * KB - 16);  // the bucket: the image's top 16 bits
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t tid = threadIdx.x, lane = tid & 63;
@@ -1864,293 +1857,6 @@ __global__ __launch_bounds__(LocKV::THREADS) void thrs_local_kv(typename KeyTrai
       if (j * 64 < lim) vdst[j * 64] = make_uint4((uint32_t)o[j], (uint32_t)(o[j] >> 32), (uint32_t)h, (uint32_t)(h >> 32));
     }
   }
-  if constexpr (LIST) lds_barrier();  // the stage is reused by the next listed chunk
-  }
-}
-
-
-// ------------------------- local sort, 8-byte keys, two workgroups per CU
-// thrs_local_kv runs one 152-KiB workgroup per CU, so a chunk's HBM phases
-// and its LDS rounds never overlap.  thrs_local_kv2 (8-byte keys with no,
-// 4- or 8-byte values) holds the same 17408-key chunk in 76 KiB, two
-// workgroups of 16 waves x 17 items per CU at <= 64 VGPRs:
-//   items     32-bit: the 16 image bits below the bucket << 16 | position;
-//             two LDS rounds with 16-bit per-wave counters, two digits per
-//             word (counts stay below 2^15)
-//   low bits  the image's low 32 bits: read again after the rounds (from
-//             the Infinity Cache mostly) into the stage by position, then
-//             gathered by sorted position
-//   ties      slots sharing their 16 bits with a neighbour (random keys: ~1
-//             in 4) are compacted in slot order into 64-bit entries (16 bits
-//             | low bits | position) in the stage; each run is then
-//             insertion-sorted there by its first entry's thread: stable
-//   hand-over a run longer than kTieScan, or more tie slots than the stage
-//             holds (8704), leaves the chunk untouched for thrs_local_kv
-//             (list meta[kMetaKvBail], a persistent launch after this one)
-//   out       keys rebuilt from bucket, 16 bits and low bits; values (and
-//             f64 keys) permuted through the stage one 4-byte word at a time
-struct LocKV2 {
-  static constexpr int WAVES = 16, KPT = 17, THREADS = 64 * WAVES;
-  static constexpr uint32_t CAP = (uint32_t)THREADS * KPT;  // 17408
-  static constexpr uint32_t CNT_WORDS = kBins / 2;          // per wave: two 16-bit counters per word
-  static constexpr size_t LDS = (size_t)CAP * 4 + (size_t)WAVES * CNT_WORDS * 4 + 32 * 4;
-};
-static_assert(LocKV2::CAP == LocKV::CAP, "one chunk capacity for the plan");
-
-template <bool ATOMIC_RANK>
-__device__ __forceinline__ void kv2_round(uint32_t (&it)[LocKV2::KPT], uint32_t* st, uint32_t* s_cnt, int shift,
-                                          int nItems) {
-  constexpr int KPT = LocKV2::KPT, W = LocKV2::WAVES, CW = LocKV2::CNT_WORDS;
-  const uint32_t tid = threadIdx.x, lane = tid & 63;
-  const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  uint32_t* cnt = s_cnt + w * CW;
-  uint32_t* s_wt = s_cnt + W * CW;
-  const bool wfull = nItems == KPT;
-  auto digit_of = [&](int j) -> uint32_t { return (it[j] >> shift) & 0xFFu; };
-  auto inc_of = [](uint32_t d) -> uint32_t { return 1u << ((d & 1u) << 4); };
-  cnt[lane] = 0;
-  cnt[64 + lane] = 0;
-  if (wfull) {
-#pragma unroll
-    for (int j = 0; j < KPT; ++j) {
-      const uint32_t d = digit_of(j);
-      __hip_atomic_fetch_add(&cnt[d >> 1], inc_of(d), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < KPT; ++j)
-      if (j < nItems) {
-        const uint32_t d = digit_of(j);
-        __hip_atomic_fetch_add(&cnt[d >> 1], inc_of(d), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-  }
-  lds_barrier();
-  // digit totals over the waves -> block exclusive scan -> per-wave running
-  // offsets (thread d < 256 owns digit d: half d & 1 of word d >> 1)
-  const uint32_t sh = (tid & 1u) << 4;
-  uint32_t tot = 0, inc = 0;
-  if (tid < kBins) {
-#pragma unroll
-    for (int ww = 0; ww < W; ++ww) tot += (s_cnt[ww * CW + (tid >> 1)] >> sh) & 0xFFFFu;
-    inc = wave_incl_scan(tot, lane);
-    if (lane == 63) s_wt[w] = inc;
-  }
-  lds_barrier();
-  if (tid < kBins) {
-    const uint32_t w0 = s_wt[0], w1 = s_wt[1], w2 = s_wt[2];
-    uint32_t run = inc - tot + (w > 0 ? w0 : 0u) + (w > 1 ? w1 : 0u) + (w > 2 ? w2 : 0u);
-    // the two digits of a word belong to lanes 2k, 2k+1: each writes its
-    // half of every wave's word in turn (the odd lane after the even one)
-#pragma unroll
-    for (int ww = 0; ww < W; ++ww) {
-      const uint32_t c = (s_cnt[ww * CW + (tid >> 1)] >> sh) & 0xFFFFu;
-      const uint32_t other = __shfl_xor(run, 1);
-      if ((tid & 1u) == 0) s_cnt[ww * CW + (tid >> 1)] = run | (other << 16);
-      run += c;
-    }
-  }
-  lds_barrier();
-  constexpr int RB = 9;
-  auto rank_scatter = [&](auto fullc) __attribute__((always_inline)) {
-    constexpr bool FULL = decltype(fullc)::value;
-#pragma unroll
-    for (int j0 = 0; j0 < KPT; j0 += RB) {
-      uint32_t sl[RB];
-#pragma unroll
-      for (int jj = 0; jj < RB; ++jj) {
-        const int j = j0 + jj;
-        if (j < KPT && (FULL || j < nItems)) {
-          const uint32_t d = digit_of(j);
-          if constexpr (ATOMIC_RANK) {
-            sl[jj] = (__hip_atomic_fetch_add(&cnt[d >> 1], inc_of(d), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >>
-                      ((d & 1u) << 4)) & 0xFFFFu;
-          } else {
-            uint32_t mlo, mhi;
-            match_digit(d, mlo, mhi);
-            const uint32_t c = (cnt[d >> 1] >> ((d & 1u) << 4)) & 0xFFFFu;
-            sl[jj] = __builtin_amdgcn_mbcnt_hi(mhi, __builtin_amdgcn_mbcnt_lo(mlo, c));
-            const uint32_t lead = mlo ? __builtin_ctz(mlo) : 32u + __builtin_ctz(mhi);
-            if (lane == lead)
-              __hip_atomic_fetch_add(&cnt[d >> 1], (uint32_t)(__builtin_popcount(mlo) + __builtin_popcount(mhi)) << ((d & 1u) << 4),
-                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          }
-        }
-      }
-#pragma unroll
-      for (int jj = 0; jj < RB; ++jj)
-        if (j0 + jj < KPT && (FULL || j0 + jj < nItems)) st[sl[jj]] = it[j0 + jj];
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-  if (wfull) rank_scatter(std::true_type{});
-  else rank_scatter(std::false_type{});
-  lds_barrier();
-}
-
-template <int KT, int VB, bool ATOMIC_RANK>
-__global__ __launch_bounds__(LocKV2::THREADS) __attribute__((amdgpu_waves_per_eu(8))) void thrs_local_kv2(
-    typename KeyTraits<KT>::U* __restrict__ keys, typename ValueWord<VB>::T* __restrict__ vals,
-    KeyMap<typename KeyTraits<KT>::U> km, const uint32_t* __restrict__ chunkOff, const uint32_t* __restrict__ chunkB0,
-    uint32_t* __restrict__ meta, uint32_t* __restrict__ bail) {
-  using U = typename KeyTraits<KT>::U;
-  static_assert(sizeof(U) == 8 && VB <= 8, "8-byte keys with 0-, 4- or 8-byte values");
-  constexpr int KPT = LocKV2::KPT;
-  constexpr uint32_t CHUNK = 64 * KPT;
-  constexpr bool PERMUTE_KEYS = KT == 3;  // f64 keys travel by position (their -0 is not rebuilt)
-  const uint32_t c = blockIdx.x;
-  if (c >= meta[kMetaChunks]) return;
-  const uint32_t start = chunkOff[c], size = chunkOff[c + 1] - start;
-  if (size == 0 || size > LocKV2::CAP) return;  // big chunk: the per-bucket fallback sorts it
-  const U hiImg = (U)chunkB0[c] << 48;          // the bucket: the image's top 16 bits
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  uint32_t* st = reinterpret_cast<uint32_t*>(smem);
-  uint32_t* s_cnt = st + LocKV2::CAP;
-  uint32_t* s_misc = s_cnt + LocKV2::WAVES * LocKV2::CNT_WORDS + 16;  // [16]: hand over
-  const uint32_t tid = threadIdx.x, lane = tid & 63;
-  const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const uint32_t myOff = w * CHUNK + lane;
-  int32_t lim = (int32_t)size - (int32_t)myOff;
-  pin(reinterpret_cast<uint32_t&>(lim));
-  const int32_t limw = __builtin_amdgcn_readfirstlane((int32_t)size - (int32_t)(w * CHUNK));
-  const int nItems = limw <= 0 ? 0 : min(KPT, (limw + 63) >> 6);  // items j with j*64 < limw
-  const bool wfull = nItems == KPT;
-  if (tid == 0) s_misc[16] = 0;  // (the rounds' barriers order this before any set)
-
-  uint32_t it[KPT];
-  {
-    U raw[KPT];
-    load_run<KPT>(raw, keys + start, myOff, size, limw);
-#pragma unroll
-    for (int j = 0; j < KPT; ++j) {
-      const uint32_t p = myOff + j * 64;
-      it[j] = (j * 64 < lim) ? ((uint32_t)(kimg<KT>(km, raw[j]) >> 32) << 16) | p : 0xFFFF0000u | p;
-    }
-  }
-  kv2_round<ATOMIC_RANK>(it, st, s_cnt, 16, nItems);
-  if (wfull) {
-#pragma unroll
-    for (int j = 0; j < KPT; ++j) it[j] = st[myOff + j * 64];
-  } else {
-#pragma unroll
-    for (int j = 0; j < KPT; ++j)
-      if (j < nItems) it[j] = st[myOff + j * 64];
-  }
-  kv2_round<ATOMIC_RANK>(it, st, s_cnt, 24, nItems);
-  // sorted items of this lane's slots (past the chunk: padding, position >= size)
-#pragma unroll
-  for (int j = 0; j < KPT; ++j) it[j] = st[myOff + j * 64];
-  lds_barrier();
-  {  // the image's low 32 bits, by input position (the keys read again)
-    const U* src = keys + start + myOff;
-    if (limw >= (int32_t)CHUNK) {
-#pragma unroll
-      for (int j = 0; j < KPT; ++j) st[myOff + j * 64] = (uint32_t)kimg<KT>(km, src[j * 64]);
-    } else {
-#pragma unroll
-      for (int j = 0; j < KPT; ++j)
-        if (j * 64 < lim) st[myOff + j * 64] = (uint32_t)kimg<KT>(km, src[j * 64]);
-    }
-  }
-  lds_barrier();
-  uint32_t lo[KPT];
-#pragma unroll
-  for (int j = 0; j < KPT; ++j) lo[j] = st[it[j] & 0xFFFFu];  // ... gathered by sorted position
-#pragma unroll
-  for (int j = 0; j < KPT; ++j) {
-    pin(it[j]);
-    pin(lo[j]);
-  }
-  lds_barrier();
-  U* kdst = keys + start + myOff;
-  if constexpr (!PERMUTE_KEYS) {
-#pragma unroll
-    for (int j = 0; j < KPT; ++j)
-      if (j * 64 < lim) kdst[j * 64] = kinv_int(km, (U)(hiImg | ((U)(it[j] >> 16) << 32) | (U)lo[j]));
-  }
-  // out[slot] = in[position] through the stage, one 4-byte word at a time
-  // (words q of elements of `words` words)
-  auto permute_word = [&](const uint32_t* src32, uint32_t* dst32, int words, int q) __attribute__((always_inline)) {
-    uint32_t x[KPT];
-    const uint32_t* sp = src32 + (uint64_t)(start + myOff) * words + q;
-    if (limw >= (int32_t)CHUNK) {
-#pragma unroll
-      for (int j = 0; j < KPT; ++j) x[j] = sp[j * 64 * words];
-    } else {
-#pragma unroll
-      for (int j = 0; j < KPT; ++j) x[j] = (j * 64 < lim) ? sp[j * 64 * words] : 0u;
-    }
-    lds_barrier();  // every earlier stage read is done
-#pragma unroll
-    for (int j = 0; j < KPT; ++j)
-      if (j * 64 < lim) st[myOff + j * 64] = x[j];
-    lds_barrier();
-#pragma unroll
-    for (int j = 0; j < KPT; ++j) x[j] = st[it[j] & 0xFFFFu];
-    uint32_t* dp = dst32 + (uint64_t)(start + myOff) * words + q;
-#pragma unroll
-    for (int j = 0; j < KPT; ++j)
-      if (j * 64 < lim) dp[j * 64 * words] = x[j];
-  };
-  if constexpr (PERMUTE_KEYS) {
-    // (each word pass reads only its own words of the chunk's keys, so
-    // writing word q in place leaves word q + 1 to read)
-    uint32_t* k32 = reinterpret_cast<uint32_t*>(keys);
-    permute_word(k32, k32, 2, 0);
-    permute_word(k32, k32, 2, 1);
-  }
-  if constexpr (VB > 0) {
-#pragma unroll
-    for (int q = 0; q < VB / 4; ++q)
-      permute_word(reinterpret_cast<const uint32_t*>(vals), reinterpret_cast<uint32_t*>(vals), VB / 4, q);
-  }
-  // Ties: the chunk is now written sorted by the 16 bits and, within equal
-  // bits, by position.  Each run of slots sharing the 16 bits (random keys:
-  // ~1 slot in 4, mostly pairs) is insertion-sorted in place in memory (L2:
-  // the workgroup just wrote it) by its first slot's thread on the whole
-  // image -- stable, equal keys keep their order.  A run longer than
-  // kTieScan hands the chunk (a stable permutation of its input, so sorting
-  // it again gives the same bytes) to thrs_local_kv.
-  lds_barrier();  // every stage read of the permutes is done
-#pragma unroll
-  for (int j = 0; j < KPT; ++j) st[myOff + j * 64] = it[j] >> 16;  // the 16 bits, by slot
-  __syncthreads();  // (also: this workgroup's key and value stores are visible in L2)
-  U* kc = keys + start;
-  typename ValueWord<VB>::T* vc = vals + start;
-  auto ld = [](const auto* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-  bool over = false;
-#ifndef THRS_KV2_TIEFIX
-#define THRS_KV2_TIEFIX 1
-#endif
-  for (uint32_t h = tid; THRS_KV2_TIEFIX && h + 1 < size; h += LocKV2::THREADS) {
-    const uint32_t pre = st[h];
-    if ((h > 0 && st[h - 1] == pre) || st[h + 1] != pre) continue;  // not a run's first slot
-    uint32_t e = h + 2;
-    while (e < size && e - h <= (uint32_t)kTieScan && st[e] == pre) ++e;
-    if (e - h > (uint32_t)kTieScan) {
-      over = true;
-      continue;
-    }
-    for (uint32_t i = h + 1; i < e; ++i) {
-      const U kx = ld(&kc[i]);
-      const U ix = kimg<KT>(km, kx);
-      typename ValueWord<VB>::T vx{};
-      if constexpr (VB > 0) vx = ld(&vc[i]);
-      uint32_t k = i;
-      for (; k > h; --k) {
-        const U ky = ld(&kc[k - 1]);
-        if (!(kimg<KT>(km, ky) > ix)) break;
-        kc[k] = ky;
-        if constexpr (VB > 0) vc[k] = ld(&vc[k - 1]);
-      }
-      if (k != i) {
-        kc[k] = kx;
-        if constexpr (VB > 0) vc[k] = vx;
-      }
-    }
-  }
-  if (over) s_misc[16] = 1;  // (every writer stores 1)
-  lds_barrier();
-  if (s_misc[16] != 0 && tid == 0) bail[atomicAdd(&meta[kMetaKvBail], 1u)] = c;
 }
 
 }  // namespace
