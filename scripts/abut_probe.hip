@@ -18,6 +18,7 @@
 #include <cstdlib>
 #include <cstdint>
 #include <vector>
+#include <type_traits>
 
 #define CK(x)                                                                 \
   do {                                                                        \
@@ -28,15 +29,27 @@
     }                                                                         \
   } while (0)
 
-constexpr int THREADS = 512, KPT = 32;
+// geometry / element size (-D): PROBE_THREADS x PROBE_KPT keys per tile,
+// PROBE_ELEM-byte elements (2: the u16 planes of the bucket path's passes)
+#ifndef PROBE_THREADS
+#define PROBE_THREADS 512
+#endif
+#ifndef PROBE_KPT
+#define PROBE_KPT 32
+#endif
+#ifndef PROBE_ELEM
+#define PROBE_ELEM 4
+#endif
+constexpr int THREADS = PROBE_THREADS, KPT = PROBE_KPT;
 constexpr uint32_t T = THREADS * KPT;
+using E = std::conditional<PROBE_ELEM == 2, uint16_t, uint32_t>::type;
 
 template <int MAP>
-__global__ __launch_bounds__(THREADS) void abut(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+__global__ __launch_bounds__(THREADS) void abut(const E* __restrict__ in, E* __restrict__ out,
                                                 const uint32_t* __restrict__ off, const uint16_t* __restrict__ lstart,
                                                 uint32_t nT) {
   __shared__ uint32_t s_off[256];
-  __shared__ uint32_t s_ls[257];
+  __shared__ uint32_t s_ls[257];  // (T itself may not fit 16 bits)
   const uint32_t b = blockIdx.x;
   // MAP 0: round-robin; 1: one contiguous range per XCD; B>1: blocks of B
   // consecutive tiles per XCD, blocks round-robin over XCDs (thrs_pass_xb)
@@ -50,7 +63,7 @@ __global__ __launch_bounds__(THREADS) void abut(const uint32_t* __restrict__ in,
     s_ls[tid] = lstart[(uint64_t)tile * 256 + tid];
   }
   if (tid == 0) s_ls[256] = T;
-  uint32_t k[KPT];
+  E k[KPT];
 #pragma unroll
   for (int j = 0; j < KPT; ++j) k[j] = in[(uint64_t)tile * T + w * 64 * KPT + j * 64 + lane];
   __syncthreads();
@@ -64,12 +77,12 @@ __global__ __launch_bounds__(THREADS) void abut(const uint32_t* __restrict__ in,
       const uint32_t mid = (lo + hi) >> 1;
       if (s_ls[mid] <= i) lo = mid; else hi = mid;
     }
-    out[s_off[lo] + (i - s_ls[lo])] = k[j] + 1;
+    out[s_off[lo] + (i - s_ls[lo])] = (E)(k[j] + 1);
   }
 }
 
 template <int MAP>
-double run(const uint32_t* in, uint32_t* out, const uint32_t* off, const uint16_t* ls, uint32_t nT, int reps) {
+double run(const E* in, E* out, const uint32_t* off, const uint16_t* ls, uint32_t nT, int reps) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
@@ -114,16 +127,18 @@ int main() {
       l += cnt[(size_t)t * 256 + d];
     }
   }
-  uint32_t *in, *out, *doff;
+  E *in, *out;
+  uint32_t* doff;
   uint16_t* dls;
-  CK(hipMalloc(&in, (size_t)n * 4));
-  CK(hipMalloc(&out, (size_t)n * 4));
+  CK(hipMalloc(&in, (size_t)n * sizeof(E)));
+  CK(hipMalloc(&out, (size_t)n * sizeof(E)));
   CK(hipMalloc(&doff, off.size() * 4));
   CK(hipMalloc(&dls, ls.size() * 2));
-  CK(hipMemset(in, 1, (size_t)n * 4));
+  CK(hipMemset(in, 1, (size_t)n * sizeof(E)));
   CK(hipMemcpy(doff, off.data(), off.size() * 4, hipMemcpyHostToDevice));
   CK(hipMemcpy(dls, ls.data(), ls.size() * 2, hipMemcpyHostToDevice));
-  const double bytes = 2.0 * n * 4;
+  const double bytes = 2.0 * n * sizeof(E);
+  printf("{\"tile\": %u, \"elem\": %d}\n", T, (int)sizeof(E));
   for (int rep = 0; rep < 2; ++rep) {
     const double r[5] = {run<0>(in, out, doff, dls, nT, 10), run<1>(in, out, doff, dls, nT, 10),
                          run<4>(in, out, doff, dls, nT, 10), run<8>(in, out, doff, dls, nT, 10),
