@@ -347,6 +347,13 @@ def load_pmc_traffic(workload: str):
 
 def main():
     args = parse()
+    # stdout carries exactly one JSON line (rank 0).  Native libraries print
+    # to file descriptor 1 (RCCL's version banner at communicator set-up, on
+    # every rank), so fd 1 points at stderr from here on and the JSON line is
+    # written to the saved descriptor.
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -590,7 +597,7 @@ def main():
                "roofline": roof, "cpu_baseline": cpu, "vendor": vendor, "reference_gpu": ref_gpu}
         if phase:
             out["phases_ms"] = phase
-        print(json.dumps(out), flush=True)
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

@@ -167,7 +167,11 @@ def test_bench_force_dist_runs_rccl_at_world_1(gpu):
                         "--steps", "2", "--warmup", "1", "--cpu-baseline", "off"],
                        capture_output=True, text=True, timeout=240, env=env)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
-    line = json.loads(r.stdout.strip().splitlines()[-1])
+    # stdout is the ONE JSON line the driver reads: RCCL's version banner
+    # (printed to fd 1 at communicator set-up) must not reach it
+    lines = r.stdout.strip().splitlines()
+    assert len(lines) == 1, r.stdout[-2000:]
+    line = json.loads(lines[0])
     assert line["n_gpus"] == 1 and line["value"] > 0 and "bucket-exchange" in line["config"]["parallelism"]
 
 
