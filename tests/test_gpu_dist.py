@@ -206,15 +206,19 @@ def _worker_big(rank, world, port, out_dir, kt, vb, n):
         ko, vo, n_out = sorter.sort(kd, n, vd, 0, 8 * kb)
         torch.cuda.synchronize()
         local = [x for x in T.profile_launches(2) if x >= 0.02]
-        fallback = [x for x in T.profile_launches(3) if x >= 0.02]
         T.profile_enable(False)
+        # what the finish's bucket path found (the finish is the last sort on
+        # the sorter's temp buffer): big chunks would have taken the fallback.
+        # (Not the fallback launches' times: two ranks share this one GPU, so
+        # a gated no-op launch can time above any threshold.)
+        mode, big = sorter.ops.rs.debugBucketMode(sorter.ops._tmp, n_out, bool(vb))
         bad = TU.count_unsorted(kt, ko, n_out, 0, 8 * kb)
         first = last = None
         if n_out:
             kk = ko.view(torch.int32 if kb == 4 else torch.int64)
             first, last = int(kk[0].item()) & ((1 << (8 * kb)) - 1), int(kk[n_out - 1].item()) & ((1 << (8 * kb)) - 1)
         res = {"n_out": n_out, "unsorted": bad, "first": first, "last": last, "local_launches": len(local),
-               "fallback_launches": len(fallback), "range": sorter.last_range}
+               "mode": mode, "big_chunks": big, "range": sorter.last_range}
         if vb:   # the payload is the global index: every one arrives once (one rank: all of them)
             vkt = 1 if vb == 8 else 0
             res["fp_in"], res["fp_out"] = TU.fingerprint(vkt, vd, n), TU.fingerprint(vkt, vo, n_out)
@@ -241,7 +245,7 @@ def test_bucket_finish_with_key_range(gpu, tmp_path, world, kt, vb, n):
     assert sum(r["n_out"] for r in res) == world * n
     for r in res:
         assert r["unsorted"] == 0, r
-        assert r["local_launches"] >= 1 and r["fallback_launches"] == 0, r
+        assert r["local_launches"] >= 1 and r["mode"] == 0 and r["big_chunks"] == 0, r
     for a, b in zip(res, res[1:]):
         assert a["last"] <= b["first"], (a, b)
     if world > 1:
