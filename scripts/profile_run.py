@@ -31,7 +31,8 @@ for w16 in (1, 0):
         TU.copy(dst, src, G, bool(w16))
 torch.cuda.synchronize()
 del src, dst
-cfg = T.RadixSort.Config(keyType=T.KeyType(kt), valueType={0: T.ValueType.U32, 4: T.ValueType.U32, 8: T.ValueType.U64}[vb])
+cfg = T.RadixSort.Config(keyType=T.KeyType(kt), valueType={0: T.ValueType.U32, 4: T.ValueType.U32, 8: T.ValueType.U64,
+                                                                   16: T.ValueType.U128}[vb])
 rs = T.RadixSort([], cfg)
 d = rs.getTemporaryBufferBytes(n)
 tmp = torch.empty(d.getTemporaryBufferBytesForSortPairs() if vb else d.getTemporaryBufferBytesForSortKeys(),
