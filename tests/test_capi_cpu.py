@@ -78,8 +78,9 @@ def test_temporary_buffer_layout(kt, vt, n):
     # (the reference's pSum region is 4*256*ceil(n/2048) = n/2 bytes, hpp:839),
     # plus a fixed ~1.1 MiB: the 3-pass path's bucket histogram and chunk table
     # and the segmented pass's extra look-back rows; u32 keys: + the bucket
-    # path's u8 plane (n bytes: its two u16 planes fill keyOut)
-    plane = -(-n // 256) * 256 if kt == T.KeyType.U32 else 0
+    # path's u8 plane (n bytes: its two u16 planes fill keyOut), reserved only
+    # where the default takes that path (n in [2^28, 2^31 + 2^25])
+    plane = -(-n // 256) * 256 if kt == T.KeyType.U32 and (1 << 28) <= n <= (1 << 31) + (1 << 25) else 0
     if n >= (1 << 20):
         assert d.pSumBuffer < 0.3 * d.keyOutBuffer + plane + (3 << 20) // 2
 
