@@ -97,8 +97,11 @@ typedef struct thrs_options {
                             finish, tinyhipradixsort_amd/dist.py).  rangeLo == rangeHi:
                             every key is equal, the sort returns at once.  Ignored
                             where it does not apply (windows; 4-byte keys-only sorts
-                            on the 32-bit local sort).  A false promise gives
-                            unspecified output.  0 = no range.                     */
+                            on the 32-bit local sort), but always validated:
+                            rangeLo > rangeHi, or rangeHi above the key width's
+                            largest image, is THRS_ERROR_INVALID_VALUE on every
+                            sort.  A false promise gives unspecified output.
+                            0 = no range.                                          */
   int32_t reserved;      /* zero */
   uint64_t rangeLo;
   uint64_t rangeHi;

@@ -153,6 +153,39 @@ def test_bucket_exchange_gloo(world):
     mp.spawn(_worker, args=(world, free_port(), cases), nprocs=world, join=True)
 
 
+def _subgroup_worker(rank, world, port):
+    """Two concurrent sorts on subgroups whose group ranks differ from the
+    global ranks ({0, 2} and {1, 3} of a world of 4): every segment must reach
+    the right process (P2POp group_peer)."""
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        groups = [dist.new_group([0, 2]), dist.new_group([1, 3])]
+        mine = groups[rank % 2]
+        members = [0, 2] if rank % 2 == 0 else [1, 3]
+        sizes = [3001, 2500]
+        glob = np.concatenate([gen("random", O.U32, sizes[i], 91 * members[0] + 7 * i) for i in range(2)])
+        gidx = np.arange(glob.shape[0], dtype=np.uint32)
+        me = members.index(rank)
+        lo = sum(sizes[:me])
+        keys = torch.from_numpy(np.ascontiguousarray(glob[lo:lo + sizes[me]]).view(np.uint8).copy())
+        vals = torch.from_numpy(gidx[lo:lo + sizes[me]].view(np.uint8).copy())
+        sorter = D.DistributedRadixSort(O.U32, 0, 0, group=mine, ops=OracleOps(O.U32, 4, False))
+        assert sorter.rank == me and sorter.world == 2
+        ko, vo, n_out = sorter.sort(keys, sizes[me], vals, 0, 32)
+        ek, ev = O.lsd_sort(O.U32, glob, gidx.view(np.uint8).reshape(-1, 4).copy(), 0, 32, False)
+        total = glob.shape[0]
+        off = me * total // 2
+        assert n_out == (me + 1) * total // 2 - off
+        assert np.array_equal(ko.numpy().view(np.uint32)[:n_out], ek[off:off + n_out])
+        assert np.array_equal(vo.numpy().reshape(n_out, 4), ev[off:off + n_out])
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bucket_exchange_on_subgroups():
+    mp.spawn(_subgroup_worker, args=(4, free_port()), nprocs=4, join=True)
+
+
 def _simulate(ranks, kt, s, e, desc=False):
     """The host split logic on in-memory ranks (numpy histograms): returns
     each rank's received keys after the finish, to compare with one stable sort."""

@@ -642,3 +642,39 @@ def test_key_range_keeps_buckets_local(gpu, kt, vb, desc):
     rs = make_sorter(kt, vb, desc, keyRange=(int(img[0]), int(img[0])))
     k, _ = gpu_sort(torch, rs, {"keys": one, "values": None if not vb else vals[:1000]}, kt, vb, 0, 8 * kb)
     assert np.array_equal(k, one)
+
+
+@pytest.mark.parametrize("kt,vb", [(O.F32, 0), (O.F64, 0), (O.F64, 8)])
+@pytest.mark.parametrize("desc", [False, True])
+@pytest.mark.parametrize("where", ["straddles_zero", "excludes_zero"])
+def test_key_range_float_zeros(gpu, kt, vb, desc, where):
+    """keyRange on the float local sorts: f32 keys-only is
+    thrs_local16's +-0 chunk (+0 and -0 share one image and must keep their
+    input order and bits), f64 the permuted-key thrs_local_kv.  A range that
+    straddles zero with mixed +0 / -0 keys, and one that excludes zero (the
+    image of 0 then lies outside [lo, hi]); bit-exact with the oracle."""
+    torch = gpu
+    kb = O.KEY_BYTES[kt]
+    kdt = O.KEY_DTYPE[kt]
+    fdt = np.float32 if kb == 4 else np.float64
+    n = (1 << 20) + 4097
+    rng = np.random.default_rng(1000 * kb + vb + (7 if desc else 0) + len(where))
+    if where == "straddles_zero":
+        f = rng.uniform(-1e-3, 1e-3, n).astype(fdt)
+        z = rng.random(n)
+        f[z < 0.1] = fdt(0.0)
+        f[(z >= 0.1) & (z < 0.2)] = -fdt(0.0)
+    else:
+        f = rng.uniform(1.0, 2.0, n).astype(fdt)
+    keys = f.view(kdt).copy()
+    img = O.key_bits_np(kt, keys, desc)
+    lo, hi = int(img.min()), int(img.max())
+    vals = None
+    if vb:
+        vals = (np.arange(n * vb // 4, dtype=np.uint32) * np.uint32(2654435761)).view(np.uint64)
+    ek, ev = O.lsd_sort(kt, keys, vals, 0, 8 * kb, desc)
+    rs = make_sorter(kt, vb, desc, path="bucket", keyRange=(lo, hi))
+    (mode, big), k, v = _mode_after(torch, rs, keys, vals, kt, vb)
+    assert np.array_equal(k.view(kdt), ek.view(kdt)), (where, mode, big)
+    if vb:
+        assert np.array_equal(v, ev), where

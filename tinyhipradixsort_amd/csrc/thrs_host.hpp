@@ -547,7 +547,9 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
       hipLaunchKernelGGL(kern, dim3((uint32_t)segPerCU * cu_count()), dim3(G::THREADS), lds, stream, kin, kout, vin,
                          vout, codec == kCodecPlanes ? kid : km, codec == kCodecPlanes ? 16 : startBits + 8 * p,
                          reinterpret_cast<uint32_t*>(hyb + infoOff), reinterpret_cast<const uint32_t*>(hyb + baseOff),
-                         status[p & 1], err, grp[p & 1], gate, gateMask, hiP);
+                         status[p & 1], err, grp[p & 1], gate, gateMask, hiP,
+                         g_stamps ? g_stamps + (uint64_t)(p - nLow) * (plan.nTiles + kSegTilePad) * kStampSlots
+                                  : nullptr);
     };
     const uint64_t sw = plan.wideStatus ? 8 : 4;
     const int setB = (nLow + 1) & 1;

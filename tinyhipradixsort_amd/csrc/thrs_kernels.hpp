@@ -1365,7 +1365,8 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
     const typename ValueWord<VB>::T* __restrict__ valsIn, typename ValueWord<VB>::T* __restrict__ valsOut,
     KeyMap<typename KeyTraits<KT>::U> km, int shift, uint32_t* __restrict__ segInfo,
     const uint32_t* __restrict__ segBase, ST* __restrict__ status, uint32_t* __restrict__ errFlag,
-    GroupTables<ST> grp, const uint32_t* __restrict__ gate, uint32_t gateMask, uint8_t* __restrict__ hiPlane) {
+    GroupTables<ST> grp, const uint32_t* __restrict__ gate, uint32_t gateMask, uint8_t* __restrict__ hiPlane,
+    uint64_t* __restrict__ stamps) {
   using U = typename KeyTraits<KT>::U;
   using VW = typename ValueWord<VB>::T;
   using G = PassGeom<sizeof(U), VB>;
@@ -1400,6 +1401,15 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
       }
       s_misc[8] = seg;
       s_misc[9] = t;
+#ifdef THRS_STAMPS
+      if (stamps && seg < (uint32_t)kSegs) {  // slot 7: xcc | segment << 4 (| walk maxima, pass_tile)
+        uint64_t* s_stamp = reinterpret_cast<uint64_t*>(s_misc + 16);
+        for (int i = 0; i < kStampSlots; ++i) s_stamp[i] = 0;
+        s_stamp[0] = __builtin_amdgcn_s_memrealtime();
+        s_stamp[7] = xcc_id() | (seg << 4);
+        s_misc[1] = s_misc[2] = s_misc[3] = 0;
+      }
+#endif
     }
     for (uint32_t i = tid; i < (uint32_t)(G::WAVES * kBins); i += G::THREADS) s_cnt[i] = 0;
     lds_barrier();
@@ -1418,7 +1428,7 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
     load_tile<KT, VB, CODEC>(keysIn, valsIn, keyStart, valid, k, v, hiPlane);
     pass_tile<KT, VB, ST, ATOMIC_RANK, NoMid, CODEC>(keysIn, keysOut, valsIn, valsOut, keyStart, valid, km,
                                                      shift, myBase, segPos[kSegs], status, nullptr, errFlag, chain + t, chain, g, smem,
-                                                     nullptr, k, v, NoMid{}, hiPlane);
+                                                     stamps, k, v, NoMid{}, hiPlane);
     lds_barrier();  // stage, s_gofs and s_misc are reused by the next tile
   }
 }

@@ -204,6 +204,13 @@ class HipLocalOps:
         """stream-ordered: acc |= the error word of the step that just ran on tmp"""
         self.rs.accumulateDeviceError(tmp, self._acc)
 
+    def reset_errors(self):
+        """Stream-ordered: forget what an earlier, failed sort accumulated
+        (a step that raised before check_errors ran), so a later healthy sort
+        never reports it."""
+        if self._acc is not None:
+            self._acc.zero_()
+
     def check_errors(self):
         """Synchronising: raise if any step since the last check hit a device
         look-back / claim timeout (its output would be wrong)."""
@@ -303,10 +310,12 @@ class DistributedRadixSort:
                     if d > c:
                         dst[c:d].copy_(src[a:b])
                     continue
+                # peer is a rank of self.group: pass it as group_peer (P2POp's
+                # `peer` is a GLOBAL rank, which differs inside a subgroup)
                 if b > a:
-                    ops.append(self.dist.P2POp(self.dist.isend, src[a:b], peer, self.group))
+                    ops.append(self.dist.P2POp(self.dist.isend, src[a:b], group=self.group, group_peer=peer))
                 if d > c:
-                    ops.append(self.dist.P2POp(self.dist.irecv, dst[c:d], peer, self.group))
+                    ops.append(self.dist.P2POp(self.dist.irecv, dst[c:d], group=self.group, group_peer=peer))
         if ops:
             for r in self.dist.batch_isend_irecv(ops):
                 r.wait()
@@ -349,6 +358,8 @@ class DistributedRadixSort:
         dev = kflat.device
         clock = _Clock(timings, dev)
 
+        if hasattr(self.ops, "reset_errors"):
+            self.ops.reset_errors()
         k_in, v_in = kflat[:n * kb], (vflat[:n * vb] if vflat is not None else None)
         pk, pv, counts = self.ops.partition(k_in, v_in, n, locs[-1])
         clock.mark("partition")
