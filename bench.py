@@ -24,10 +24,10 @@ metric: "Gkeys/s and achieved HBM GB/s (% of peak), u32 keys N=2^30, 1/2/4/8 GPU
 
 Timing: W warm-up steps, then barrier + synchronize, K steps, synchronize +
 barrier; the max over ranks.  rank 0 prints ONE JSON line.  `roofline` prices
-the DOMINANT kernel kind -- device passes, local sort or the per-bucket
-fallback's passes, whichever took the most time -- from per-launch HIP events
-on the sort's own stream inside the timed region (gated launches that found
-nothing to do, < 20 us, are not launches of the kernel's work); `cpu_baseline`
+the DOMINANT kernel -- the kernel with the most time per sort -- at its own
+algorithmic bytes per launch, from per-launch HIP events on the sort's own
+stream inside the timed region (gated launches that found nothing to do,
+< 20 us, are not launches of the kernel's work); `cpu_baseline`
 times the reference's CPU path (std::sort, unittest.cpp:156) on bounded
 samples on this host, with the C1 size (2^20 keys) as its own legs.
 """
@@ -58,6 +58,11 @@ WORKLOADS = {
     "k64v128": (1, 16, 1 << 29, "uniform", "sortPairs u64 key + 16-B payload (K64V128), N=2^29"),
     "k32v64": (0, 8, 1 << 30, "uniform", "sortPairs u32 key + u64 payload, N=2^30"),
     "kf32v32": (2, 4, 1 << 30, "uniform", "sortPairs f32 key + u32 payload, N=2^30"),
+    # the reference's own bench size: OrochiRadixSort.bench / benchKeyPair sort 160,000,000 u32 keys
+    # (unittest.cpp:490-494, 574-578)
+    "ref160m": (0, 0, 160_000_000, "uniform", "OrochiRadixSort.bench: sortKeys u32, N=160,000,000 (unittest.cpp:490-571)"),
+    "ref160m_pairs": (0, 4, 160_000_000, "uniform",
+                      "OrochiRadixSort.benchKeyPair: sortPairs u32 key + u32 payload, N=160,000,000 (unittest.cpp:574-)"),
     "u32large": (0, 0, (1 << 31) + 100, "uniform", "u32Large: sortKeys u32, N=2^31+100 uniform (unittest.cpp:688-717)"),
     # low-entropy inputs of C2's shape (not bench lines of BASELINE.json: robustness)
     "c2_sorted": (0, 0, 1 << 30, "sorted", "C2 shape, already-sorted input (stratified sorted uniform sample)"),
@@ -266,15 +271,21 @@ GATED_NOOP_MS = 0.02   # a gated launch with nothing to do takes ~4-6 us; real l
 KIND_NAMES = {0: "hist", 1: "pass", 2: "local", 3: "fallback"}
 
 
-def build_roofline(prof, steps, n, kb, vb, pinfo, elapsed, global_keys, world, wl):
-    """`roofline` of the bench line from per-launch HIP-event times (kinds:
-    0 histogram + plan, 1 device-wide digit passes, 2 local sort, 3 the
-    per-bucket fallback's launches)."""
+def build_roofline(prof, kern, steps, n, kb, vb, pinfo, elapsed, global_keys, world, wl, big_keys=0):
+    """`roofline` of the bench line from per-launch HIP-event times.  Every
+    launch carries its kernel (thrs_profile_read_launch_kernels) and
+    algorithmic bytes: 2 * keys * (K + V) for a launch that permutes keys
+    (SURVEY.md s8(d)), keys * K for one that only counts them; the per-bucket
+    fallback's launches move the big chunks' keys only (big_keys, read from
+    the last sort's plan).  The DOMINANT kernel is the one with the most time
+    per sort; its `achieved` = its bytes per launch / its average launch time.
+    Gated launches that found nothing to do (< GATED_NOOP_MS) are not launches
+    of the kernel's work.  `kinds` keeps the per-kind summary (hist / pass /
+    local / fallback)."""
     if not prof:
         return None
     step_s = elapsed / steps
-    alg = 2 * n * (kb + vb)                      # per pass-like launch
-    kinds = {}
+    kinds, kernels = {}, {}
     for k, ms in prof.items():
         eff = [x for x in ms if x >= GATED_NOOP_MS]
         kinds[KIND_NAMES[k]] = {"ms_per_sort": round(sum(eff) / steps, 4), "launches_per_sort": round(len(eff) / steps, 2),
@@ -283,23 +294,35 @@ def build_roofline(prof, steps, n, kb, vb, pinfo, elapsed, global_keys, world, w
         per = len(eff) // steps if eff and len(eff) % steps == 0 else 0
         if per > 1:   # the same launches every sort: each one's average, in launch order
             kinds[KIND_NAMES[k]]["by_launch_ms"] = [round(sum(eff[i::per]) / steps, 4) for i in range(per)]
-    cand = {k: v for k, v in kinds.items() if k in ("pass", "local", "fallback") and v["avg_launch_ms"]}
+        for x, (name, byts) in zip(ms, kern.get(k, [])):
+            if x < GATED_NOOP_MS:
+                continue
+            if byts == 0:   # data-dependent: the per-bucket fallback's work on the big chunks
+                byts = {"thrs_big_hist": big_keys * kb, "thrs_pass_big": 2 * big_keys * (kb + vb),
+                        "thrs_big_copy": 2 * big_keys * (kb + vb)}.get(name, 0)
+            e = kernels.setdefault(name, {"ms": 0.0, "launches": 0, "bytes": 0})
+            e["ms"] += x
+            e["launches"] += 1
+            e["bytes"] += byts
+    for name, e in kernels.items():
+        e["ms_per_sort"] = round(e.pop("ms") / steps, 4)
+        e["avg_launch_ms"] = round(e["ms_per_sort"] * steps / e["launches"], 4)
+        e["alg_bytes_per_launch"] = e.pop("bytes") // e["launches"]
+        e["launches_per_sort"] = round(e.pop("launches") / steps, 2)
+        e["GBps"] = round(e["alg_bytes_per_launch"] / (e["avg_launch_ms"] / 1e3) / 1e9, 1)
+    cand = {k: v for k, v in kernels.items() if v["alg_bytes_per_launch"] > 0}
     if not cand:
         return None
     dom = max(cand, key=lambda k: cand[k]["ms_per_sort"])
     avg = cand[dom]["avg_launch_ms"]
+    alg = cand[dom]["alg_bytes_per_launch"]
     achieved = alg / (avg / 1e3) / 1e9
-    bucket = bool(pinfo and pinfo["path"] == "bucket")
-    names = {"pass": "thrs_pass_seg" if bucket else ("thrs_pass_xb" if kb == 4 and not vb and n >= (1 << 29) else "thrs_pass"),
-             "local": (pinfo or {}).get("local") or "local", "fallback": "thrs_pass_big"}
     frac = achieved / PEAK_HBM_GBS
-    traffic, traffic_src = load_pmc_traffic(wl)
+    traffic, traffic_src = load_pmc_traffic(wl, dom)
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-            "frac": round(frac, 4) if frac <= 1 else None, "traffic": traffic, "traffic_source": traffic_src,
-            "kernel": names[dom], "kind": dom, "avg_launch_ms": avg, "alg_bytes_per_launch": alg,
-            "kinds": kinds}
-    if frac > 1:   # e.g. fallback passes over only part of the keys: not a roofline
-        roof["note"] = "dominant launches moved fewer than 2*n*(K+V) bytes; frac withheld"
+            "frac": round(frac, 4), "traffic": traffic, "traffic_source": traffic_src,
+            "kernel": dom, "avg_launch_ms": avg, "alg_bytes_per_launch": alg,
+            "kernels": kernels, "kinds": kinds}
     # whole sort: B_alg = P*2*N*(K+V) for P 8-bit digits, the
     # work of P LSD passes whatever path ran ...
     passes = kb
@@ -328,16 +351,21 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def load_pmc_traffic(workload: str):
+def load_pmc_traffic(workload: str, kernel: str):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3
     --pmc run (profiles/pmc_traffic.json: which run, counters and gfx950
-    corrections are recorded there).  Not measured by this process: returned
-    with its source so the line says so."""
+    corrections are recorded there), when that run measured this kernel.  Not
+    measured by this process: returned with its source so the line says so."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         d = json.load(open(path))
         e = d.get(workload, {})
-        v = e.get("thrs_pass_bytes_per_launch")
+        if kernel.startswith("thrs_pass"):
+            v = e.get("thrs_pass_bytes_per_launch")
+        elif kernel == e.get("local_kernel") or kernel.startswith("thrs_local"):
+            v = e.get("local_bytes_per_launch") if kernel == e.get("local_kernel") else None
+        else:
+            v = e.get(f"{kernel}_bytes_per_launch")
         if v is None:
             return None, None
         return v, f"profiles/pmc_traffic.json[{workload}] from {e.get('source', '?')} (rocprofv3 --pmc, not this run)"
@@ -463,7 +491,9 @@ def main():
         barrier()
         t1 = time.perf_counter()
         prof = {k: T.profile_launches(k) for k in range(4)}
+        kern = {k: T.profile_launch_kernels(k) for k in range(4)}
         T.profile_enable(False)
+        big_keys = T.debug_big_keys(tmp, kt, vb, n, stream)   # the last sort's fallback work (0: none)
         rs.checkDeviceError(tmp)      # raises on a look-back / claim timeout in any timed step
         # correctness of the last timed step (outside the timed region)
         last = steps - 1
@@ -529,6 +559,8 @@ def main():
         barrier()
         t1 = time.perf_counter()
         prof = {k: T.profile_launches(k) for k in range(4)}
+        kern = {k: T.profile_launch_kernels(k) for k in range(4)}
+        big_keys = 0
         T.profile_enable(False)
         ko, _vo, n_out = out
         bad = TU.count_unsorted(kt, ko, n_out, 0, kb * 8)
@@ -576,7 +608,7 @@ def main():
                                                                      8: T.ValueType.U64, 16: T.ValueType.U128}[vb])
     pinfo = T.RadixSort([], cfg_info, T.Options(**dict(kv.split("=", 1) for kv in args.opt.split(",") if kv))).pathInfo(
         n, 0, kb * 8, bool(vb)) if not use_dist else None
-    roof = build_roofline(prof, steps, n, kb, vb, pinfo, elapsed, global_keys, world, wl)
+    roof = build_roofline(prof, kern, steps, n, kb, vb, pinfo, elapsed, global_keys, world, wl, big_keys)
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline == "auto":

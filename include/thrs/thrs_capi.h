@@ -219,6 +219,18 @@ int thrs_profile_read_kind(int kind, double* ms, int* launches);
  * key-codec variants of the top passes when the planes ran) takes a few
  * microseconds. */
 int thrs_profile_read_launches(int kind, double* ms, int cap, int* count);
+/* The kernel of each of those launches (THRS_PK_*) and its algorithmic bytes
+ * (one read + one write of every key and value it permutes, a read of every
+ * key it counts; 0 = data-dependent: the per-bucket fallback's launches, whose
+ * bytes follow from thrs_debug_big_keys), in the same order as
+ * thrs_profile_read_launches. */
+enum { THRS_PK_ZERO = 0, THRS_PK_HIST = 1, THRS_PK_SCAN = 2, THRS_PK_HIST_JOINT = 3, THRS_PK_PLAN = 4,
+       THRS_PK_PASS = 5, THRS_PK_PASS_XB = 6, THRS_PK_PASS_SEG = 7, THRS_PK_LOCAL16 = 8, THRS_PK_LOCAL = 9,
+       THRS_PK_LOCAL_PAIRS = 10, THRS_PK_LOCAL_KV = 11, THRS_PK_LOCAL_COUNT16 = 12, THRS_PK_BIG_PLAN = 13,
+       THRS_PK_BIG_HIST = 14, THRS_PK_PASS_BIG = 15, THRS_PK_BIG_COPY = 16, THRS_PK_COPY = 17 };
+int thrs_profile_read_launch_kernels(int kind, int32_t* kernel, uint64_t* bytes, int cap, int* count);
+/* The kernel function's name for a THRS_PK_* id ("" for an unknown id). */
+const char* thrs_profile_kernel_name(int kernel);
 
 /* The path a sort with these arguments takes -- a host decision, no device
  * work -- and the bytes it reads and writes in HBM when no bucket overflows
@@ -249,6 +261,13 @@ int thrs_rank_mode(void);
  * an LSD-path sort.  keyType / valueBytes / n: as that sort's. */
 int thrs_debug_bucket_mode(const void* temporaryBuffer, int keyType, int valueBytes, uint32_t n, hipStream_t stream,
                            int* mode, int* bigChunks);
+
+/* Diagnostic: synchronises `stream`; *keys = the keys of the LAST bucket-path
+ * sort on `temporaryBuffer` that sat in big chunks (the per-bucket fallback's
+ * work), 0 when every bucket fit its local sort.  Arguments as
+ * thrs_debug_bucket_mode. */
+int thrs_debug_big_keys(const void* temporaryBuffer, int keyType, int valueBytes, uint32_t n, hipStream_t stream,
+                        uint64_t* keys);
 
 /* Diagnostic: resident workgroups per CU of the 3-pass path's local bucket
  * sort kernel (4-byte keys), from the runtime's occupancy calculator. */

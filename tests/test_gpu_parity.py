@@ -678,3 +678,104 @@ def test_key_range_float_zeros(gpu, kt, vb, desc, where):
     assert np.array_equal(k.view(kdt), ek.view(kdt)), (where, mode, big)
     if vb:
         assert np.array_equal(v, ev), where
+
+
+def _float_keys_from_images(kt, img, desc):
+    """raw float bit patterns whose sort image (getKeyBits ^ descending mask,
+    kernel.cu:18-24, 46-69) is img (img never the image of -0)."""
+    kb = O.KEY_BYTES[kt]
+    dt = O.KEY_DTYPE[kt]
+    top = dt(1) << dt(8 * kb - 1)
+    b = (img ^ dt(~dt(0) if desc else 0)).astype(dt)     # getKeyBits(raw)
+    return np.where((b & top) != 0, b ^ top, ~b).astype(dt)
+
+
+def _squeeze_case_keys(kt, n, desc, varying, seed):
+    """Images whose 16 bucket bits are the half bit + `varying - 1` other
+    varying bits; the rest of the bucket field is constant per half, with a
+    different constant pattern in each half (some bits 1, some 0).  The bits
+    below the bucket field are random.  So only 2^varying buckets hold keys
+    until the squeeze drops one constant bit per half (thrs_plan_rows)."""
+    kb = O.KEY_BYTES[kt]
+    dt = O.KEY_DTYPE[kt]
+    W = 8 * kb
+    rng = np.random.default_rng(seed)
+    img = rng.integers(0, np.iinfo(dt).max, n, dtype=dt, endpoint=True)
+    h = (img >> dt(W - 1)) & dt(1)
+    pos = [2, 5, 9, 11, 13][:varying - 1]            # varying bucket bits besides the half bit
+    vmask = sum(1 << p for p in pos)
+    cst = [0x5A31 & ~vmask & 0x7FFF, 0x26C4 & ~vmask & 0x7FFF]   # per half
+    field = (img >> dt(W - 16)) & dt(0x7FFF)
+    field = (field & dt(vmask)) | np.where(h == 1, dt(cst[1]), dt(cst[0])).astype(dt)
+    img = (img & dt((1 << (W - 16)) - 1)) | (field << dt(W - 16)) | (h << dt(W - 1))
+    return _float_keys_from_images(kt, img.astype(dt), desc)
+
+
+@pytest.mark.parametrize("kt,vb", [(O.F32, 0), (O.F32, 4), (O.F32, 8), (O.F64, 0), (O.F64, 8)])
+@pytest.mark.parametrize("desc", [False, True])
+@pytest.mark.parametrize("fits", [True, False])
+def test_squeeze_vs_oracle(gpu, kt, vb, desc, fits):
+    """The data-chosen bucket bits (float keys, thrs_plan_rows + KeyMap<U,
+    true>): keys whose images share constant bits inside the bucket field
+    overflow their buckets; the plan drops one constant bit per image half,
+    histograms again under that map and the local sorts fit (fits=True, mode 0)
+    -- or, with too few varying bits, the per-bucket fallback runs under the
+    squeezed map (fits=False, mode 1).  Bit-exact with the oracle either way."""
+    torch = gpu
+    kb = O.KEY_BYTES[kt]
+    kdt = O.KEY_DTYPE[kt]
+    n = (1 << 20) + 333
+    kv = kb == 8 or vb >= 8          # 17408-key chunks (thrs_local_kv), else 9216 (n <= 2^29)
+    varying = (5 if kv else 6) if fits else 3
+    keys = _squeeze_case_keys(kt, n, desc, varying, 71 * kb + vb + (5 if desc else 0) + (3 if fits else 0))
+    vals = None
+    if vb:
+        vals = (np.arange(n * vb // 4, dtype=np.uint32) * np.uint32(2654435761)).view(
+            {4: np.uint32, 8: np.uint64}[vb])
+    ek, ev = O.lsd_sort(kt, keys, vals, 0, 8 * kb, desc)
+    rs = make_sorter(kt, vb, desc, path="bucket")
+    (mode, big), k, v = _mode_after(torch, rs, keys, vals, kt, vb)
+    assert np.array_equal(k.view(kdt), ek.view(kdt)), (mode, big)
+    if vb:
+        assert np.array_equal(v, ev)
+    assert mode == (0 if fits else 1), (mode, big)
+
+
+@pytest.mark.large
+@pytest.mark.parametrize("kt,vb,n", [(O.F32, 0, 1 << 30),    # f32 keys-only, the reference's generator
+                                     (O.F32, 4, 1 << 30),    # SortPairs.KF32V32's distribution (unittest.cpp:433-439)
+                                     (O.F64, 8, 1 << 29)])   # f64 pairs (randomizeValues clears bit 52)
+def test_reference_float_generator_stays_local(gpu, kt, vb, n):
+    """randomizeValues (unittest.cpp:96-116) clears the lowest exponent bit of
+    every f32 / f64 key, so half of the 65536 top-16-bit buckets are empty and
+    at these sizes every used bucket would overflow its local sort.  The
+    squeeze keeps the whole sort on the bucket path: mode 0, no big chunks;
+    sortedness, the multiset fingerprint and (pairs) gather + stability."""
+    torch = gpu
+    import tinyhipradixsort_amd as T
+    from tinyhipradixsort_amd import testutil as TU
+    kb = O.KEY_BYTES[kt]
+    keys = _big_keys(torch, kt, n)
+    orig = keys.clone() if vb else None
+    torch.cuda.synchronize()
+    fp = TU.fingerprint(kt, keys, n)
+    rs = make_sorter(kt, vb, False)
+    d = rs.getTemporaryBufferBytes(n)
+    if vb:
+        vals = torch.empty(vb * n, dtype=torch.uint8, device="cuda")
+        TU.iota(vb, vals, n)
+        tmp = torch.empty(d.getTemporaryBufferBytesForSortPairs(), dtype=torch.uint8, device="cuda")
+        rs.sortPairs(keys, vals, n, tmp, 0, kb * 8)
+    else:
+        tmp = torch.empty(d.getTemporaryBufferBytesForSortKeys(), dtype=torch.uint8, device="cuda")
+        rs.sortKeys(keys, n, tmp, 0, kb * 8)
+    torch.cuda.synchronize()
+    rs.checkDeviceError(tmp)
+    assert rs.debugBucketMode(tmp, n, bool(vb)) == (0, 0)
+    assert T.debug_big_keys(tmp, kt, vb, n) == 0
+    assert TU.count_unsorted(kt, keys, n, 0, kb * 8) == 0
+    assert TU.fingerprint(kt, keys, n) == fp
+    if vb:
+        r = TU.check_pairs(kt, vb, orig, keys, vals, n, 0, kb * 8)
+        assert r["gather_mismatch"] == 0 and r["unstable"] == 0
+        assert (r["index_sum"], r["index_xor"]) == TU.expected_index_fingerprint(n)

@@ -89,6 +89,13 @@ def lib() -> ctypes.CDLL:
         L.thrs_rank_mode.restype = i32
         L.thrs_profile_read_launches.argtypes = [i32, ctypes.POINTER(ctypes.c_double), i32, ctypes.POINTER(i32)]
         L.thrs_profile_read_launches.restype = i32
+        L.thrs_profile_read_launch_kernels.argtypes = [i32, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(u64), i32,
+                                                       ctypes.POINTER(i32)]
+        L.thrs_profile_read_launch_kernels.restype = i32
+        L.thrs_profile_kernel_name.argtypes = [i32]
+        L.thrs_profile_kernel_name.restype = ctypes.c_char_p
+        L.thrs_debug_big_keys.argtypes = [vp, i32, i32, u32, vp, ctypes.POINTER(u64)]
+        L.thrs_debug_big_keys.restype = i32
         L.thrs_get_path_info.argtypes = [ctypes.POINTER(_CConfig), ctypes.POINTER(_COptions), i32, u32, i32, i32,
                                      ctypes.POINTER(_CPathInfo)]
         L.thrs_get_path_info.restype = i32
@@ -434,6 +441,27 @@ def profile_launches(kind: int) -> list:
     buf = (ctypes.c_double * max(1, cnt.value))()
     _check(lib().thrs_profile_read_launches(int(kind), buf, cnt.value, ctypes.byref(cnt)))
     return [buf[i] for i in range(cnt.value)]
+
+
+def profile_launch_kernels(kind: int) -> list:
+    """(kernel name, algorithmic bytes) of every launch of one kind since
+    profile_enable, in the order of profile_launches (bytes 0 = data-dependent:
+    the per-bucket fallback's launches; see debug_big_keys)."""
+    cnt = ctypes.c_int()
+    _check(lib().thrs_profile_read_launch_kernels(int(kind), None, None, 0, ctypes.byref(cnt)))
+    ids = (ctypes.c_int32 * max(1, cnt.value))()
+    byt = (ctypes.c_uint64 * max(1, cnt.value))()
+    _check(lib().thrs_profile_read_launch_kernels(int(kind), ids, byt, cnt.value, ctypes.byref(cnt)))
+    return [(lib().thrs_profile_kernel_name(ids[i]).decode(), int(byt[i])) for i in range(cnt.value)]
+
+
+def debug_big_keys(temporaryBuffer, keyType: int, valueBytes: int, n: int, stream=None) -> int:
+    """Keys of the last bucket-path sort on this buffer that took the
+    per-bucket fallback (thrs_debug_big_keys; synchronising)."""
+    out = ctypes.c_uint64()
+    _check(lib().thrs_debug_big_keys(_ptr(temporaryBuffer), int(keyType), int(valueBytes), int(n),
+                                     _stream(stream), ctypes.byref(out)))
+    return int(out.value)
 
 
 def profile_read() -> dict:

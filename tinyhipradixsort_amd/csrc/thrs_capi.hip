@@ -35,6 +35,8 @@ namespace {
 struct ProfRec {
   hipEvent_t a, b;
   int kind;
+  int kernel;      // THRS_PK_*
+  uint64_t bytes;  // algorithmic bytes of the launch (0 = data-dependent)
 };
 std::mutex g_prof_mu;
 bool g_prof_on = false;
@@ -60,12 +62,12 @@ hipEvent_t prof_begin(hipStream_t s) {
   if (a) (void)hipEventRecord(a, s);
   return a;
 }
-void prof_end(hipEvent_t a, hipStream_t s, int kind) {
+void prof_end(hipEvent_t a, hipStream_t s, int kind, int kernel, uint64_t bytes) {
   std::lock_guard<std::mutex> g(g_prof_mu);
   hipEvent_t b = prof_event();
   if (!b) return;
   (void)hipEventRecord(b, s);
-  g_prof.push_back({a, b, kind});
+  g_prof.push_back({a, b, kind, kernel, bytes});
 }
 
 uint64_t* g_stamps = nullptr;
@@ -343,6 +345,28 @@ THRS_API int thrs_debug_bucket_mode(const void* tmp, int keyType, int valueBytes
   return THRS_SUCCESS;
 }
 
+THRS_API int thrs_debug_big_keys(const void* tmp, int keyType, int valueBytes, uint32_t n, hipStream_t stream,
+                                 uint64_t* keys) {
+  if (!tmp || !keys || !valid_key(keyType) ||
+      !(valueBytes == 0 || valueBytes == 4 || valueBytes == 8 || valueBytes == 16))
+    return THRS_ERROR_INVALID_VALUE;
+  const Plan plan = make_plan(keyType, valueBytes, n);
+  const char* hyb = static_cast<const char*>(tmp) + plan.hybridOff;
+  uint32_t meta[8] = {};
+  if (hipMemcpyAsync(meta, hyb + kMetaOff, sizeof(meta), hipMemcpyDeviceToHost, stream) != hipSuccess ||
+      hipStreamSynchronize(stream) != hipSuccess)
+    return THRS_ERROR_HIP;
+  *keys = 0;
+  const uint32_t m = meta[kMetaBigCount];
+  if (meta[kMetaMode] != 1 || m == 0 || m > kBuckets) return THRS_SUCCESS;
+  uint32_t total = 0;
+  if (hipMemcpyAsync(&total, hyb + kBigPosOff + (uint64_t)m * 4, 4, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+      hipStreamSynchronize(stream) != hipSuccess)
+    return THRS_ERROR_HIP;
+  *keys = total;
+  return THRS_SUCCESS;
+}
+
 THRS_API int thrs_check_device_error(void* tmp, hipStream_t stream) {
   if (!tmp) return THRS_ERROR_INVALID_VALUE;
   uint32_t err = 0;
@@ -406,6 +430,29 @@ THRS_API int thrs_profile_read_launches(int kind, double* ms, int cap, int* coun
   }
   if (count) *count = c;
   return THRS_SUCCESS;
+}
+
+THRS_API int thrs_profile_read_launch_kernels(int kind, int32_t* kernel, uint64_t* bytes, int cap, int* count) {
+  std::lock_guard<std::mutex> g(g_prof_mu);
+  int c = 0;
+  for (auto& r : g_prof) {
+    if (r.kind != kind) continue;
+    if (c < cap) {
+      if (kernel) kernel[c] = r.kernel;
+      if (bytes) bytes[c] = r.bytes;
+    }
+    ++c;
+  }
+  if (count) *count = c;
+  return THRS_SUCCESS;
+}
+
+THRS_API const char* thrs_profile_kernel_name(int kernel) {
+  static const char* names[] = {"thrs_zero_ranges", "thrs_hist", "thrs_scan", "thrs_hist_joint", "thrs_plan",
+                                "thrs_pass", "thrs_pass_xb", "thrs_pass_seg", "thrs_local16", "thrs_local",
+                                "thrs_local_pairs", "thrs_local_kv", "thrs_local_count16", "thrs_big_plan",
+                                "thrs_big_hist", "thrs_pass_big", "thrs_big_copy", "copy-back"};
+  return kernel >= 0 && kernel < (int)(sizeof(names) / sizeof(names[0])) ? names[kernel] : "";
 }
 
 THRS_API int thrs_get_path_info(const thrs_config* cfg, const thrs_options* options, int pairs, uint32_t n,

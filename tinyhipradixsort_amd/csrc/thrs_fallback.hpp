@@ -110,9 +110,9 @@ constexpr size_t kBigHistLds = (size_t)kBigMaxLow * kBins * kBigCopies * 4;
 
 template <int KT>
 __global__ __launch_bounds__(kHistThreads) void thrs_big_hist(
-    const typename KeyTraits<KT>::U* __restrict__ keys, KeyMap<typename KeyTraits<KT>::U> km, int startBits, int nLow,
+    const typename KeyTraits<KT>::U* __restrict__ keys, KeyMap<typename KeyTraits<KT>::U> kmh, int startBits, int nLow,
     const uint32_t* __restrict__ chunkOff, uint32_t* __restrict__ meta, const uint32_t* __restrict__ bigB,
-    const uint32_t* __restrict__ bigPos, uint32_t* __restrict__ bigHist) {
+    const uint32_t* __restrict__ bigPos, uint32_t* __restrict__ bigHist, const SqueezeWords* __restrict__ sq) {
   using U = typename KeyTraits<KT>::U;
   if (meta[kMetaFallback] == 0) return;
   extern __shared__ __attribute__((aligned(16))) uint32_t s_h[];  // [nLow][256][kBigCopies]
@@ -125,7 +125,7 @@ __global__ __launch_bounds__(kHistThreads) void thrs_big_hist(
   const uint32_t len = (total + G - 1) / G;
   const uint32_t lo = min(total, blockIdx.x * len), hi = min(total, lo + len);
   uint32_t* my = s_h + (tid % kBigCopies);
-  if (lo < hi) {
+  if (lo < hi) with_map<KT>(kmh, sq, [&](auto km) {
     for (uint32_t c = big_find(bigPos, M, lo); c < M && bigPos[c] < hi; ++c) {
       const uint32_t p0 = bigPos[c], a = max(lo, p0), b = min(hi, bigPos[c + 1]);
       const uint32_t start = chunkOff[bigB[c]], size = bigPos[c + 1] - p0;
@@ -163,7 +163,7 @@ __global__ __launch_bounds__(kHistThreads) void thrs_big_hist(
       }
       __syncthreads();
     }
-  }
+  });
   // the last workgroup to finish plans the low passes
   __threadfence();
   if (tid == 0) s_last = atomicAdd(&meta[kMetaBigDone], 1u) == G - 1;
@@ -194,7 +194,7 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
     KeyMap<typename KeyTraits<KT>::U> km, int shift, int p, int nLow, const uint32_t* __restrict__ chunkOff,
     uint32_t* __restrict__ meta, const uint32_t* __restrict__ bigB, const uint32_t* __restrict__ bigPos,
     const uint32_t* __restrict__ bigTile, const uint32_t* __restrict__ bigHist, ST* __restrict__ status0,
-    ST* __restrict__ status1, uint32_t* __restrict__ errFlag) {
+    ST* __restrict__ status1, uint32_t* __restrict__ errFlag, const SqueezeWords* __restrict__ sq) {
   using U = typename KeyTraits<KT>::U;
   using VW = typename ValueWord<VB>::T;
   using G = PassGeom<sizeof(U), VB>;
@@ -215,6 +215,7 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
   ST* statusNext = p + 1 < nLow ? (par ? status0 : status1) : nullptr;
   const uint32_t M = meta[kMetaBigCount], nTiles = bigTile[M];
   const uint32_t tid = threadIdx.x;
+  with_map<KT>(km, sq, [&](auto kmx) {
   U k[G::KPT];
   VW v[VB ? G::KPT : 1];
   for (;;) {
@@ -243,11 +244,12 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
     GroupTables<ST> g{};  // (flat look-back: no group tables)
     g.nTiles = chain + (size + T - 1) / T;
     load_tile<KT, VB>(kin, vin, keyStart, valid, k, v);
-    pass_tile<KT, VB, ST, ATOMIC_RANK, NoMid, kCodecKeys, false>(kin, kout, vin, vout, keyStart, valid, km, shift,
+    pass_tile<KT, VB, ST, ATOMIC_RANK, NoMid, kCodecKeys, false>(kin, kout, vin, vout, keyStart, valid, kmx, shift,
                                                                 myBase, start + size, status, statusNext, errFlag, tile, chain, g,
                                                                 smem, nullptr, k, v, NoMid{});
     lds_barrier();  // stage, s_gofs, s_misc and s_w are reused by the next tile
   }
+  });
 }
 
 // An odd number of running low passes left the big chunks in the temporary

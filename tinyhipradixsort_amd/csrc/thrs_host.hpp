@@ -83,13 +83,17 @@ struct Plan {
                           // fallback area [+ u8 plane]
 };
 
-// hybrid area: u32 joint[65536] | segHistA[8][256] | rowHist[256] | meta[64]
-// (all zeroed up front) | chunkOff[65537] | chunkB0[65537] | segment tables
+// hybrid area: u32 joint[65536] | segHistA[8][256] | rowHist[256] | the same
+// three for a squeezed second histogram | meta[64] (all zeroed up front) | chunkOff[65537] | chunkB0[65537] | segment tables
 // of the two top-digit passes
 constexpr uint64_t kJointBytes = kBuckets * 4;
 constexpr uint64_t kSegHistAOff = kJointBytes;                    // per position segment: second-digit counts
 constexpr uint64_t kRowHistOff = kSegHistAOff + kSegs * 256 * 4;  // top-digit counts (thrs_hist_joint)
-constexpr uint64_t kMetaOff = kRowHistOff + 256 * 4;              // zero: thrs_plan_rows raises its flags atomically
+// the second histogram of a squeezed sort (float keys: thrs_plan_rows, KeyMap<U, true>): joint | segHistA | rowHist
+constexpr uint64_t kJoint2Off = kRowHistOff + 256 * 4;
+constexpr uint64_t kSegHistA2Off = kJoint2Off + kJointBytes;
+constexpr uint64_t kRowHist2Off = kSegHistA2Off + kSegs * 256 * 4;
+constexpr uint64_t kMetaOff = kRowHist2Off + 256 * 4;             // zero: thrs_plan_rows raises its flags atomically
 constexpr uint64_t kJointZero = kMetaOff + 256;
 constexpr uint64_t kChunkOffOff = kJointZero;
 constexpr uint64_t kChunkB0Off = kChunkOffOff + round_up_c((kBuckets + 1) * 4, 256);
@@ -150,14 +154,17 @@ int cu_count();
 // HIP-event timing of the launches (thrs_profile_*): kind 0 = histogram +
 // plan, 1 = device-wide digit pass, 2 = local sort, 3 = fallback-only launches
 hipEvent_t prof_begin(hipStream_t s);
-void prof_end(hipEvent_t a, hipStream_t s, int kind);
-struct ProfScope {  // records [a, b) around the launches issued in its lifetime
+void prof_end(hipEvent_t a, hipStream_t s, int kind, int kernel, uint64_t bytes);
+// records [a, b) around the launches issued in its lifetime, with the
+// kernel's id (THRS_PK_*) and algorithmic bytes (0 = data-dependent)
+struct ProfScope {
   hipStream_t s;
-  int kind;
+  int kind, kernel;
+  uint64_t bytes;
   hipEvent_t a;
-  ProfScope(hipStream_t s_, int k) : s(s_), kind(k), a(prof_begin(s_)) {}
+  ProfScope(hipStream_t s_, int k, int kern, uint64_t b) : s(s_), kind(k), kernel(kern), bytes(b), a(prof_begin(s_)) {}
   ~ProfScope() {
-    if (a) prof_end(a, s, kind);
+    if (a) prof_end(a, s, kind, kernel, bytes);
   }
 };
 extern uint64_t* g_stamps;   // THRS_STAMPS diagnostic builds only (thrs_debug_set_stamps)
@@ -330,6 +337,11 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   const bool planes = P.planes, ranged = P.ranged, useXb = P.useXb;
   const int nLow = P.nLow;
   const uint32_t cap = P.cap;
+  // the device-chosen squeeze (float keys over the whole key, single-bucket
+  // chunks: thrs_plan_rows; KeyMap<U, true> in thrs_kernels.hpp)
+  const bool squeeze = kSqueezable<KT> && bucket && P.fullWindow && !local32;
+  const SqueezeWords* sqw =
+      squeeze ? reinterpret_cast<const SqueezeWords*>(scratch + plan.hybridOff + kMetaOff + kMetaSqueeze * 4) : nullptr;
   KeyMap<U> km{orderMask, (U)0, 0u};
   if (ranged) {
     const U span = (U)opt.rangeHi - (U)opt.rangeLo;  // > 0 (sort_impl returns at once for 0)
@@ -363,7 +375,8 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
       allow_lds(kernelXb, lds) != hipSuccess || allow_lds(kernelBig, lds) != hipSuccess)
     return THRS_ERROR_HIP;
   if (bucket) {
-    if (allow_lds(thrs_hist_joint<KT>, kJointLds) != hipSuccess || allow_lds(sk, lds) != hipSuccess)
+    if (allow_lds(thrs_hist_joint<KT>, kJointLds) != hipSuccess || allow_lds(sk, lds) != hipSuccess ||
+        (squeeze && allow_lds(thrs_hist_joint<KT, true>, kJointLds) != hipSuccess))
       return THRS_ERROR_HIP;
     if (planes && (allow_lds(skSplit, lds) != hipSuccess || allow_lds(skPlanes, lds) != hipSuccess))
       return THRS_ERROR_HIP;
@@ -449,26 +462,46 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   }
   char* claim = scratch + kHeaderBytes + 2 * plan.setBytes;  // 8 per-pass claim areas
 
+  const uint64_t keyBytes = (uint64_t)n * sizeof(U), moveBytes = 2 * (uint64_t)n * (sizeof(U) + VB);
   {  // histograms of every pass in one read of the keys
-    ProfScope prof(stream, 0);
     const int vec = (reinterpret_cast<uintptr_t>(keys) % 16) == 0;
     const uint64_t want = ((uint64_t)n + kHistThreads * 64 - 1) / (kHistThreads * 64);
     const int hgrid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cu_count() * THRS_HIST_GRID_MULT));
     if (bucket) {
-      hipLaunchKernelGGL(thrs_hist_joint<KT>, dim3(hgrid), dim3(kHistThreads), kJointLds, stream,
+      {
+        ProfScope prof(stream, 0, THRS_PK_HIST_JOINT, keyBytes);
+        hipLaunchKernelGGL(thrs_hist_joint<KT>, dim3(hgrid), dim3(kHistThreads), kJointLds, stream,
                          static_cast<const U*>(keys), n, km, startBits + 8 * nLow, vec, joint,
                          reinterpret_cast<uint32_t*>(hyb + kSegHistAOff), reinterpret_cast<uint32_t*>(hyb + kRowHistOff),
-                         tables);
-      if (!local32) {
-        // single-bucket chunks: one workgroup per top digit
-        hipLaunchKernelGGL(thrs_plan_rows, dim3(kBins), dim3(kPlanRowThreads), 0, stream, joint,
-                           reinterpret_cast<const uint32_t*>(hyb + kRowHistOff),
-                           reinterpret_cast<const uint32_t*>(hyb + kSegHistAOff), n, cap, base + nLow * kBins,
+                         tables, meta, nullptr);
+      }
+      // single-bucket chunks: one workgroup per top digit; float keys with
+      // the whole key decide the squeeze (sqMode 1) and, if it went on,
+      // histogram and plan once more under it (gated: a few us otherwise)
+      auto plan_rows = [&](int sqMode, uint64_t jOff, uint64_t sOff, uint64_t rOff) {
+        ProfScope prof(stream, 0, THRS_PK_PLAN, 3 * kJointBytes);
+        hipLaunchKernelGGL(thrs_plan_rows, dim3(kBins), dim3(kPlanRowThreads), 0, stream,
+                           reinterpret_cast<const uint32_t*>(hyb + jOff), reinterpret_cast<const uint32_t*>(hyb + rOff),
+                           reinterpret_cast<const uint32_t*>(hyb + sOff), n, cap, base + nLow * kBins,
                            chunkOff, chunkB0, meta, reinterpret_cast<uint32_t*>(hyb + kSegInfoOff),
                            reinterpret_cast<uint32_t*>(hyb + kSegBaseOff), (uint32_t)G::TILE, (uint32_t)hgrid,
                            reinterpret_cast<uint32_t*>(hyb + kSegInfoAOff), reinterpret_cast<uint32_t*>(hyb + kSegBaseAOff),
-                           reinterpret_cast<uint32_t*>(hyb + kBigBOff));
+                           reinterpret_cast<uint32_t*>(hyb + kBigBOff), sqMode, 8 * KB);
+      };
+      if (!local32 && squeeze) {
+        plan_rows(1, 0, kSegHistAOff, kRowHistOff);
+        {
+          ProfScope prof(stream, 0, THRS_PK_HIST_JOINT, keyBytes);
+          hipLaunchKernelGGL((thrs_hist_joint<KT, true>), dim3(hgrid), dim3(kHistThreads), kJointLds, stream,
+                             static_cast<const U*>(keys), n, km, startBits + 8 * nLow, vec,
+                             reinterpret_cast<uint32_t*>(hyb + kJoint2Off), reinterpret_cast<uint32_t*>(hyb + kSegHistA2Off),
+                             reinterpret_cast<uint32_t*>(hyb + kRowHist2Off), ZeroRanges{}, meta, sqw);
+        }
+        plan_rows(2, kJoint2Off, kSegHistA2Off, kRowHist2Off);
+      } else if (!local32) {
+        plan_rows(0, 0, kSegHistAOff, kRowHistOff);
       } else {
+        ProfScope prof(stream, 0, THRS_PK_PLAN, 3 * kJointBytes);
         // chunks: whole buckets; neighbouring buckets below kLocCap/2 keys share one
         hipLaunchKernelGGL(thrs_plan, dim3(1), dim3(kPlanThreads), 0, stream, joint, n, base + nLow * kBins, chunkOff,
                            chunkB0, meta, cap, smallLocal ? kLocSmallLogT : kLocLogT,
@@ -478,8 +511,12 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                            reinterpret_cast<uint32_t*>(hyb + kBigBOff));
       }
     } else {
-      hipLaunchKernelGGL(thrs_hist<KT>, dim3(hgrid), dim3(kHistThreads), histLds, stream, static_cast<const U*>(keys),
-                         n, km, startBits, nPass, vec, hist);
+      {
+        ProfScope prof(stream, 0, THRS_PK_HIST, keyBytes);
+        hipLaunchKernelGGL(thrs_hist<KT>, dim3(hgrid), dim3(kHistThreads), histLds, stream,
+                           static_cast<const U*>(keys), n, km, startBits, nPass, vec, hist);
+      }
+      ProfScope prof(stream, 0, THRS_PK_SCAN, 2 * (uint64_t)nPass * kBins * 4);
       hipLaunchKernelGGL(thrs_scan, dim3(1), dim3(kThreads), 0, stream, hist, base, nPass);
     }
     if (counts && hipMemcpyAsync(counts, hist, kBins * sizeof(uint32_t), hipMemcpyDeviceToDevice, stream) != hipSuccess)
@@ -495,7 +532,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     GroupTables<ST> g = grp[p & 1];
     g.gaNext = more ? grp[(p + 1) & 1].ga : nullptr;
     g.gpNext = more ? grp[(p + 1) & 1].gp : nullptr;
-    ProfScope prof(stream, 1);
+    ProfScope prof(stream, 1, useXb ? THRS_PK_PASS_XB : THRS_PK_PASS, moveBytes);
     hipLaunchKernelGGL(kernel, dim3(grid), dim3(G::THREADS), lds, stream, kin, kout, vin, vout, n, km, startBits + 8 * p,
                        base + p * kBins, status[p & 1], next,
                        useXb ? reinterpret_cast<uint32_t*>(claim + p * plan.claimBytes) : counters + p, err, g,
@@ -541,7 +578,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     // and skipping both keeps the keys in K.
     auto launch_seg = [&](int p, U* kin, U* kout, VW* vin, VW* vout, uint64_t infoOff, uint64_t baseOff,
                           const uint32_t* gate, uint32_t gateMask, int codec = kCodecKeys) {
-      ProfScope prof(stream, 1);
+      ProfScope prof(stream, 1, THRS_PK_PASS_SEG, moveBytes);
       auto kern = codec == kCodecSplit ? skSplit : codec == kCodecPlanes ? skPlanes : sk;
       // kCodecPlanes: image-space input (identity map), digit at bits 16-23 of k'
       hipLaunchKernelGGL(kern, dim3((uint32_t)segPerCU * cu_count()), dim3(G::THREADS), lds, stream, kin, kout, vin,
@@ -549,7 +586,8 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                          reinterpret_cast<uint32_t*>(hyb + infoOff), reinterpret_cast<const uint32_t*>(hyb + baseOff),
                          status[p & 1], err, grp[p & 1], gate, gateMask, hiP,
                          g_stamps ? g_stamps + (uint64_t)(p - nLow) * (plan.nTiles + kSegTilePad) * kStampSlots
-                                  : nullptr);
+                                  : nullptr,
+                         sqw);
     };
     const uint64_t sw = plan.wideStatus ? 8 : 4;
     const int setB = (nLow + 1) & 1;
@@ -584,7 +622,12 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     else
       launch_pass(nLow + 1, keyOut, K, valOut, V, mode, kGateMode0 | kGateMode1);
     {
-      ProfScope prof(stream, 2);
+      ProfScope prof(stream, 2,
+                     kKV ? THRS_PK_LOCAL_KV
+                     : kPairs4 ? THRS_PK_LOCAL_PAIRS
+                     : count16 ? THRS_PK_LOCAL_COUNT16
+                     : local16 ? THRS_PK_LOCAL16 : THRS_PK_LOCAL,
+                     moveBytes);
       // never more workgroups than chunks can exist: <= 256 (one per top digit)
       // + 2 per non-empty bucket, and <= the number of buckets (single-bucket
       // chunks -- every local sort but the 32-bit one: thrs_plan_rows makes
@@ -593,14 +636,15 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
       const dim3 lgrid((uint32_t)maxChunks);
       if constexpr (kKV) {
         auto lk = atomicRank ? thrs_local_kv<KT, VB, true> : thrs_local_kv<KT, VB, false>;
-        hipLaunchKernelGGL(lk, lgrid, dim3(LocKV::THREADS), LocKV::LDS, stream, K, V, km, chunkOff, chunkB0, meta);
+        hipLaunchKernelGGL(lk, lgrid, dim3(LocKV::THREADS), LocKV::LDS, stream, K, V, km, chunkOff, chunkB0, meta,
+                           sqw);
       } else if constexpr (kPairs4) {
         auto launch_pairs = [&](auto geom) {
           using LG = decltype(geom);
           auto lk = atomicRank ? thrs_local_pairs<KT, true, LG> : thrs_local_pairs<KT, false, LG>;
           hipLaunchKernelGGL(lk, lgrid, dim3(LG::THREADS), LG::template lds<U>(), stream,
                              reinterpret_cast<uint32_t*>(K), reinterpret_cast<uint32_t*>(V), km32, chunkOff, chunkB0,
-                             meta);
+                             meta, sqw);
         };
         if (smallLocal) launch_pairs(LocSmall{});
         else launch_pairs(LocBig{});
@@ -609,7 +653,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
           using LG = decltype(geom);
           auto lk = atomicRank ? thrs_local16<KT, true, LG> : thrs_local16<KT, false, LG>;
           hipLaunchKernelGGL(lk, lgrid, dim3(LG::THREADS), LG::LDS, stream, reinterpret_cast<uint32_t*>(K), km32,
-                             chunkOff, chunkB0, meta, planes ? static_cast<const uint16_t*>(lo2P) : nullptr);
+                             chunkOff, chunkB0, meta, planes ? static_cast<const uint16_t*>(lo2P) : nullptr, sqw);
         };
         auto launch32 = [&](auto geom) {
           using LG = decltype(geom);
@@ -650,24 +694,24 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
       uint32_t* bigHist = reinterpret_cast<uint32_t*>(scratch + plan.bigHistOff);
       // (the low passes reuse both look-back table sets: zeroed by thrs_big_plan)
       {
-        ProfScope prof(stream, 3);
+        ProfScope prof(stream, 3, THRS_PK_BIG_PLAN, 0);
         hipLaunchKernelGGL(thrs_big_plan, dim3(std::min<uint32_t>(256, cu_count())), dim3(kBigPlanThreads), 0, stream,
                            chunkOff, meta, bigB, bigPos, bigTile, (uint32_t)G::TILE, reinterpret_cast<uint4*>(bigHist),
                            nLow, reinterpret_cast<uint4*>(scratch + kHeaderBytes), (uint64_t)(2 * plan.setBytes / 16));
       }
       {
-        ProfScope prof(stream, 3);
+        ProfScope prof(stream, 3, THRS_PK_BIG_HIST, 0);
         hipLaunchKernelGGL(thrs_big_hist<KT>, dim3(cu_count()), dim3(kHistThreads),
                            (size_t)nLow * kBins * kBigCopies * 4, stream, static_cast<const U*>(keys), km, startBits,
-                           nLow, chunkOff, meta, bigB, bigPos, bigHist);
+                           nLow, chunkOff, meta, bigB, bigPos, bigHist, sqw);
       }
       for (int p = 0; p < nLow; ++p) {
-        ProfScope prof(stream, 3);
+        ProfScope prof(stream, 3, THRS_PK_PASS_BIG, 0);
         hipLaunchKernelGGL(kernelBig, dim3(gridBig), dim3(G::THREADS), lds, stream, K, keyOut, V, valOut, km,
                            startBits + 8 * p, p, nLow, chunkOff, meta, bigB, bigPos, bigTile, bigHist, status[0],
-                           status[1], err);
+                           status[1], err, sqw);
       }
-      ProfScope prof(stream, 3);
+      ProfScope prof(stream, 3, THRS_PK_BIG_COPY, 0);
       hipLaunchKernelGGL((thrs_big_copy<U, VW>), dim3(2048), dim3(256), 0, stream, K, keyOut, VB ? V : nullptr, valOut,
                          chunkOff, meta, bigB, bigPos);
     }

@@ -55,7 +55,15 @@ enum {
   kMetaBigPass = 8,  // [8]: per low pass p, bit 0 = runs (not the identity for every big chunk), bit 1 = parity
   kMetaBigTicket = 16,  // [8]: per low pass p, its tile ticket
   kMetaBigSingle = 24,  // [6]: per low pass p, big chunks whose digit p is one value
+  // the squeeze (float keys, thrs_plan_rows; KeyMap<U, true>):
+  kMetaRehist = 32,     // 1: the squeeze is on -- histogram and plan again under it
+  kMetaPlanDone = 33,   // thrs_plan_rows workgroups finished (the last one decides)
+  kMetaOr1 = 34,        // [2]: per image half, OR of the non-empty buckets' indices
+  kMetaOr0 = 36,        // [2]: per image half, OR of their complements (16 bits)
+  kMetaBigHalf = 38,    // [2]: per image half, buckets above the local capacity
+  kMetaSqueeze = 48,    // SqueezeWords (14 words, to 61)
 };
+static_assert(kMetaSqueeze * 4 + sizeof(SqueezeWords) <= 256, "meta is 64 words");
 // gate masks of the gated launches: bit v set = run when the gate word is v
 constexpr uint32_t kGateMode0 = 1u << 0, kGateMode1 = 1u << 1, kGateMode2 = 1u << 2;  // on meta[kMetaMode]
 
@@ -90,15 +98,26 @@ __device__ __forceinline__ uint32_t hj_seg_pos(uint32_t n, uint32_t G, uint32_t 
   return (uint32_t)min((uint64_t)n, first * hj_len(n, G));
 }
 
-template <int KT>
+// SQ: the second histogram of a squeezed sort (float keys; thrs_plan_rows
+// found constant bits among the bucket bits and switched the squeeze on):
+// runs only when meta[kMetaRehist] is set, under the squeezed map.
+template <int KT, bool SQ = false>
 __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename KeyTraits<KT>::U* __restrict__ keys,
-                                                                uint32_t n, KeyMap<typename KeyTraits<KT>::U> km,
+                                                                uint32_t n, KeyMap<typename KeyTraits<KT>::U> kmh,
                                                                 int bucketShift, int vec,
                                                                 uint32_t* __restrict__ joint,
                                                                 uint32_t* __restrict__ segHist /* [8][256] */,
                                                                 uint32_t* __restrict__ rowHist /* [256] */,
-                                                                ZeroRanges tables) {
+                                                                ZeroRanges tables, const uint32_t* __restrict__ meta,
+                                                                const SqueezeWords* __restrict__ sq) {
   using U = typename KeyTraits<KT>::U;
+  if constexpr (SQ) {
+    if (meta[kMetaRehist] == 0) return;
+  }
+  const auto km = [&]() {
+    if constexpr (SQ) return with_squeeze(kmh, sq);
+    else return kmh;
+  }();
   extern __shared__ __attribute__((aligned(16))) uint32_t s_joint[];
   uint32_t* s_d2 = s_joint + kJointWords;
   uint32_t* s_log = s_d2 + kBins;
@@ -310,13 +329,60 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
 // Workgroup 0 also writes the second digit's bases, both passes' segment
 // tables and the chunk count.
 constexpr int kPlanRowThreads = 256;
+// The squeeze decision (float keys, sqMode 1), by the last workgroup to
+// finish: in each image half that holds big buckets, the highest bucket bit
+// below the half bit that every non-empty bucket of the half shares (from the
+// OR of the indices and of their complements) is dropped (KeyMap<U, true>);
+// if any half gets one, the squeeze goes on and the histogram and the plan
+// are taken again under it (meta[kMetaRehist]; the flags raised by this plan
+// are cleared for the second one).  Only when some bucket would take the
+// per-bucket fallback (mode 1): an in-capacity plan is kept as it is.
+__device__ __forceinline__ void plan_squeeze(uint32_t* __restrict__ meta, int keyBits) {
+  if (load_agent(&meta[kMetaMode]) != 1u) return;
+  uint64_t hiM[2], loM[2], cst[2];
+  bool any = false;
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t o1 = load_agent(&meta[kMetaOr1 + h]), o0 = load_agent(&meta[kMetaOr0 + h]);
+    const uint32_t big = load_agent(&meta[kMetaBigHalf + h]);
+    const uint32_t cm = ~(o1 & o0) & 0x7FFFu;  // constant bucket bits below the half bit
+    hiM[h] = ~0ull;
+    loM[h] = 0;
+    cst[h] = 0;
+    if (big && (o1 | o0) && cm) {
+      const int bb = 31 - __builtin_clz(cm);
+      const int b = bb + keyBits - 16;  // its image bit
+      hiM[h] = ~((2ull << b) - 1ull);
+      loM[h] = (1ull << b) - 1ull;
+      cst[h] = (uint64_t)((o1 >> bb) & 1u) << b;
+      any = true;
+    }
+  }
+  if (!any) return;
+  SqueezeWords* sq = reinterpret_cast<SqueezeWords*>(meta + kMetaSqueeze);
+  for (int h = 0; h < 2; ++h) {
+    sq->hiM[h] = hiM[h];
+    sq->loM[h] = loM[h];
+    sq->cst[h] = cst[h];
+  }
+  sq->on = 1;
+  meta[kMetaRehist] = 1;
+  meta[kMetaMode] = 0;
+  meta[kMetaFallback] = 0;
+  meta[kMetaBigCount] = 0;
+}
+
+// sqMode: 0 = plain plan; 1 = float keys, first plan (gathers the bucket
+// occupancy per image half and decides the squeeze, plan_squeeze); 2 = the
+// plan of the squeezed histogram (runs only if the squeeze went on).
 __global__ __launch_bounds__(kPlanRowThreads) void thrs_plan_rows(
     const uint32_t* __restrict__ joint, const uint32_t* __restrict__ rowHist, const uint32_t* __restrict__ segHistA,
     uint32_t n, uint32_t cap, uint32_t* __restrict__ baseTop /* [2][256]: second, top */,
     uint32_t* __restrict__ chunkOff, uint32_t* __restrict__ chunkB0, uint32_t* __restrict__ meta,
     uint32_t* __restrict__ segInfo, uint32_t* __restrict__ segBase, uint32_t tileKeys, uint32_t histGrid,
-    uint32_t* __restrict__ segInfoA, uint32_t* __restrict__ segBaseA, uint32_t* __restrict__ bigB) {
-  __shared__ uint32_t s_w[2][4], s_base, s_b2[kBins];
+    uint32_t* __restrict__ segInfoA, uint32_t* __restrict__ segBaseA, uint32_t* __restrict__ bigB, int sqMode,
+    int keyBits) {
+  if (sqMode == 2 && meta[kMetaRehist] == 0) return;
+  __shared__ uint32_t s_w[2][4], s_base, s_b2[kBins], s_sq[3];
   const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6, r = blockIdx.x;
   // 256-thread exclusive scan (4 waves)
   auto scan256 = [&](uint32_t v, int slot, uint32_t* total) -> uint32_t {
@@ -348,6 +414,30 @@ __global__ __launch_bounds__(kPlanRowThreads) void thrs_plan_rows(
     atomicOr(&meta[kMetaFallback], 1u);
     atomicMax(&meta[kMetaMode], x == n ? 2u : 1u);
     bigB[atomicAdd(&meta[kMetaBigCount], 1u)] = kBins * r + t;
+  }
+  if (sqMode == 1) {  // occupancy of this row's image half; the last workgroup decides
+    if (t == 0) s_sq[0] = s_sq[1] = s_sq[2] = 0;
+    __syncthreads();
+    const uint32_t b = kBins * r + t;
+    if (x) {
+      atomicOr(&s_sq[0], b);
+      atomicOr(&s_sq[1], ~b & 0xFFFFu);
+    }
+    if (x > cap) atomicAdd(&s_sq[2], 1u);
+    __syncthreads();
+    if (t == 0) {
+      const uint32_t h = r >> 7;
+      if (s_sq[0] | s_sq[1]) {
+        atomicOr(&meta[kMetaOr1 + h], s_sq[0]);
+        atomicOr(&meta[kMetaOr0 + h], s_sq[1]);
+      }
+      if (s_sq[2]) atomicAdd(&meta[kMetaBigHalf + h], s_sq[2]);
+      __threadfence();
+      if (atomicAdd(&meta[kMetaPlanDone], 1u) == gridDim.x - 1) {
+        __threadfence();
+        plan_squeeze(meta, keyBits);
+      }
+    }
   }
   if (r != 0) return;
   // second digit: totals over the position segments -> bases, segment bases
@@ -977,8 +1067,8 @@ using Loc16Wide = Loc16G<THRS_WIDE_W, THRS_WIDE_K, 4, THRS_WIDE_K / 2>;
 // give each zero its rank among the zeros and its sign, as bits in the
 // counters' LDS (free after the rounds); the write-out takes the zeros' bit
 // patterns from there and rebuilds every other key.
-template <typename LG>
-__device__ __attribute__((noinline)) void loc16_write_zero_chunk(uint32_t* __restrict__ keys, KeyMap<uint32_t> km,
+template <typename LG, typename KM>
+__device__ __attribute__((noinline)) void loc16_write_zero_chunk(uint32_t* __restrict__ keys, KM km,
                                                                  uint32_t start, uint32_t size, uint32_t hiBits,
                                                                  unsigned char* smem) {
   constexpr int KPT = LG::KPT;
@@ -1030,19 +1120,21 @@ __device__ __attribute__((noinline)) void loc16_write_zero_chunk(uint32_t* __res
 }
 
 template <int KT, bool ATOMIC_RANK, typename LG>
-__global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(LG::WPE))) void thrs_local16(uint32_t* __restrict__ keys, KeyMap<uint32_t> km,
+__global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(LG::WPE))) void thrs_local16(uint32_t* __restrict__ keys, KeyMap<uint32_t> kmh,
                                                             const uint32_t* __restrict__ chunkOff,
                                                             const uint32_t* __restrict__ chunkB0,
                                                             const uint32_t* __restrict__ meta,
-                                                            const uint16_t* __restrict__ lo) {
+                                                            const uint16_t* __restrict__ lo,
+                                                            const SqueezeWords* __restrict__ sq) {
   constexpr int KPT = LG::KPT, NP = LG::NP;
   constexpr uint32_t CHUNK = 64 * KPT;
   const uint32_t c = blockIdx.x;
   if (c >= meta[kMetaChunks]) return;
   const uint32_t start = chunkOff[c], size = chunkOff[c + 1] - start;
   if (size == 0 || size > LG::CAP) return;  // big chunk: the per-bucket fallback sorts it
-  const uint32_t hiBits = chunkB0[c] << 16;  // the bucket: the image's top 16 bits
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  with_map<KT>(kmh, sq, [&](auto km) {
+  const uint32_t hiBits = chunkB0[c] << 16;  // the bucket: the image's top 16 bits
   uint16_t* stage = reinterpret_cast<uint16_t*>(smem);
   uint32_t* s_cnt = reinterpret_cast<uint32_t*>(smem + LG::STAGE_BYTES);  // [waves][256]
   const uint32_t tid = threadIdx.x, lane = tid & 63;
@@ -1196,6 +1288,7 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(LG:
     for (int jj = 0; jj < LB; ++jj)
       if ((h + jj) * 64 < lim) src[(h + jj) * 64] = kinv<KT>(km, hiBits | o[jj]);
   }
+  });
 }
 
 // ------------------------------------------- local sort, counting (keys only)
@@ -1419,7 +1512,8 @@ __global__ __launch_bounds__(LocCount::THREADS) void thrs_local_count16(
 template <int KT, bool ATOMIC_RANK, typename LG>
 __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(4))) void thrs_local_pairs(
     uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, KeyMap<uint32_t> km,
-    const uint32_t* __restrict__ chunkOff, const uint32_t* __restrict__ chunkB0, const uint32_t* __restrict__ meta) {
+    const uint32_t* __restrict__ chunkOff, const uint32_t* __restrict__ chunkB0, const uint32_t* __restrict__ meta,
+    const SqueezeWords* __restrict__ sq) {
   constexpr int KPT = LG::KPT;
   constexpr uint32_t CHUNK = 64 * KPT;
   const uint32_t c = blockIdx.x;
@@ -1444,11 +1538,13 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(4))
   const int32_t avail = __builtin_amdgcn_readfirstlane((int32_t)ch.size - (int32_t)(w * CHUNK));
   uint32_t it[KPT];
   load_run<KPT>(it, keys + ch.start, myOff, ch.size, avail);
+  with_map<KT>(km, sq, [&](auto kmx) {  // (the squeeze, f32 keys: only the items' images depend on it)
 #pragma unroll
-  for (int j = 0; j < KPT; ++j) {
-    const uint32_t pos = myOff + j * 64;
-    it[j] = (j * 64 < lim) ? ((kimg<KT>(km, it[j]) << 16) | pos) : 0xFFFF0000u;  // padding: digits 255
-  }
+    for (int j = 0; j < KPT; ++j) {
+      const uint32_t pos = myOff + j * 64;
+      it[j] = (j * 64 < lim) ? ((kimg<KT>(kmx, it[j]) << 16) | pos) : 0xFFFF0000u;  // padding: digits 255
+    }
+  });
   loc_rounds<0, ATOMIC_RANK, LG>(it, ch, KeyMap<uint32_t>{0u, 0u, 0u}, 16, 2, smem, nullptr);
   pin(reinterpret_cast<uint32_t&>(lim));
   // values of this thread's positions (the item registers are free again;
@@ -1652,10 +1748,11 @@ __device__ __noinline__ void kv8_six_rounds(unsigned char* smem, uint32_t size) 
 template <int KT, int VB, bool ATOMIC_RANK>
 __global__ __launch_bounds__(LocKV::THREADS) void thrs_local_kv(typename KeyTraits<KT>::U* __restrict__ keys,
                                                                 typename ValueWord<VB>::T* __restrict__ vals,
-                                                                KeyMap<typename KeyTraits<KT>::U> km,
+                                                                KeyMap<typename KeyTraits<KT>::U> kmh,
                                                                 const uint32_t* __restrict__ chunkOff,
                                                                 const uint32_t* __restrict__ chunkB0,
-                                                                const uint32_t* __restrict__ meta) {
+                                                                const uint32_t* __restrict__ meta,
+                                                                const SqueezeWords* __restrict__ sq) {
   using U = typename KeyTraits<KT>::U;
   constexpr int KB = (int)sizeof(U);
   using Item = typename std::conditional<KB == 4, uint32_t, uint64_t>::type;
@@ -1667,8 +1764,9 @@ __global__ __launch_bounds__(LocKV::THREADS) void thrs_local_kv(typename KeyTrai
   if (c >= meta[kMetaChunks]) return;
   const uint32_t start = chunkOff[c], size = chunkOff[c + 1] - start;
   if (size == 0 || size > LocKV::CAP) return;  // big chunk: the per-bucket fallback sorts it
-  const U hiImg = (U)chunkB0[c] << (8 * KB - 16);  // the bucket: the image's top 16 bits
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  with_map<KT>(kmh, sq, [&](auto km) {
+  const U hiImg = (U)chunkB0[c] << (8 * KB - 16);  // the bucket: the image's top 16 bits
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t myOff = w * CHUNK + lane;
@@ -1857,6 +1955,7 @@ __global__ __launch_bounds__(LocKV::THREADS) void thrs_local_kv(typename KeyTrai
       if (j * 64 < lim) vdst[j * 64] = make_uint4((uint32_t)o[j], (uint32_t)(o[j] >> 32), (uint32_t)h, (uint32_t)(h >> 32));
     }
   }
+  });
 }
 
 }  // namespace

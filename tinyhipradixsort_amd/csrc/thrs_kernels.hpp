@@ -71,18 +71,78 @@ template <> struct KeyTraits<3> {  // F64
 // so sorting by img is sorting by the key, and the range's keys fill the
 // whole image width (the bucket path's 16-bit buckets stay balanced).
 // Without a range lo = sh = 0.
-template <typename U> struct KeyMap {
+//
+// SQ = true adds a SQUEEZE chosen on the device from the data (float keys on
+// the bucket path, thrs_plan_rows): in each half of the image space (top
+// image bit h) one bit b that every key of that half has at the same value
+// (cst[h]) is dropped and the bits below it move up by one:
+//   img' = (img & hiM[h]) | ((img & loM[h]) << 1),  hiM = ~(2^(b+1) - 1),
+//   loM = 2^b - 1  (identity: hiM = ~0, loM = 0).
+// Monotone and one-to-one on the keys of that half (the dropped bit is the
+// same for all of them) and the top bit stays, so the order is unchanged; the
+// 16-bit buckets then take one more varying bit.  The reference's own float
+// generator clears the lowest exponent bit of every key (unittest.cpp:103,
+// 108), which is such a bit: without the squeeze half the buckets are empty.
+template <typename U, bool SQ = false> struct KeyMap {
   U mask;
   U lo;
   uint32_t sh;
 };
-template <int KT>
-__device__ __forceinline__ typename KeyTraits<KT>::U kimg(const KeyMap<typename KeyTraits<KT>::U>& m,
+template <typename U> struct KeyMap<U, true> {
+  U mask;
+  U lo;
+  uint32_t sh;
+  U hiM[2], loM[2], cst[2];
+};
+// the squeeze as thrs_plan_rows writes it (in the bucket path's meta words)
+struct SqueezeWords {
+  uint32_t on, pad;
+  uint64_t hiM[2], loM[2], cst[2];
+};
+template <int KT> constexpr bool kSqueezable = KT == 2 || KT == 3;  // float keys
+template <typename U> __device__ __forceinline__ KeyMap<U, true> with_squeeze(const KeyMap<U>& m,
+                                                                              const SqueezeWords* s) {
+  KeyMap<U, true> r;
+  r.mask = m.mask;
+  r.lo = m.lo;
+  r.sh = m.sh;
+  for (int h = 0; h < 2; ++h) {
+    r.hiM[h] = (U)s->hiM[h];
+    r.loM[h] = (U)s->loM[h];
+    r.cst[h] = (U)s->cst[h];
+  }
+  return r;
+}
+// body(km) with the host's map, or with the device-chosen squeeze when
+// thrs_plan_rows switched it on (float keys only: compiled out otherwise)
+template <int KT, typename F>
+__device__ __forceinline__ void with_map(const KeyMap<typename KeyTraits<KT>::U>& km, const SqueezeWords* sq,
+                                         F&& body) {
+  if constexpr (kSqueezable<KT>) {
+    if (sq && sq->on) {
+      body(with_squeeze(km, sq));
+      return;
+    }
+  }
+  body(km);
+}
+template <int KT, bool SQ>
+__device__ __forceinline__ typename KeyTraits<KT>::U kimg(const KeyMap<typename KeyTraits<KT>::U, SQ>& m,
                                                           typename KeyTraits<KT>::U k) {
-  return ((KeyTraits<KT>::bits(k) ^ m.mask) - m.lo) << m.sh;
+  using U = typename KeyTraits<KT>::U;
+  U y = ((KeyTraits<KT>::bits(k) ^ m.mask) - m.lo) << m.sh;
+  if constexpr (SQ) {
+    const bool h = (y >> (8 * sizeof(U) - 1)) != 0;
+    y = (y & (h ? m.hiM[1] : m.hiM[0])) | ((y & (h ? m.loM[1] : m.loM[0])) << 1);
+  }
+  return y;
 }
 // the key whose image is y (u32 / u64: getKeyBits is the identity)
-template <typename U> __device__ __forceinline__ U kinv_int(const KeyMap<U>& m, U y) {
+template <typename U, bool SQ> __device__ __forceinline__ U kinv_int(const KeyMap<U, SQ>& m, U y) {
+  if constexpr (SQ) {
+    const bool h = (y >> (8 * sizeof(U) - 1)) != 0;
+    y = (y & (h ? m.hiM[1] : m.hiM[0])) | ((y >> 1) & (h ? m.loM[1] : m.loM[0])) | (h ? m.cst[1] : m.cst[0]);
+  }
   return ((y >> m.sh) + m.lo) ^ m.mask;
 }
 // raw 4-byte key whose getKeyBits image is y (inverse of KeyTraits::bits, for
@@ -92,7 +152,7 @@ template <int KT> __device__ __forceinline__ uint32_t unbits32(uint32_t y) {
   else return y;
 }
 // the 4-byte key whose image (under m) is y
-template <int KT> __device__ __forceinline__ uint32_t kinv(const KeyMap<uint32_t>& m, uint32_t y) {
+template <int KT, bool SQ> __device__ __forceinline__ uint32_t kinv(const KeyMap<uint32_t, SQ>& m, uint32_t y) {
   return unbits32<KT>(kinv_int(m, y));
 }
 
@@ -804,11 +864,12 @@ struct NoMid {
 
 // GROUPED = false: the flat per-tile look-back (the per-bucket fallback,
 // whose chains may be shorter than a group; thrs_fallback.hpp).
-template <int KT, int VB, typename ST, bool ATOMIC_RANK, typename Mid, int CODEC = kCodecKeys, bool GROUPED = true>
+template <int KT, int VB, typename ST, bool ATOMIC_RANK, typename Mid, int CODEC = kCodecKeys, bool GROUPED = true,
+          typename KM>
 __device__ __forceinline__ void pass_tile(
     const typename KeyTraits<KT>::U* __restrict__ keysIn, typename KeyTraits<KT>::U* __restrict__ keysOut,
     const typename ValueWord<VB>::T* __restrict__ valsIn, typename ValueWord<VB>::T* __restrict__ valsOut,
-    uint64_t keyStart, uint32_t valid, KeyMap<typename KeyTraits<KT>::U> km, int shift, uint32_t myBase,
+    uint64_t keyStart, uint32_t valid, KM km, int shift, uint32_t myBase,
     uint32_t outEnd, ST* __restrict__ status, ST* __restrict__ statusNext, uint32_t* __restrict__ errFlag, uint32_t tile,
     uint32_t chainStart, const GroupTables<ST>& grp, unsigned char* smem, uint64_t* __restrict__ stamps,
     typename KeyTraits<KT>::U (&k)[PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::KPT],
@@ -1366,7 +1427,7 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
     KeyMap<typename KeyTraits<KT>::U> km, int shift, uint32_t* __restrict__ segInfo,
     const uint32_t* __restrict__ segBase, ST* __restrict__ status, uint32_t* __restrict__ errFlag,
     GroupTables<ST> grp, const uint32_t* __restrict__ gate, uint32_t gateMask, uint8_t* __restrict__ hiPlane,
-    uint64_t* __restrict__ stamps) {
+    uint64_t* __restrict__ stamps, const SqueezeWords* __restrict__ sq) {
   using U = typename KeyTraits<KT>::U;
   using VW = typename ValueWord<VB>::T;
   using G = PassGeom<sizeof(U), VB>;
@@ -1381,6 +1442,7 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
   if (tid < 2 * (kSegs + 1)) (tid <= (uint32_t)kSegs ? segPos[tid] : segTiles[tid - kSegs - 1]) = segInfo[tid];
   __syncthreads();
   const uint32_t home = xcc_id() & (kSegs - 1);
+  with_map<KT>(km, sq, [&](auto kmx) {
   uint32_t done = 0;  // thread 0: segments found exhausted
   U k[G::KPT];
   VW v[VB ? G::KPT : 1];
@@ -1426,11 +1488,12 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
     g.gpNext = nullptr;
     const uint32_t myBase = segBase[seg * kBins + (tid & 255u)];
     load_tile<KT, VB, CODEC>(keysIn, valsIn, keyStart, valid, k, v, hiPlane);
-    pass_tile<KT, VB, ST, ATOMIC_RANK, NoMid, CODEC>(keysIn, keysOut, valsIn, valsOut, keyStart, valid, km,
+    pass_tile<KT, VB, ST, ATOMIC_RANK, NoMid, CODEC>(keysIn, keysOut, valsIn, valsOut, keyStart, valid, kmx,
                                                      shift, myBase, segPos[kSegs], status, nullptr, errFlag, chain + t, chain, g, smem,
                                                      stamps, k, v, NoMid{}, hiPlane);
     lds_barrier();  // stage, s_gofs and s_misc are reused by the next tile
   }
+  });
 }
 
 // Zeroing of up to three 16-byte-aligned ranges in one launch (the scratch
