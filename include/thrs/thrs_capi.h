@@ -28,7 +28,7 @@ extern "C" {
 typedef struct ihipStream_t* hipStream_t; /* identical to HIP's own typedef */
 #endif
 
-#define THRS_ABI_VERSION 3
+#define THRS_ABI_VERSION 4
 
 typedef enum thrs_status {
   THRS_SUCCESS = 0,
@@ -173,6 +173,19 @@ int thrs_partition_pass(const thrs_config* config, const void* keysIn, const voi
  * needs no particular alignment (any sub-range of a key buffer). */
 int thrs_digit_histogram(const thrs_config* config, const void* keys, uint32_t numberOfInputs, uint64_t prefixMask,
                          uint64_t prefixValue, int bitLocation, uint32_t* counts, hipStream_t stream);
+/* The same for nTargets key ranges of one buffer at once (one memset and one
+ * launch per 16 ranges: every boundary still being refined at one level of
+ * the multi-GPU split): counts[i][256] for keys[offset_i, offset_i + count_i)
+ * with prefix (prefixMask_i, prefixValue_i).  targets is a host array. */
+typedef struct thrs_hist_target {
+  uint64_t offset;       /* first key of the range (keys, not bytes) */
+  uint32_t count;        /* keys in the range                        */
+  uint32_t reserved;     /* zero                                     */
+  uint64_t prefixMask;
+  uint64_t prefixValue;
+} thrs_hist_target;
+int thrs_digit_histogram_batch(const thrs_config* config, const void* keys, const thrs_hist_target* targets,
+                               int nTargets, int bitLocation, uint32_t* counts, hipStream_t stream);
 
 /* Device-side failures (no reference counterpart; the reference would hang
  * where these give up).  A look-back or tile-claim wait is bounded; when the

@@ -42,12 +42,15 @@ class OracleOps:
             pv = torch.from_numpy(np.ascontiguousarray(vals.numpy().reshape(n, self.vb)[order]).reshape(-1).copy())
         return pk, pv, torch.from_numpy(np.bincount(d, minlength=256).astype(np.int32))
 
-    def histogram(self, keys, n, mask, value, bit):
-        k = keys.numpy().view(self.dt)[:n]
-        t = O.key_bits_np(self.kt, k, self.desc)
-        sel = (t & np.uint64(mask)) == np.uint64(value)
-        d = ((t[sel] >> np.uint64(bit)) & np.uint64(0xFF)).astype(np.int64)
-        return torch.from_numpy(np.bincount(d, minlength=256).astype(np.int32))
+    def histograms(self, keys, ranges, bit):
+        allk = keys.numpy().view(self.dt)
+        out = []
+        for lo, n, mask, value in ranges:
+            t = O.key_bits_np(self.kt, allk[lo:lo + n], self.desc)
+            sel = (t & np.uint64(mask)) == np.uint64(value)
+            d = ((t[sel] >> np.uint64(bit)) & np.uint64(0xFF)).astype(np.int64)
+            out.append(np.bincount(d, minlength=256).astype(np.int32))
+        return torch.from_numpy(np.stack(out))
 
     def sort(self, keys, vals, n, s, e, finish=True, key_range=None):
         if n == 0:

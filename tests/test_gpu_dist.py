@@ -156,6 +156,41 @@ def test_digit_histogram_vs_numpy(gpu, kt, desc):
         assert np.array_equal(h.cpu().numpy().astype(np.int64), exp), (mask, value, bit)
 
 
+@pytest.mark.parametrize("kt,desc", [(O.U32, False), (O.F64, True)])
+def test_digit_histogram_batch_vs_numpy(gpu, kt, desc):
+    """thrs_digit_histogram_batch: several ranges of one buffer (unaligned,
+    overlapping, empty, and more than one launch's 16) with their own prefixes
+    in one call -- a whole refinement level of the multi-GPU split."""
+    import tinyhipradixsort_amd as T
+    torch = gpu
+    n = 300007
+    k = O.randomize_np(kt, O.splitmix64_stream(43, n))
+    kb = O.KEY_BYTES[kt]
+    k[::3] &= np.array(0xFF00FFFF if kb == 4 else 0xFF00FFFFFFFFFFFF, k.dtype)
+    cfg = T.RadixSort.Config(keyType=T.KeyType(kt), sortOrder=T.SortOrder.Descending if desc else T.SortOrder.Ascending)
+    rs = T.RadixSort([], cfg)
+    kd = torch.from_numpy(k.view(np.uint8).copy()).cuda()
+    t = O.key_bits_np(kt, k, desc)
+    top = 0xFF << (kb * 8 - 8)
+    rng = np.random.default_rng(5)
+    ranges = []
+    for i in range(19):
+        lo = int(rng.integers(0, n - 1))
+        cnt = 0 if i == 4 else int(rng.integers(1, n - lo))
+        mask = 0 if i % 3 == 0 else top
+        ranges.append((lo, cnt, mask, int(t[lo]) & mask if cnt else 0))
+    bit = kb * 8 - 16
+    h = torch.empty((len(ranges), 256), dtype=torch.int32, device="cuda")
+    rs.digitHistograms(kd, ranges, bit, h)
+    torch.cuda.synchronize()
+    got = h.cpu().numpy().astype(np.int64)
+    for i, (lo, cnt, mask, value) in enumerate(ranges):
+        tt = t[lo:lo + cnt]
+        sel = (tt & np.uint64(mask)) == np.uint64(value)
+        exp = np.bincount(((tt[sel] >> np.uint64(bit)) & np.uint64(0xFF)).astype(np.int64), minlength=256)
+        assert np.array_equal(got[i], exp), i
+
+
 def test_bench_force_dist_runs_rccl_at_world_1(gpu):
     """bench.py --force-dist: the bucket exchange through the nccl (= RCCL)
     backend at world size 1 -- the code path of the N-GPU bench lines."""

@@ -120,3 +120,79 @@ def test_normal_library_reports_nothing():
 def test_first_sort_under_stream_capture():
     res = _run(CAPTURE.format(root=ROOT))
     assert res == {"graph": True, "after": True}, res
+
+
+BUCKET = r"""
+import sys, torch
+sys.path.insert(0, {root!r})
+import tinyhipradixsort_amd as T
+from tinyhipradixsort_amd import testutil as TU
+T.LIB_PATH = {lib!r}
+torch.cuda.set_device(0)
+GUARD = 1 << 20
+def guarded(nbytes):
+    buf = torch.full((nbytes + 2 * GUARD,), 0xA5, dtype=torch.uint8, device="cuda")
+    return buf, buf[GUARD:GUARD + nbytes]
+def guards_ok(buf):
+    return bool((buf[:GUARD] == 0xA5).all().item()) and bool((buf[-GUARD:] == 0xA5).all().item())
+res = dict(failed=0, reported=0, guards_ok=0, other_ok=0, sorts=0)
+for kt, vb, dist in ((0, 0, "uniform"), (0, 0, "fewuniq"), (0, 4, "uniform"), (0, 4, "fewuniq"), (1, 8, "uniform"),
+                     (1, 8, "fewuniq"), (2, 4, "uniform")):
+    cfg = T.RadixSort.Config(keyType=T.KeyType(kt), valueType={{0: T.ValueType.U32, 4: T.ValueType.U32,
+                                                                 8: T.ValueType.U64}}[vb])
+    rs = T.RadixSort([], cfg, T.Options(path="bucket"))
+    n = 1 << 24
+    kb = 8 if kt in (1, 3) else 4
+    d = rs.getTemporaryBufferBytes(n)
+    tbytes = d.getTemporaryBufferBytesForSortPairs() if vb else d.getTemporaryBufferBytesForSortKeys()
+    kbuf, keys = guarded(kb * n)
+    tbuf, tmp = guarded(tbytes)
+    vbuf, vals = guarded(max(1, vb * n))
+    if dist == "uniform":
+        TU.fill_keys(kt, keys, n, start=7 * n)
+    else:
+        TU.fill_dist(kt, keys, n, dist)                 # few distinct keys: big chunks, the per-bucket fallback
+    if vb:
+        TU.iota(vb, vals, n)
+    torch.cuda.synchronize()
+    res["sorts"] += 1
+    try:
+        if vb:
+            rs.sortPairs(keys, vals, n, tmp, 0, 8 * kb, checked=True)
+        else:
+            rs.sortKeys(keys, n, tmp, 0, 8 * kb, checked=True)
+    except T.ThrsError as e:
+        res["failed"] += 1
+        res["reported"] += e.status == -5
+    torch.cuda.synchronize()
+    res["guards_ok"] += guards_ok(kbuf) and guards_ok(tbuf) and guards_ok(vbuf)
+    try:
+        T.take_device_error()
+    except T.ThrsError:
+        pass
+m = 1000
+small = torch.empty(4 * m, dtype=torch.uint8, device="cuda")
+rs = T.RadixSort([], T.RadixSort.Config())
+tmp2 = torch.empty(rs.getTemporaryBufferBytes(m).getTemporaryBufferBytesForSortKeys(), dtype=torch.uint8, device="cuda")
+TU.fill_keys(0, small, m, start=3)
+rs.sortKeys(small, m, tmp2, 0, 32, checked=True)
+res["other_ok"] = TU.count_unsorted(0, small, m, 0, 32) == 0
+print(res)
+"""
+
+
+def test_forced_timeout_on_the_bucket_path_stays_in_bounds():
+    """the bucket path with every look-back giving up at
+    once (libthrs_spin0.so): the segmented top-digit passes, the local sorts
+    and -- for few-distinct-key inputs -- the per-bucket fallback's passes
+    (thrs_pass_big) and copy-back (thrs_big_copy).  Every failing sort is
+    reported to its caller, nothing outside the keys, values and temporary
+    buffer is written (1 MiB canary bands on both sides of each, checked
+    after every sort), and an unrelated sort afterwards succeeds."""
+    lib = os.path.join(ROOT, "tinyhipradixsort_amd", "libthrs_spin0.so")
+    assert os.path.exists(lib), "build it first (make)"
+    res = _run(BUCKET.format(root=ROOT, lib=lib))
+    print(res)
+    assert res["sorts"] == 7 and res["guards_ok"] == 7, res
+    assert res["failed"] >= 1 and res["reported"] == res["failed"], res
+    assert res["other_ok"], res

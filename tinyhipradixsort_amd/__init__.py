@@ -31,7 +31,7 @@ from dataclasses import dataclass
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libthrs.so")
 TESTUTIL_PATH = os.path.join(_HERE, "libthrs_testutil.so")
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 __all__ = ["KeyType", "ValueType", "SortOrder", "bytesOf", "div_round_up64", "next_multiple64", "Buffer",
            "RadixSort", "Options", "ThrsError", "lib", "LIB_PATH", "take_device_error"]
@@ -71,6 +71,9 @@ def lib() -> ctypes.CDLL:
         L.thrs_take_device_error.restype = i32
         L.thrs_digit_histogram.argtypes = [ctypes.POINTER(_CConfig), vp, u32, u64, u64, i32, vp, vp]
         L.thrs_digit_histogram.restype = i32
+        L.thrs_digit_histogram_batch.argtypes = [ctypes.POINTER(_CConfig), vp, ctypes.POINTER(_CHistTarget), i32, i32,
+                                                 vp, vp]
+        L.thrs_digit_histogram_batch.restype = i32
         L.thrs_check_device_error.argtypes = [vp, vp]
         L.thrs_accumulate_device_error.argtypes = [vp, vp, vp]
         L.thrs_partition_pass.argtypes = [ctypes.POINTER(_CConfig), vp, vp, u32, vp, vp, vp, i32, vp, vp]
@@ -173,6 +176,11 @@ def take_device_error():
 class _CPathInfo(ctypes.Structure):
     _fields_ = [("path", ctypes.c_int32), ("local", ctypes.c_int32), ("planes", ctypes.c_int32),
                 ("devicePasses", ctypes.c_int32), ("minBytes", ctypes.c_uint64), ("localCap", ctypes.c_uint64)]
+
+
+class _CHistTarget(ctypes.Structure):
+    _fields_ = [("offset", ctypes.c_uint64), ("count", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
+                ("prefixMask", ctypes.c_uint64), ("prefixValue", ctypes.c_uint64)]
 
 
 class _CTempDef(ctypes.Structure):
@@ -396,6 +404,18 @@ class RadixSort:
         _check(lib().thrs_digit_histogram(ctypes.byref(self._c()), _ptr(inputKeyBuffer), _n(numberOfInputs),
                                           int(prefixMask) & (2**64 - 1), int(prefixValue) & (2**64 - 1),
                                           int(bitLocation), _ptr(counts), _stream(stream)))
+
+    def digitHistograms(self, inputKeyBuffer, targets, bitLocation: int, counts, stream=None):
+        """counts[i] (device u32[len(targets)][256], zeroed first) = the
+        digitHistogram of keys [offset, offset + count) with prefix (mask,
+        value), for every (offset, count, mask, value) in targets, in one
+        launch (thrs_digit_histogram_batch: a refinement level of the
+        multi-GPU split)."""
+        arr = (_CHistTarget * max(1, len(targets)))()
+        for i, (off, cnt, mask, value) in enumerate(targets):
+            arr[i] = _CHistTarget(int(off), _n(cnt), 0, int(mask) & (2**64 - 1), int(value) & (2**64 - 1))
+        _check(lib().thrs_digit_histogram_batch(ctypes.byref(self._c()), _ptr(inputKeyBuffer), arr, len(targets),
+                                                int(bitLocation), _ptr(counts), _stream(stream)))
 
     def pathInfo(self, numberOfInputs: int, startBits: int, endBits: int, pairs: bool) -> dict:
         """The path such a sort takes and the HBM bytes it moves when no bucket

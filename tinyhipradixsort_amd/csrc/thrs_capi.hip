@@ -305,28 +305,53 @@ THRS_API int thrs_partition_pass(const thrs_config* config, const void* keysIn, 
   return partition_impl(config, keysIn, valuesIn, n, tmp, keysOut, valuesOut, bitLocation, counts, stream);
 }
 
-THRS_API int thrs_digit_histogram(const thrs_config* config, const void* keys, uint32_t n, uint64_t prefixMask,
-                                  uint64_t prefixValue, int bitLocation, uint32_t* counts, hipStream_t stream) {
-  if (!config || !valid_key(config->keyType) || !counts) return THRS_ERROR_INVALID_VALUE;
+THRS_API int thrs_digit_histogram_batch(const thrs_config* config, const void* keys, const thrs_hist_target* targets,
+                                        int nTargets, int bitLocation, uint32_t* counts, hipStream_t stream) {
+  if (!config || !valid_key(config->keyType) || nTargets < 0 || (nTargets && (!targets || !counts)))
+    return THRS_ERROR_INVALID_VALUE;
   if (config->sortOrder != THRS_ORDER_ASCENDING && config->sortOrder != THRS_ORDER_DESCENDING)
     return THRS_ERROR_INVALID_VALUE;
   const int kb = key_bytes_of(config->keyType);
   if (bitLocation < 0 || bitLocation + 8 > kb * 8) return THRS_ERROR_INVALID_VALUE;
-  if (n && !keys) return THRS_ERROR_INVALID_VALUE;
-  if (hipMemsetAsync(counts, 0, kBins * sizeof(uint32_t), stream) != hipSuccess) return THRS_ERROR_HIP;
-  if (n == 0) return THRS_SUCCESS;
+  uint64_t most = 0;
+  for (int i = 0; i < nTargets; ++i) {
+    if (targets[i].count && !keys) return THRS_ERROR_INVALID_VALUE;
+    most = std::max<uint64_t>(most, targets[i].count);
+  }
+  if (nTargets == 0) return THRS_SUCCESS;
+  if (hipMemsetAsync(counts, 0, (size_t)nTargets * kBins * sizeof(uint32_t), stream) != hipSuccess)
+    return THRS_ERROR_HIP;
+  if (most == 0) return THRS_SUCCESS;
   const bool desc = config->sortOrder == THRS_ORDER_DESCENDING;
-  const uint64_t want = ((uint64_t)n + kHistThreads * 8 - 1) / (kHistThreads * 8);
+  const uint64_t want = (most + kHistThreads * 8 - 1) / (kHistThreads * 8);
   const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cu_count()));
-  if (kb == 4)
-    hipLaunchKernelGGL(thrs_digit_hist_u32, dim3(grid), dim3(kHistThreads), 0, stream,
-                       static_cast<const uint32_t*>(keys), n, config->keyType, desc ? 0xFFFFFFFFu : 0u,
-                       (uint32_t)prefixMask, (uint32_t)prefixValue, bitLocation, counts);
-  else
-    hipLaunchKernelGGL(thrs_digit_hist_u64, dim3(grid), dim3(kHistThreads), 0, stream,
-                       static_cast<const uint64_t*>(keys), n, config->keyType, desc ? ~0ull : 0ull, prefixMask,
-                       prefixValue, bitLocation, counts);
+  for (int t0 = 0; t0 < nTargets; t0 += kMaxHistTargets) {  // one launch per kMaxHistTargets ranges
+    const int cnt = std::min(kMaxHistTargets, nTargets - t0);
+    HistTargets tg{};
+    for (int i = 0; i < cnt; ++i) {
+      tg.off[i] = targets[t0 + i].offset;
+      tg.n[i] = targets[t0 + i].count;
+      tg.mask[i] = targets[t0 + i].prefixMask;
+      tg.value[i] = targets[t0 + i].prefixValue;
+    }
+    uint32_t* out = counts + (uint64_t)t0 * kBins;
+    if (kb == 4)
+      hipLaunchKernelGGL(thrs_digit_hist<uint32_t>, dim3(grid, cnt), dim3(kHistThreads), 0, stream,
+                         static_cast<const uint32_t*>(keys), tg, config->keyType, desc ? 0xFFFFFFFFu : 0u, bitLocation,
+                         out);
+    else
+      hipLaunchKernelGGL(thrs_digit_hist<uint64_t>, dim3(grid, cnt), dim3(kHistThreads), 0, stream,
+                         static_cast<const uint64_t*>(keys), tg, config->keyType, desc ? ~0ull : 0ull, bitLocation,
+                         out);
+  }
   return hipGetLastError() == hipSuccess ? THRS_SUCCESS : THRS_ERROR_HIP;
+}
+
+THRS_API int thrs_digit_histogram(const thrs_config* config, const void* keys, uint32_t n, uint64_t prefixMask,
+                                  uint64_t prefixValue, int bitLocation, uint32_t* counts, hipStream_t stream) {
+  if (!counts) return THRS_ERROR_INVALID_VALUE;
+  const thrs_hist_target t{0, n, 0, prefixMask, prefixValue};
+  return thrs_digit_histogram_batch(config, keys, &t, 1, bitLocation, counts, stream);
 }
 
 THRS_API int thrs_debug_bucket_mode(const void* tmp, int keyType, int valueBytes, uint32_t n, hipStream_t stream,

@@ -439,56 +439,49 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist(const typename KeyTrai
   }
 }
 
-// Digit histogram of the keys matching a prefix (multi-GPU split refinement,
-// tinyhipradixsort_amd/dist.py): counts[d] += #keys whose transformed key t
-// has (t & prefixMask) == prefixValue and digit d at bit `shift`.  One read,
-// any alignment; LDS bins in 32 bank-private copies (conflict-free whatever the
-// skew), merged with one device atomic per bin and workgroup.
-__global__ __launch_bounds__(kHistThreads) void thrs_digit_hist_u32(const uint32_t* __restrict__ keys, uint32_t n,
-                                                                    int keyType, uint32_t orderMask,
-                                                                    uint32_t prefixMask, uint32_t prefixValue,
-                                                                    int shift, uint32_t* __restrict__ counts) {
+// Digit histograms of the keys matching a prefix, for up to
+// kMaxHistTargets key ranges at once (multi-GPU split refinement: one launch
+// per level for every boundary still being refined,
+// tinyhipradixsort_amd/dist.py): counts[y][d] += #keys of range y whose
+// transformed key t has (t & mask[y]) == value[y] and digit d at bit `shift`.
+// blockIdx.y = the range.  One read, any alignment; LDS bins in 32
+// bank-private copies (conflict-free whatever the skew), merged with one
+// device atomic per bin and workgroup.
+constexpr int kMaxHistTargets = 16;
+struct HistTargets {
+  uint64_t off[kMaxHistTargets];
+  uint64_t mask[kMaxHistTargets];
+  uint64_t value[kMaxHistTargets];
+  uint32_t n[kMaxHistTargets];
+};
+template <typename U>
+__global__ __launch_bounds__(kHistThreads) void thrs_digit_hist(const U* __restrict__ keys, HistTargets tg,
+                                                                int keyType, U orderMask, int shift,
+                                                                uint32_t* __restrict__ counts) {
   __shared__ uint32_t s_h[kBins * 32];
-  const uint32_t tid = threadIdx.x;
+  const uint32_t tid = threadIdx.x, y = blockIdx.y;
+  const U* kk = keys + tg.off[y];
+  const uint32_t n = tg.n[y];
+  const U prefixMask = (U)tg.mask[y], prefixValue = (U)tg.value[y];
   for (uint32_t i = tid; i < kBins * 32; i += kHistThreads) s_h[i] = 0;
   __syncthreads();
   uint32_t* my = s_h + (tid & 31);
   for (uint64_t i = (uint64_t)blockIdx.x * kHistThreads + tid; i < n; i += (uint64_t)gridDim.x * kHistThreads) {
-    const uint32_t k = keys[i];
-    const uint32_t t = (keyType == 2 ? KeyTraits<2>::bits(k) : k) ^ orderMask;
-    if ((t & prefixMask) == prefixValue)
-      __hip_atomic_fetch_add(&my[((t >> shift) & 0xFFu) * 32], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  }
-  __syncthreads();
-  for (uint32_t b = tid; b < (uint32_t)kBins; b += kHistThreads) {
-    uint32_t c = 0;
-#pragma unroll
-    for (int j = 0; j < 32; ++j) c += s_h[b * 32 + ((j + b) & 31)];
-    if (c) atomicAdd(&counts[b], c);
-  }
-}
-__global__ __launch_bounds__(kHistThreads) void thrs_digit_hist_u64(const uint64_t* __restrict__ keys, uint32_t n,
-                                                                    int keyType, uint64_t orderMask,
-                                                                    uint64_t prefixMask, uint64_t prefixValue,
-                                                                    int shift, uint32_t* __restrict__ counts) {
-  __shared__ uint32_t s_h[kBins * 32];
-  const uint32_t tid = threadIdx.x;
-  for (uint32_t i = tid; i < kBins * 32; i += kHistThreads) s_h[i] = 0;
-  __syncthreads();
-  uint32_t* my = s_h + (tid & 31);
-  for (uint64_t i = (uint64_t)blockIdx.x * kHistThreads + tid; i < n; i += (uint64_t)gridDim.x * kHistThreads) {
-    const uint64_t k = keys[i];
-    const uint64_t t = (keyType == 3 ? KeyTraits<3>::bits(k) : k) ^ orderMask;
+    const U k = kk[i];
+    U t;
+    if constexpr (sizeof(U) == 4) t = (keyType == 2 ? KeyTraits<2>::bits(k) : k) ^ orderMask;
+    else t = (keyType == 3 ? KeyTraits<3>::bits(k) : k) ^ orderMask;
     if ((t & prefixMask) == prefixValue)
       __hip_atomic_fetch_add(&my[(uint32_t)((t >> shift) & 0xFFu) * 32], 1u, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_WORKGROUP);
   }
   __syncthreads();
+  uint32_t* out = counts + (uint64_t)y * kBins;
   for (uint32_t b = tid; b < (uint32_t)kBins; b += kHistThreads) {
     uint32_t c = 0;
 #pragma unroll
     for (int j = 0; j < 32; ++j) c += s_h[b * 32 + ((j + b) & 31)];
-    if (c) atomicAdd(&counts[b], c);
+    if (c) atomicAdd(&out[b], c);
   }
 }
 

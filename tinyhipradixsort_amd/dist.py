@@ -17,8 +17,9 @@ One sort:
                 needs host split sizes).
   3. split      target g = floor(gN/G) falls in some top-digit bucket b_g at
                 offset o_g.  If o_g > 0 the boundary is refined digit by digit
-                (thrs_digit_histogram of the keys of b_g matching the digits
-                fixed so far, all_gather, pick the digit that holds o_g) until
+                (thrs_digit_histogram_batch: the keys of every b_g still being
+                refined, matching the digits fixed so far, in one launch; one
+                all_gather per level; pick the digit that holds o_g) until
                 the full sort key v_g is known; the keys equal to v_g are then
                 split in global (source rank, source position) order.  Every
                 rank computes every rank's cut points from the gathered counts.
@@ -233,11 +234,13 @@ class HipLocalOps:
         self._note(tmp)
         return pk, pv, counts
 
-    def histogram(self, keys, n: int, mask: int, value: int, bit: int):
-        """device int32[256]: digit histogram of the keys matching the prefix."""
+    def histograms(self, keys, ranges, bit: int):
+        """device int32[len(ranges)][256]: for each (first key, count, mask,
+        value) range, the digit histogram of its keys matching the prefix --
+        one launch for the whole refinement level."""
         import torch
-        h = torch.empty(BINS, dtype=torch.int32, device=keys.device)
-        self.rs.digitHistogram(keys, n, mask, value, bit, h)
+        h = torch.empty((len(ranges), BINS), dtype=torch.int32, device=keys.device)
+        self.rs.digitHistograms(keys, ranges, bit, h)
         return h
 
     def sort(self, keys, vals, n: int, start_bits: int, end_bits: int, finish: bool = True, key_range=None):
@@ -374,11 +377,8 @@ class DistributedRadixSort:
             active = [t for t in targets if t.refining]
             if not active:
                 break
-            hs = []
-            for t in active:
-                lo, cnt = int(off[t.bucket]), int(mine[t.bucket])
-                hs.append(self.ops.histogram(pk[lo * kb:(lo + cnt) * kb], cnt, t.mask, t.value, loc))
-            refine(targets, self._gather(torch.stack(hs)), loc)
+            ranges = [(int(off[t.bucket]), int(mine[t.bucket]), t.mask, t.value) for t in active]
+            refine(targets, self._gather(self.ops.histograms(pk, ranges, loc)), loc)
         # buckets holding a refined boundary: stable local sort, so each cut is one position
         if len(locs) > 1:
             for b in sorted({t.bucket for t in targets if t.inside}):
