@@ -58,6 +58,9 @@ WORKLOADS = {
     "k64v128": (1, 16, 1 << 29, "uniform", "sortPairs u64 key + 16-B payload (K64V128), N=2^29"),
     "k32v64": (0, 8, 1 << 30, "uniform", "sortPairs u32 key + u64 payload, N=2^30"),
     "kf32v32": (2, 4, 1 << 30, "uniform", "sortPairs f32 key + u32 payload, N=2^30"),
+    # the reference's float generator (randomizeValues clears the lowest exponent bit, unittest.cpp:103/108)
+    "f32k": (2, 0, 1 << 30, "uniform", "sortKeys f32, N=2^30 (bits & 0xFF7FFFFF)"),
+    "kf64v64": (3, 8, 1 << 29, "uniform", "sortPairs f64 key (bits & 0xFFEFFFFFFFFFFFFF) + u64 payload, N=2^29"),
     # the reference's own bench size: OrochiRadixSort.bench / benchKeyPair sort 160,000,000 u32 keys
     # (unittest.cpp:490-494, 574-578)
     "ref160m": (0, 0, 160_000_000, "uniform", "OrochiRadixSort.bench: sortKeys u32, N=160,000,000 (unittest.cpp:490-571)"),

@@ -11,10 +11,12 @@
 // gated on meta[kMetaFallback] (written by the plan): no host
 // synchronisation, and ~5 us per launch when nothing overflowed.
 //
-//   thrs_big_plan   workgroup 0: prefix of the big chunks' sizes (bigPos,
-//                   positions in the concatenation of the big chunks) and of
-//                   their tile counts (bigTile); all: zero the big chunks'
-//                   digit counts and the fallback's look-back tables
+//   (plan)          the plan's last workgroup (thrs_plan_rows; thrs_big_plan
+//                   after thrs_plan's multi-bucket chunks): prefix of the big
+//                   chunks' sizes (bigPos, positions in the concatenation of
+//                   the big chunks) and of their tile counts (bigTile); their
+//                   digit counts zeroed as they are listed; the fallback's
+//                   look-back tables zeroed by thrs_big_hist
 //   thrs_big_hist   persistent: counts every low digit of every
 //                   big chunk (bigHist[chunk][pass][256]); the last workgroup
 //                   decides per low pass whether it RUNS -- a pass whose
@@ -112,9 +114,15 @@ template <int KT>
 __global__ __launch_bounds__(kHistThreads) void thrs_big_hist(
     const typename KeyTraits<KT>::U* __restrict__ keys, KeyMap<typename KeyTraits<KT>::U> kmh, int startBits, int nLow,
     const uint32_t* __restrict__ chunkOff, uint32_t* __restrict__ meta, const uint32_t* __restrict__ bigB,
-    const uint32_t* __restrict__ bigPos, uint32_t* __restrict__ bigHist, const SqueezeWords* __restrict__ sq) {
+    const uint32_t* __restrict__ bigPos, uint32_t* __restrict__ bigHist, const SqueezeWords* __restrict__ sq,
+    uint4* __restrict__ tables, uint64_t tableWords) {
   using U = typename KeyTraits<KT>::U;
   if (meta[kMetaFallback] == 0) return;
+  {  // (plan_rows paths) the fallback passes' look-back tables: read from the first pass on
+    const uint64_t gstride = (uint64_t)gridDim.x * kHistThreads, g0 = (uint64_t)blockIdx.x * kHistThreads + threadIdx.x;
+    if (tables)
+      for (uint64_t i = g0; i < tableWords; i += gstride) tables[i] = make_uint4(0, 0, 0, 0);
+  }
   extern __shared__ __attribute__((aligned(16))) uint32_t s_h[];  // [nLow][256][kBigCopies]
   __shared__ uint32_t s_last;
   const uint32_t tid = threadIdx.x, G = gridDim.x;
@@ -253,14 +261,21 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
 }
 
 // An odd number of running low passes left the big chunks in the temporary
-// buffer: copy them back (values too).
+// buffer: copy them back (values too).  The last launch of every bucket-path
+// sort, so it also publishes the sort's error word to the sticky word (the
+// LSD path's thrs_err_publish), whether or not it has anything to copy.
 template <typename U, typename VW>
 __global__ __launch_bounds__(256) void thrs_big_copy(U* __restrict__ keys, const U* __restrict__ tmpKeys,
                                                      VW* __restrict__ vals, const VW* __restrict__ tmpVals,
                                                      const uint32_t* __restrict__ chunkOff,
                                                      const uint32_t* __restrict__ meta,
                                                      const uint32_t* __restrict__ bigB,
-                                                     const uint32_t* __restrict__ bigPos) {
+                                                     const uint32_t* __restrict__ bigPos,
+                                                     const uint32_t* __restrict__ err, uint32_t* __restrict__ sticky) {
+  if (sticky && blockIdx.x == 0 && threadIdx.x == 0) {
+    const uint32_t e = *err;
+    if (e) __hip_atomic_fetch_or(sticky, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   if (meta[kMetaFallback] == 0 || meta[kMetaBigCopy] == 0) return;
   const uint32_t M = meta[kMetaBigCount], total = bigPos[M];
   const uint32_t G = gridDim.x, len = (total + G - 1) / G;

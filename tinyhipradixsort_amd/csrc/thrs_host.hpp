@@ -339,7 +339,8 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   const uint32_t cap = P.cap;
   // the device-chosen squeeze (float keys over the whole key, single-bucket
   // chunks: thrs_plan_rows; KeyMap<U, true> in thrs_kernels.hpp)
-  const bool squeeze = kSqueezable<KT> && bucket && P.fullWindow && !local32;
+  // (both top passes segmented: the squeeze-aware pass kernel)
+  const bool squeeze = kSqueezable<KT> && bucket && P.fullWindow && !local32 && P.segA;
   const SqueezeWords* sqw =
       squeeze ? reinterpret_cast<const SqueezeWords*>(scratch + plan.hybridOff + kMetaOff + kMetaSqueeze * 4) : nullptr;
   KeyMap<U> km{orderMask, (U)0, 0u};
@@ -486,7 +487,9 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                            chunkOff, chunkB0, meta, reinterpret_cast<uint32_t*>(hyb + kSegInfoOff),
                            reinterpret_cast<uint32_t*>(hyb + kSegBaseOff), (uint32_t)G::TILE, (uint32_t)hgrid,
                            reinterpret_cast<uint32_t*>(hyb + kSegInfoAOff), reinterpret_cast<uint32_t*>(hyb + kSegBaseAOff),
-                           reinterpret_cast<uint32_t*>(hyb + kBigBOff), sqMode, 8 * KB);
+                           reinterpret_cast<uint32_t*>(hyb + kBigBOff), sqMode, 8 * KB,
+                           reinterpret_cast<uint32_t*>(hyb + kBigPosOff), reinterpret_cast<uint32_t*>(hyb + kBigTileOff),
+                           reinterpret_cast<uint4*>(scratch + plan.bigHistOff), nLow);
       };
       if (!local32 && squeeze) {
         plan_rows(1, 0, kSegHistAOff, kRowHistOff);
@@ -692,8 +695,10 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
       uint32_t* bigPos = reinterpret_cast<uint32_t*>(hyb + kBigPosOff);
       uint32_t* bigTile = reinterpret_cast<uint32_t*>(hyb + kBigTileOff);
       uint32_t* bigHist = reinterpret_cast<uint32_t*>(scratch + plan.bigHistOff);
-      // (the low passes reuse both look-back table sets: zeroed by thrs_big_plan)
-      {
+      // (the low passes reuse both look-back table sets: zeroed by
+      // thrs_big_hist; the big chunks' prefixes and counts' zeroing are
+      // thrs_plan_rows's -- thrs_plan's multi-bucket chunks take thrs_big_plan)
+      if (local32) {
         ProfScope prof(stream, 3, THRS_PK_BIG_PLAN, 0);
         hipLaunchKernelGGL(thrs_big_plan, dim3(std::min<uint32_t>(256, cu_count())), dim3(kBigPlanThreads), 0, stream,
                            chunkOff, meta, bigB, bigPos, bigTile, (uint32_t)G::TILE, reinterpret_cast<uint4*>(bigHist),
@@ -703,7 +708,9 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
         ProfScope prof(stream, 3, THRS_PK_BIG_HIST, 0);
         hipLaunchKernelGGL(thrs_big_hist<KT>, dim3(cu_count()), dim3(kHistThreads),
                            (size_t)nLow * kBins * kBigCopies * 4, stream, static_cast<const U*>(keys), km, startBits,
-                           nLow, chunkOff, meta, bigB, bigPos, bigHist, sqw);
+                           nLow, chunkOff, meta, bigB, bigPos, bigHist, sqw,
+                           local32 ? nullptr : reinterpret_cast<uint4*>(scratch + kHeaderBytes),
+                           (uint64_t)(2 * plan.setBytes / 16));
       }
       for (int p = 0; p < nLow; ++p) {
         ProfScope prof(stream, 3, THRS_PK_PASS_BIG, 0);
@@ -712,12 +719,12 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                            status[1], err, sqw);
       }
       ProfScope prof(stream, 3, THRS_PK_BIG_COPY, 0);
+      // (also publishes the sort's error word: no thrs_err_publish launch)
       hipLaunchKernelGGL((thrs_big_copy<U, VW>), dim3(2048), dim3(256), 0, stream, K, keyOut, VB ? V : nullptr, valOut,
-                         chunkOff, meta, bigB, bigPos);
+                         chunkOff, meta, bigB, bigPos, err, sticky);
     }
-    if (hipGetLastError() != hipSuccess) return THRS_ERROR_HIP;
   }
-  return publish_error();
+  return hipGetLastError() == hipSuccess ? THRS_SUCCESS : THRS_ERROR_HIP;
 }
 
 template <int KT, int VB>

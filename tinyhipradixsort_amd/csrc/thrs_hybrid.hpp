@@ -61,6 +61,7 @@ enum {
   kMetaOr1 = 34,        // [2]: per image half, OR of the non-empty buckets' indices
   kMetaOr0 = 36,        // [2]: per image half, OR of their complements (16 bits)
   kMetaBigHalf = 38,    // [2]: per image half, buckets above the local capacity
+  kMetaPlanDone2 = 40,  // the squeezed plan's finished workgroups
   kMetaSqueeze = 48,    // SqueezeWords (14 words, to 61)
 };
 static_assert(kMetaSqueeze * 4 + sizeof(SqueezeWords) <= 256, "meta is 64 words");
@@ -371,18 +372,64 @@ __device__ __forceinline__ void plan_squeeze(uint32_t* __restrict__ meta, int ke
   meta[kMetaBigCount] = 0;
 }
 
+// The per-bucket fallback's plan (thrs_fallback.hpp), by the plan's last
+// workgroup (256 threads): prefixes of the big chunks' sizes (bigPos: their
+// positions in the concatenation of the big chunks) and tile counts (bigTile).
+__device__ __forceinline__ void plan_big_prefix(const uint32_t* __restrict__ joint, const uint32_t* __restrict__ meta,
+                                                const uint32_t* __restrict__ bigB, uint32_t* __restrict__ bigPos,
+                                                uint32_t* __restrict__ bigTile, uint32_t tileKeys, uint32_t (*s_w)[4]) {
+  const uint32_t M = load_agent(&meta[kMetaBigCount]);
+  if (M == 0) return;
+  const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const uint32_t per = (M + kPlanRowThreads - 1) / kPlanRowThreads;
+  const uint32_t i0 = min(M, t * per), i1 = min(M, i0 + per);
+  auto tiles_of = [&](uint32_t sz) { return (sz + tileKeys - 1) / tileKeys; };
+  uint32_t ks = 0, ts = 0;
+  for (uint32_t i = i0; i < i1; ++i) {
+    const uint32_t sz = joint[bigB[i]];
+    ks += sz;
+    ts += tiles_of(sz);
+  }
+  const uint32_t ik = wave_incl_scan(ks, lane), it = wave_incl_scan(ts, lane);
+  if (lane == 63) {
+    s_w[0][w] = ik;
+    s_w[1][w] = it;
+  }
+  __syncthreads();
+  uint32_t pk = ik - ks, pt = it - ts;
+  for (uint32_t ww = 0; ww < w; ++ww) {
+    pk += s_w[0][ww];
+    pt += s_w[1][ww];
+  }
+  for (uint32_t i = i0; i < i1; ++i) {
+    const uint32_t sz = joint[bigB[i]];
+    bigPos[i] = pk;
+    bigTile[i] = pt;
+    pk += sz;
+    pt += tiles_of(sz);
+  }
+  if (t == kPlanRowThreads - 1) {
+    bigPos[M] = pk;
+    bigTile[M] = pt;
+  }
+}
+
 // sqMode: 0 = plain plan; 1 = float keys, first plan (gathers the bucket
 // occupancy per image half and decides the squeeze, plan_squeeze); 2 = the
-// plan of the squeezed histogram (runs only if the squeeze went on).
+// plan of the squeezed histogram (runs only if the squeeze went on).  The
+// last workgroup to finish also plans the per-bucket fallback (the big
+// chunks' prefixes); the thread that lists a big chunk zeroes its low-digit
+// counts (bigHist, nLow x 256 words).
 __global__ __launch_bounds__(kPlanRowThreads) void thrs_plan_rows(
     const uint32_t* __restrict__ joint, const uint32_t* __restrict__ rowHist, const uint32_t* __restrict__ segHistA,
     uint32_t n, uint32_t cap, uint32_t* __restrict__ baseTop /* [2][256]: second, top */,
     uint32_t* __restrict__ chunkOff, uint32_t* __restrict__ chunkB0, uint32_t* __restrict__ meta,
     uint32_t* __restrict__ segInfo, uint32_t* __restrict__ segBase, uint32_t tileKeys, uint32_t histGrid,
     uint32_t* __restrict__ segInfoA, uint32_t* __restrict__ segBaseA, uint32_t* __restrict__ bigB, int sqMode,
-    int keyBits) {
+    int keyBits, uint32_t* __restrict__ bigPos, uint32_t* __restrict__ bigTile, uint4* __restrict__ bigHist,
+    int nLow) {
   if (sqMode == 2 && meta[kMetaRehist] == 0) return;
-  __shared__ uint32_t s_w[2][4], s_base, s_b2[kBins], s_sq[3];
+  __shared__ uint32_t s_w[2][4], s_base, s_b2[kBins], s_sq[3], s_last;
   const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6, r = blockIdx.x;
   // 256-thread exclusive scan (4 waves)
   auto scan256 = [&](uint32_t v, int slot, uint32_t* total) -> uint32_t {
@@ -413,9 +460,12 @@ __global__ __launch_bounds__(kPlanRowThreads) void thrs_plan_rows(
   if (x > cap) {  // a bucket above the chunk capacity: a big chunk; all n keys in one bucket: mode 2
     atomicOr(&meta[kMetaFallback], 1u);
     atomicMax(&meta[kMetaMode], x == n ? 2u : 1u);
-    bigB[atomicAdd(&meta[kMetaBigCount], 1u)] = kBins * r + t;
+    const uint32_t slot = atomicAdd(&meta[kMetaBigCount], 1u);
+    bigB[slot] = kBins * r + t;
+    uint4* h = bigHist + (uint64_t)slot * nLow * kBins / 4;
+    for (int i = 0; i < nLow * (int)kBins / 4; ++i) h[i] = make_uint4(0, 0, 0, 0);
   }
-  if (sqMode == 1) {  // occupancy of this row's image half; the last workgroup decides
+  if (sqMode == 1) {  // occupancy of this row's image half (for the squeeze decision)
     if (t == 0) s_sq[0] = s_sq[1] = s_sq[2] = 0;
     __syncthreads();
     const uint32_t b = kBins * r + t;
@@ -432,12 +482,22 @@ __global__ __launch_bounds__(kPlanRowThreads) void thrs_plan_rows(
         atomicOr(&meta[kMetaOr0 + h], s_sq[1]);
       }
       if (s_sq[2]) atomicAdd(&meta[kMetaBigHalf + h], s_sq[2]);
-      __threadfence();
-      if (atomicAdd(&meta[kMetaPlanDone], 1u) == gridDim.x - 1) {
-        __threadfence();
-        plan_squeeze(meta, keyBits);
-      }
     }
+  }
+  // the last workgroup: the squeeze decision (sqMode 1), then -- unless the
+  // squeeze went on and a second plan follows -- the fallback's prefixes
+  if (t == 0) {
+    __threadfence();
+    s_last = atomicAdd(&meta[sqMode == 2 ? kMetaPlanDone2 : kMetaPlanDone], 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (s_last) {
+    __threadfence();
+    if (sqMode == 1 && t == 0) plan_squeeze(meta, keyBits);
+    __syncthreads();
+    if (!(sqMode == 1 && load_agent(&meta[kMetaRehist]) != 0u))
+      plan_big_prefix(joint, meta, bigB, bigPos, bigTile, tileKeys, s_w);
+    __syncthreads();  // s_w is reused below
   }
   if (r != 0) return;
   // second digit: totals over the position segments -> bases, segment bases

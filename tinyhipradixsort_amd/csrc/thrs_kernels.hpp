@@ -751,6 +751,12 @@ struct GroupWalk {
           atomicOr(errFlag, 1u);
           break;
         }
+#if THRS_WALK_BACKOFF
+        // experiment: poll less often once a walk has waited a few rounds
+        // (every poll re-reads a window of status words from memory)
+        if (spins > THRS_WALK_BACKOFF) __builtin_amdgcn_s_sleep(8);
+        else
+#endif
         __builtin_amdgcn_s_sleep(1);
       }
     }
