@@ -108,9 +108,10 @@ constexpr uint64_t kBigTileOff = kBigPosOff + round_up_c((kBuckets + 1) * 4, 256
 constexpr uint64_t kHybridBytes = kBigTileOff + round_up_c((kBuckets + 1) * 4, 256);
 // the smallest local-sort capacity (LocSmall): a big chunk holds more keys
 constexpr uint64_t kMinLocalCap = LocSmall::CAP;
-// tile ids of the segmented pass: each of the 8 segments adds at most one
-// partial tile and rounds its id range up to a multiple of kGroup
-constexpr uint64_t kSegTilePad = kSegs * kGroup;
+// tile ids of the segmented pass: each of the 8 segments adds at most two
+// partial tiles (its first and last: seg_tiles) and rounds its id range up
+// to a multiple of kGroup
+constexpr uint64_t kSegTilePad = kSegs * (kGroup + 1);
 
 inline Plan make_plan(int keyType, int valueBytesOrZero, uint32_t n) {
   Plan p{};
@@ -609,10 +610,11 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
       // the segmented pass's tile ids reach past nTiles (per-segment
       // rounding): clear those rows (pass nLow cleared rows [0, nTiles))
       const uint64_t nGroups0 = (plan.nTiles + kGroup - 1) / kGroup;
+      constexpr uint64_t kPadGroups = (kSegTilePad + kGroup - 1) / kGroup + 1;
       if (hipMemsetAsync(reinterpret_cast<char*>(status[setB]) + plan.nTiles * kBins * sw, 0,
                          kSegTilePad * kBins * sw, stream) != hipSuccess ||
-          hipMemsetAsync(grp[setB].ga + nGroups0 * kBins, 0, (kSegs + 1) * kBins * 4, stream) != hipSuccess ||
-          hipMemsetAsync(reinterpret_cast<char*>(grp[setB].gp) + nGroups0 * kBins * sw, 0, (kSegs + 1) * kBins * sw,
+          hipMemsetAsync(grp[setB].ga + nGroups0 * kBins, 0, kPadGroups * kBins * 4, stream) != hipSuccess ||
+          hipMemsetAsync(reinterpret_cast<char*>(grp[setB].gp) + nGroups0 * kBins * sw, 0, kPadGroups * kBins * sw,
                          stream) != hipSuccess)
         return THRS_ERROR_HIP;
     }

@@ -531,8 +531,7 @@ __global__ __launch_bounds__(kPlanRowThreads) void thrs_plan_rows(
       info[sg] = pos;
       info[kSegs + 1 + sg] = tiles;
       if (sg < kSegs) {
-        const uint32_t len = pos_of(sg + 1) - pos;
-        const uint32_t nT = (len + tileKeys - 1) / tileKeys;
+        const uint32_t nT = seg_tiles(pos, pos_of(sg + 1), tileKeys);
         tiles += (nT + kGroup - 1) / kGroup * kGroup;
         info[64 + sg] = 0;  // ticket (own cache line)
       }
@@ -706,8 +705,7 @@ __global__ __launch_bounds__(kPlanThreads) void thrs_plan(const uint32_t* __rest
       info[sg] = pos;
       info[kSegs + 1 + sg] = tiles;
       if (sg < kSegs) {
-        const uint32_t len = pos_of(sg + 1) - pos;
-        const uint32_t nT = (len + tileKeys - 1) / tileKeys;
+        const uint32_t nT = seg_tiles(pos, pos_of(sg + 1), tileKeys);
         tiles += (nT + kGroup - 1) / kGroup * kGroup;
         info[64 + sg] = 0;  // ticket (own cache line)
       }

@@ -1418,6 +1418,21 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
 // plane written by kCodecSplit / read by kCodecPlanes; keysIn / keysOut are
 // then u16 planes).
 constexpr int kSegs = 8;
+// Tiles of a segment [pos, end) are aligned to the whole key array: tile t
+// covers [max(pos, a + tT), min(end, a + (t+1)T)), a = pos rounded down to a
+// multiple of T, so every interior tile's loads start on a 128-B line (the
+// second top-digit pass's segments start at data-dependent positions: with
+// tiles counted from pos every wave load of u16 keys would straddle two
+// lines); the first tile (and the last) may be partial.
+#ifndef THRS_SEG_ALIGN
+#define THRS_SEG_ALIGN 1
+#endif
+__host__ __device__ __forceinline__ uint64_t seg_tile_base(uint32_t pos, uint32_t T) {
+  return THRS_SEG_ALIGN ? (uint64_t)pos / T * T : (uint64_t)pos;
+}
+__host__ __device__ __forceinline__ uint32_t seg_tiles(uint32_t pos, uint32_t end, uint32_t T) {
+  return end > pos ? (uint32_t)(((uint64_t)end - seg_tile_base(pos, T) + T - 1) / T) : 0u;
+}
 template <int KT, int VB, typename ST, bool ATOMIC_RANK, int CODEC = kCodecKeys>
 __global__ __launch_bounds__((PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::THREADS))
 __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::WPE))) void thrs_pass_seg(
@@ -1451,7 +1466,7 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
       for (int q = 0; q < kSegs; ++q) {
         const uint32_t s = (home + q) & (kSegs - 1);
         if (done & (1u << s)) continue;
-        const uint32_t nT = (segPos[s + 1] - segPos[s] + T - 1) / T;
+        const uint32_t nT = seg_tiles(segPos[s], segPos[s + 1], T);
         const uint32_t x = nT ? atomicAdd(&tickets[s], 1u) : nT;
         if (x < nT) {
           seg = s;
@@ -1477,11 +1492,12 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
     const uint32_t seg = s_misc[8], t = s_misc[9];
     if (seg >= (uint32_t)kSegs) break;
     const uint32_t segStart = segPos[seg], segEnd = segPos[seg + 1];
-    const uint64_t keyStart = (uint64_t)segStart + (uint64_t)t * T;
-    const uint32_t valid = (uint32_t)min((uint64_t)T, (uint64_t)segEnd - keyStart);
+    const uint64_t t0 = seg_tile_base(segStart, T) + (uint64_t)t * T;
+    const uint64_t keyStart = max((uint64_t)segStart, t0);
+    const uint32_t valid = (uint32_t)(min((uint64_t)segEnd, t0 + T) - keyStart);
     const uint32_t chain = segTiles[seg];
     GroupTables<ST> g = grp;
-    g.nTiles = chain + (segEnd - segStart + T - 1) / T;  // end of this segment's tile ids
+    g.nTiles = chain + seg_tiles(segStart, segEnd, T);  // end of this segment's tile ids
     g.gmin = chain / kGroup;
     g.gaNext = nullptr;
     g.gpNext = nullptr;
