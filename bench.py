@@ -514,7 +514,7 @@ def main():
         # (the reference's kernels index with 32-bit ints: up to 2^30 keys here)
         if args.ref_gpu == "auto" and world == 1 and dist_kind == "uniform" and n <= (1 << 30):
             ref_gpu = reference_gpu_bench(TU, kt, kb, vb, n, keys, vals, gen, stream)
-        recycled = False
+        inputs = "fresh per step"
         elapsed = t1 - t0
         parallelism = "single"
         phase = None
@@ -587,7 +587,8 @@ def main():
             for (_a0, a1), (b0, _b1) in zip(seq, seq[1:]):
                 if a1 > b0:
                     raise SystemExit("bench: ranks' key ranges overlap after the exchange")
-        recycled = False
+        inputs = ("2 input buffers per rank, alternated: the exchange sort is out of place, so every step "
+                  "sorts an unmodified input (the same two inputs repeat)")
         vendor = ref_gpu = None
         elapsed = t1 - t0
         parallelism = f"bucket-exchange x{world} (RCCL all_gather + grouped point-to-point exchange)"
@@ -628,7 +629,7 @@ def main():
                           "value": None if not vb else f"{vb}B index payload", "bits": [0, kb * 8],
                           "parallelism": parallelism,
                           "distribution": dist_name,
-                          "inputs": "fresh per step" if not recycled else "pool recycled (some steps re-sort)"},
+                          "inputs": inputs},
                "roofline": roof, "cpu_baseline": cpu, "vendor": vendor, "reference_gpu": ref_gpu}
         if phase:
             out["phases_ms"] = phase

@@ -262,14 +262,18 @@ def _worker_big(rank, world, port, out_dir, kt, vb, n):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,kt,vb,n", [(2, O.U32, 0, 1 << 28), (1, O.U64, 8, 1 << 28)])
+@pytest.mark.parametrize("world,kt,vb,n", [(2, O.U32, 0, 1 << 28), (1, O.U64, 8, 1 << 28),
+                                           (2, O.U32, 0, 1 << 27), (1, O.U32, 0, 1 << 27),
+                                           (2, O.U64, 8, 1 << 27), (2, O.U32, 0, 1 << 29)])
 def test_bucket_finish_with_key_range(gpu, tmp_path, world, kt, vb, n):
     """The exchange's finish runs the bucket path (VERDICT r02
     next-step 3): each rank passes the key range the exact split fixed
     (dist.key_range -> thrs_options.keyRange), so its 16-bit buckets stay
     balanced and the local sort -- not the per-bucket fallback -- finishes
-    the sort.  World 2 over gloo with real HIP steps (u32 keys, 2^28 per rank),
-    world 1 over RCCL (the C5 shape at 2^28: u64 keys + u64 index payload)."""
+    the sort.  World 2 over gloo with real HIP steps (u32 keys, 2^27 .. 2^29
+    per rank: 2^27 is C2's per-rank share at 8 GPUs),
+    world 1 over RCCL (u32 at 2^27; the C5 shape at 2^28: u64 keys + u64
+    index payload)."""
     import json
     import torch.multiprocessing as mp
     with socket.socket() as so:

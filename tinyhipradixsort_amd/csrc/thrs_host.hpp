@@ -33,6 +33,10 @@
 namespace thrs_host {
 using namespace thrs_dev;
 
+#ifndef THRS_SEG_MERGE
+#define THRS_SEG_MERGE 0  // experiment: see thrs_pass_seg ALT
+#endif
+
 constexpr uint64_t kAlign = 256;
 constexpr uint64_t kHistOff = 0;                       // u32 [8][256]
 constexpr uint64_t kBaseOff = 8 * 256 * 4;             // u32 [8][256]
@@ -232,7 +236,12 @@ PathSel select_path(uint32_t n, int startBits, int nPass, const thrs_options& op
   // below the capacity); 4-byte keys-only up to 2^31 + 2^25 in 34816-key
   // chunks (Loc16Wide).
   const uint64_t nn = n;
-  const bool sizeOk = nn >= (1ull << 28) && nn <= (1ull << 30) + (kKV ? (1ull << 24) : (1ull << 26));
+  // a key range (the multi-GPU finish: its keys fill the image space, so the
+  // buckets are uniform whatever the global distribution) takes the bucket
+  // path from 2^27 (C2's 2^30 keys over 8 GPUs; docs/EXPERIMENTS.md row 84)
+  const bool rangedReq = opt.keyRange == 1 && fullWindow && !counts;
+  const uint64_t minN = rangedReq ? (1ull << 27) : (1ull << 28);
+  const bool sizeOk = nn >= minN && nn <= (1ull << 30) + (kKV ? (1ull << 24) : (1ull << 26));
   const bool wideOk = kKeys4 && fullWindow && nn > (1ull << 30) + (1ull << 26) && nn <= (1ull << 31) + (1ull << 25);
   const bool smallLocal = opt.localGeometry == THRS_LOCAL_SMALL ? true
                           : opt.localGeometry != THRS_LOCAL_AUTO  // BIG, BIG32 and the 16-bit kernels
@@ -371,6 +380,15 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                             : thrs_pass_seg<KT, VB, ST, false, (KT == 0 && VB == 0) ? kCodecSplit : kCodecKeys>;
   auto skPlanes = atomicRank ? thrs_pass_seg<KT, VB, ST, true, (KT == 0 && VB == 0) ? kCodecPlanes : kCodecKeys>
                              : thrs_pass_seg<KT, VB, ST, false, (KT == 0 && VB == 0) ? kCodecPlanes : kCodecKeys>;
+  // THRS_SEG_MERGE: the plane codecs and their whole-key alternative (mode 1)
+  // in one launch each (thrs_pass_seg ALT)
+  // (other key / value types: the plain keys kernel, never launched merged)
+  constexpr int kAltM = (KT == 0 && VB == 0 && THRS_SEG_MERGE) ? kCodecKeys : -1;
+  auto skSplitM = atomicRank ? thrs_pass_seg<KT, VB, ST, true, (KT == 0 && VB == 0) ? kCodecSplit : kCodecKeys, kAltM>
+                             : thrs_pass_seg<KT, VB, ST, false, (KT == 0 && VB == 0) ? kCodecSplit : kCodecKeys, kAltM>;
+  auto skPlanesM = atomicRank
+                       ? thrs_pass_seg<KT, VB, ST, true, (KT == 0 && VB == 0) ? kCodecPlanes : kCodecKeys, kAltM>
+                       : thrs_pass_seg<KT, VB, ST, false, (KT == 0 && VB == 0) ? kCodecPlanes : kCodecKeys, kAltM>;
   const int histPasses = nPass;
   const size_t histLds = (size_t)histPasses * kBins * hist_copies<(int)sizeof(U)>() * 4;
   if (allow_lds(thrs_hist<KT>, histLds) != hipSuccess || allow_lds(kernel, lds) != hipSuccess ||
@@ -380,7 +398,8 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     if (allow_lds(thrs_hist_joint<KT>, kJointLds) != hipSuccess || allow_lds(sk, lds) != hipSuccess ||
         (squeeze && allow_lds(thrs_hist_joint<KT, true>, kJointLds) != hipSuccess))
       return THRS_ERROR_HIP;
-    if (planes && (allow_lds(skSplit, lds) != hipSuccess || allow_lds(skPlanes, lds) != hipSuccess))
+    if (planes && (allow_lds(skSplit, lds) != hipSuccess || allow_lds(skPlanes, lds) != hipSuccess ||
+                   allow_lds(skSplitM, lds) != hipSuccess || allow_lds(skPlanesM, lds) != hipSuccess))
       return THRS_ERROR_HIP;
     if constexpr (kKV) {
       if (allow_lds(atomicRank ? thrs_local_kv<KT, VB, true> : thrs_local_kv<KT, VB, false>, LocKV::LDS) != hipSuccess)
@@ -591,14 +610,34 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                          status[p & 1], err, grp[p & 1], gate, gateMask, hiP,
                          g_stamps ? g_stamps + (uint64_t)(p - nLow) * (plan.nTiles + kSegTilePad) * kStampSlots
                                   : nullptr,
-                         sqw);
+                         sqw, static_cast<const U*>(nullptr), static_cast<U*>(nullptr), km, 0);
     };
     const uint64_t sw = plan.wideStatus ? 8 : 4;
     const int setB = (nLow + 1) & 1;
+    // one launch per top pass for both plan modes (the plane codecs in mode
+    // 0, whole keys in mode 1)
+    auto launch_seg_merged = [&](int p, bool second) {
+      ProfScope prof(stream, 1, THRS_PK_PASS_SEG, moveBytes);
+      const U* kin = second ? reinterpret_cast<const U*>(loP) : K;
+      U* kout = second ? reinterpret_cast<U*>(lo2P) : reinterpret_cast<U*>(loP);
+      const U* kin2 = second ? keyOut : K;
+      U* kout2 = second ? K : keyOut;
+      hipLaunchKernelGGL(second ? skPlanesM : skSplitM, dim3((uint32_t)segPerCU * cu_count()), dim3(G::THREADS), lds,
+                         stream, kin, kout, second ? valOut : V, second ? V : valOut, second ? kid : km,
+                         second ? 16 : startBits + 8 * p,
+                         reinterpret_cast<uint32_t*>(hyb + (second ? kSegInfoOff : kSegInfoAOff)),
+                         reinterpret_cast<const uint32_t*>(hyb + (second ? kSegBaseOff : kSegBaseAOff)), status[p & 1],
+                         err, grp[p & 1], mode, kGateMode0, hiP,
+                         g_stamps ? g_stamps + (uint64_t)(p - nLow) * (plan.nTiles + kSegTilePad) * kStampSlots
+                                  : nullptr,
+                         sqw, kin2, kout2, km, startBits + 8 * p);
+    };
     if (segA) {
       // Both table sets are clean (zeroed up front); the segmented passes'
       // extra tile ids (rows past nTiles) are touched by nothing else.
-      if (planes) {
+      if (planes && THRS_SEG_MERGE) {
+        launch_seg_merged(nLow, false);
+      } else if (planes) {
         launch_seg(nLow, K, reinterpret_cast<U*>(loP), V, valOut, kSegInfoAOff, kSegBaseAOff, mode, kGateMode0,
                    kCodecSplit);
         launch_seg(nLow, K, keyOut, V, valOut, kSegInfoAOff, kSegBaseAOff, mode, kGateMode1);
@@ -618,7 +657,9 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                          stream) != hipSuccess)
         return THRS_ERROR_HIP;
     }
-    if (planes) {  // mode 0: planes -> lo2; mode 1 (big chunks): keys
+    if (planes && THRS_SEG_MERGE) {
+      launch_seg_merged(nLow + 1, true);
+    } else if (planes) {  // mode 0: planes -> lo2; mode 1 (big chunks): keys
       launch_seg(nLow + 1, reinterpret_cast<U*>(loP), reinterpret_cast<U*>(lo2P), valOut, V, kSegInfoOff, kSegBaseOff,
                  mode, kGateMode0, kCodecPlanes);
       launch_seg(nLow + 1, keyOut, K, valOut, V, kSegInfoOff, kSegBaseOff, mode, kGateMode1);

@@ -1433,20 +1433,18 @@ __host__ __device__ __forceinline__ uint64_t seg_tile_base(uint32_t pos, uint32_
 __host__ __device__ __forceinline__ uint32_t seg_tiles(uint32_t pos, uint32_t end, uint32_t T) {
   return end > pos ? (uint32_t)(((uint64_t)end - seg_tile_base(pos, T) + T - 1) / T) : 0u;
 }
-template <int KT, int VB, typename ST, bool ATOMIC_RANK, int CODEC = kCodecKeys>
-__global__ __launch_bounds__((PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::THREADS))
-__attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::WPE))) void thrs_pass_seg(
+template <int KT, int VB, typename ST, bool ATOMIC_RANK, int CODEC>
+__device__ __forceinline__ void thrs_pass_seg_body(
     const typename KeyTraits<KT>::U* __restrict__ keysIn, typename KeyTraits<KT>::U* __restrict__ keysOut,
     const typename ValueWord<VB>::T* __restrict__ valsIn, typename ValueWord<VB>::T* __restrict__ valsOut,
     KeyMap<typename KeyTraits<KT>::U> km, int shift, uint32_t* __restrict__ segInfo,
     const uint32_t* __restrict__ segBase, ST* __restrict__ status, uint32_t* __restrict__ errFlag,
-    GroupTables<ST> grp, const uint32_t* __restrict__ gate, uint32_t gateMask, uint8_t* __restrict__ hiPlane,
-    uint64_t* __restrict__ stamps, const SqueezeWords* __restrict__ sq) {
+    GroupTables<ST> grp, uint8_t* __restrict__ hiPlane, uint64_t* __restrict__ stamps,
+    const SqueezeWords* __restrict__ sq) {
   using U = typename KeyTraits<KT>::U;
   using VW = typename ValueWord<VB>::T;
   using G = PassGeom<sizeof(U), VB>;
   constexpr uint32_t T = G::TILE;
-  if (gate && !((gateMask >> *gate) & 1u)) return;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint32_t* s_cnt = reinterpret_cast<uint32_t*>(smem + G::STAGE * (sizeof(U) + VB));
   uint32_t* s_misc = s_cnt + (G::WAVES + 1) * kBins;
@@ -1509,6 +1507,44 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
     lds_barrier();  // stage, s_gofs and s_misc are reused by the next tile
   }
   });
+}
+
+// ALT >= 0 (THRS_SEG_MERGE: the u32 key-plane passes): one launch serves both
+// plan modes -- CODEC with keysIn / keysOut / km / shift when the gate word
+// is in gateMask, else codec ALT with keysIn2 / keysOut2 / km2 / shift2 when
+// it is 1 (big chunks: the per-bucket fallback needs whole keys), instead of
+// a second, gated launch.
+template <int KT, int VB, typename ST, bool ATOMIC_RANK, int CODEC = kCodecKeys, int ALT = -1>
+__global__ __launch_bounds__((PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::THREADS))
+__attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::WPE))) void thrs_pass_seg(
+    const typename KeyTraits<KT>::U* __restrict__ keysIn, typename KeyTraits<KT>::U* __restrict__ keysOut,
+    const typename ValueWord<VB>::T* __restrict__ valsIn, typename ValueWord<VB>::T* __restrict__ valsOut,
+    KeyMap<typename KeyTraits<KT>::U> km, int shift, uint32_t* __restrict__ segInfo,
+    const uint32_t* __restrict__ segBase, ST* __restrict__ status, uint32_t* __restrict__ errFlag,
+    GroupTables<ST> grp, const uint32_t* __restrict__ gate, uint32_t gateMask, uint8_t* __restrict__ hiPlane,
+    uint64_t* __restrict__ stamps, const SqueezeWords* __restrict__ sq,
+    const typename KeyTraits<KT>::U* __restrict__ keysIn2 = nullptr,
+    typename KeyTraits<KT>::U* __restrict__ keysOut2 = nullptr, KeyMap<typename KeyTraits<KT>::U> km2 = {},
+    int shift2 = 0) {
+  using U = typename KeyTraits<KT>::U;
+  using VW = typename ValueWord<VB>::T;
+  using G = PassGeom<sizeof(U), VB>;
+  constexpr uint32_t T = G::TILE;
+  if constexpr (ALT >= 0) {
+    const uint32_t m = *gate;
+    if (!((gateMask >> m) & 1u)) {
+      if (m != 1u) return;
+      // mode 1: the whole-key codec on the alternative buffers (one call of
+      // this same kernel body, not inlined twice)
+      thrs_pass_seg_body<KT, VB, ST, ATOMIC_RANK, ALT>(keysIn2, keysOut2, valsIn, valsOut, km2, shift2, segInfo,
+                                                        segBase, status, errFlag, grp, hiPlane, stamps, sq);
+      return;
+    }
+  } else {
+    if (gate && !((gateMask >> *gate) & 1u)) return;
+  }
+  thrs_pass_seg_body<KT, VB, ST, ATOMIC_RANK, CODEC>(keysIn, keysOut, valsIn, valsOut, km, shift, segInfo, segBase,
+                                                      status, errFlag, grp, hiPlane, stamps, sq);
 }
 
 // Zeroing of up to three 16-byte-aligned ranges in one launch (the scratch
