@@ -565,6 +565,37 @@ def _mode_after(torch, rs, keys, vals, kt, vb):
     return mode, k, v
 
 
+def _squeezed_images(img, W, cap):
+    """numpy model of thrs_plan_rows's squeeze decision (thrs_hybrid.hpp
+    plan_squeeze): if some bucket would overflow and not every key is in one
+    bucket, in each image half holding big buckets drop the highest bucket bit
+    (below the half bit) that all its non-empty buckets share."""
+    img = img.astype(np.uint64)
+    b = (img >> np.uint64(W - 16)).astype(np.int64)
+    cnt = np.bincount(b, minlength=65536)
+    if not ((cnt > cap).any() and cnt.max() < img.shape[0]):
+        return img
+    out = img.copy()
+    any_sq = False
+    for h in (0, 1):
+        nz = np.nonzero(cnt[h << 15:(h + 1) << 15])[0] + (h << 15)
+        big = int((cnt[h << 15:(h + 1) << 15] > cap).sum())
+        if nz.size == 0 or big == 0:
+            continue
+        o1 = int(np.bitwise_or.reduce(nz))
+        o0 = int(np.bitwise_or.reduce(~nz & 0xFFFF))
+        cm = ~(o1 & o0) & 0x7FFF
+        if not cm:
+            continue
+        bit = cm.bit_length() - 1 + W - 16
+        hi = np.uint64(~((2 << bit) - 1) & ((1 << W) - 1))
+        lo = np.uint64((1 << bit) - 1)
+        sel = (img >> np.uint64(W - 1)) == np.uint64(h)
+        out[sel] = (img[sel] & hi) | ((img[sel] & lo) << np.uint64(1))
+        any_sq = True
+    return out if any_sq else img
+
+
 @pytest.mark.parametrize("kt,vb", [(O.U32, 0), (O.U32, 4), (O.F32, 0), (O.U64, 8), (O.U32, 16)])
 def test_per_bucket_fallback(gpu, kt, vb):
     """Only buckets above the local capacity take device passes (thrs_fallback.hpp):
@@ -587,7 +618,11 @@ def test_per_bucket_fallback(gpu, kt, vb):
     cap = rs.pathInfo(n, 0, 8 * kb, bool(vb))["local_cap"]
     for name, keys in cases.items():
         # expected plan: buckets (top 16 image bits) above the local capacity
-        cnt = np.bincount((O.key_bits_np(kt, keys) >> np.uint64(8 * kb - 16)).astype(np.int64), minlength=65536)
+        # -- for float keys under the squeeze thrs_plan_rows may choose
+        img = O.key_bits_np(kt, keys)
+        if kt in (O.F32, O.F64):
+            img = _squeezed_images(img, 8 * kb, cap)
+        cnt = np.bincount((img >> np.uint64(8 * kb - 16)).astype(np.int64), minlength=65536)
         ebig = int((cnt > cap).sum())
         emode = 0 if ebig == 0 else (2 if int(cnt.max()) == n else 1)
         assert ebig >= 1, name
@@ -629,9 +664,16 @@ def test_key_range_keeps_buckets_local(gpu, kt, vb, desc):
         vals = (np.arange(n * vb // 4, dtype=np.uint32) * np.uint32(2654435761)).view(
             {4: np.uint32, 8: np.uint64}[vb])
     ek, ev = O.lsd_sort(kt, keys, vals, 0, 8 * kb, desc)
-    # without the range: 16 overflowing buckets for 4-byte keys (20 random low
-    # bits reach bits 16..19), one bucket holding every key for 8-byte keys
-    for rng, want_mode in (((lo, hi), 0), (None, 1 if kb == 4 else 2)):
+    # without the range: 16 overflowing buckets for 4-byte integer keys (20
+    # random low bits reach bits 16..19), one bucket holding every key for
+    # 8-byte keys; f32 keys in [1, 2): 128 buckets, which the squeeze
+    # (thrs_plan_rows) doubles -- enough here (the model says which)
+    no_range_mode = 1 if kb == 4 else 2
+    if kt == O.F32:
+        cap = make_sorter(kt, vb, desc, path="bucket").pathInfo(n, 0, 32, bool(vb))["local_cap"]
+        cnt = np.bincount((_squeezed_images(img, 32, cap) >> np.uint64(16)).astype(np.int64), minlength=65536)
+        no_range_mode = 0 if int(cnt.max()) <= cap else 1
+    for rng, want_mode in (((lo, hi), 0), (None, no_range_mode)):
         rs = make_sorter(kt, vb, desc, path="bucket", keyRange=rng)
         (mode, big), k, v = _mode_after(torch, rs, keys, vals, kt, vb)
         assert np.array_equal(k.view(kdt), ek.view(kdt)), (rng, mode)

@@ -385,8 +385,10 @@ __device__ __forceinline__ void plan_big_prefix(const uint32_t* __restrict__ joi
   const uint32_t i0 = min(M, t * per), i1 = min(M, i0 + per);
   auto tiles_of = [&](uint32_t sz) { return (sz + tileKeys - 1) / tileKeys; };
   uint32_t ks = 0, ts = 0;
+  // (bucket ids clamped: a stale entry must never address past the histogram)
+  auto size_of = [&](uint32_t i) { return joint[min(bigB[i], kBuckets - 1)]; };
   for (uint32_t i = i0; i < i1; ++i) {
-    const uint32_t sz = joint[bigB[i]];
+    const uint32_t sz = size_of(i);
     ks += sz;
     ts += tiles_of(sz);
   }
@@ -402,7 +404,7 @@ __device__ __forceinline__ void plan_big_prefix(const uint32_t* __restrict__ joi
     pt += s_w[1][ww];
   }
   for (uint32_t i = i0; i < i1; ++i) {
-    const uint32_t sz = joint[bigB[i]];
+    const uint32_t sz = size_of(i);
     bigPos[i] = pk;
     bigTile[i] = pt;
     pk += sz;
@@ -485,7 +487,10 @@ __global__ __launch_bounds__(kPlanRowThreads) void thrs_plan_rows(
     }
   }
   // the last workgroup: the squeeze decision (sqMode 1), then -- unless the
-  // squeeze went on and a second plan follows -- the fallback's prefixes
+  // squeeze went on and a second plan follows -- the fallback's prefixes.
+  // (The barrier orders every thread's big-chunk entry, bigB[slot], before
+  // thread 0's release and arrival: the last workgroup reads them all.)
+  __syncthreads();
   if (t == 0) {
     __threadfence();
     s_last = atomicAdd(&meta[sqMode == 2 ? kMetaPlanDone2 : kMetaPlanDone], 1u) == gridDim.x - 1;
