@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdint>
 #include <cstring>
 
@@ -243,10 +244,22 @@ PathSel select_path(uint32_t n, int startBits, int nPass, const thrs_options& op
   const uint64_t minN = rangedReq ? (1ull << 27) : (1ull << 28);
   const bool sizeOk = nn >= minN && nn <= (1ull << 30) + (kKV ? (1ull << 24) : (1ull << 26));
   const bool wideOk = kKeys4 && fullWindow && nn > (1ull << 30) + (1ull << 26) && nn <= (1ull << 31) + (1ull << 25);
+  // the local geometry follows the keys per USED bucket: a range whose span
+  // is just above a power of two fills only about half of the image space
+  // ((img - lo) << sh keeps its top bit clear for most keys), so its
+  // buckets hold up to twice n / 65536 keys (the multi-GPU finish at 2
+  // GPUs: rank 1's range is [~2^31, 2^32 - 1])
+  double fill = 1.0;
+  if (rangedReq && opt.rangeHi > opt.rangeLo) {
+    const U span = (U)opt.rangeHi - (U)opt.rangeLo;
+    const int sh = sizeof(U) == 4 ? __builtin_clz((uint32_t)span) : __builtin_clzll((uint64_t)span);
+    fill = std::ldexp((double)span, sh - (int)(8 * sizeof(U)));  // in [0.5, 1)
+  }
+  const double nEff = (double)nn / std::max(fill, 0.5);
   const bool smallLocal = opt.localGeometry == THRS_LOCAL_SMALL ? true
                           : opt.localGeometry != THRS_LOCAL_AUTO  // BIG, BIG32 and the 16-bit kernels
                               ? false
-                              : nn <= (1ull << 29);
+                              : nEff <= (double)(1ull << 29);
   const bool bucket = !counts && nPass >= 3 &&
                       (opt.path == THRS_PATH_BUCKET || (opt.path == THRS_PATH_AUTO && (sizeOk || wideOk))) &&
                       (kKeys4 || fullWindow);
@@ -257,7 +270,7 @@ PathSel select_path(uint32_t n, int startBits, int nPass, const thrs_options& op
   // ... in 34816-key chunks (explicitly, or by default above 2^30 + 2^26);
   // 9216-key chunks for n <= 2^29 (or asked: SMALL)
   const bool wide16 = local16 && (opt.localGeometry == THRS_LOCAL_WIDE16 ||
-                                  (opt.localGeometry == THRS_LOCAL_AUTO && nn > (1ull << 30) + (1ull << 26)));
+                                  (opt.localGeometry == THRS_LOCAL_AUTO && nEff > (double)((1ull << 30) + (1ull << 26))));
   const bool small16 = local16 && !wide16 && smallLocal;
   // ... u32 only: sorted by counting (thrs_local_count16) when asked (it
   // measured slower, docs/EXPERIMENTS.md row 56)
