@@ -26,7 +26,7 @@ import tinyhipradixsort_amd as T  # noqa: E402
 from tinyhipradixsort_amd import testutil as TU  # noqa: E402
 
 WL = {"c2": (0, 0, 1 << 30), "c3": (0, 4, 1 << 30), "c4": (2, 0, 1 << 28), "c5": (1, 8, 1 << 28),
-      "k64": (1, 0, 1 << 29)}
+      "k64": (1, 0, 1 << 29), "kf32v32": (2, 4, 1 << 30), "f32k": (2, 0, 1 << 30), "ref160m": (0, 0, 160000000)}
 
 
 def load(path):
@@ -58,8 +58,8 @@ def main():
     kt, vb, n = WL[a.workload]
     n = a.n or n
     kb = 4 if kt in (0, 2) else 8
-    paths = [os.path.join(ROOT, "build", "variants", f"libthrs_{v}.so") for v in a.variants] if a.variants else \
-        sorted(glob.glob(os.path.join(ROOT, "build", "variants", "libthrs_*.so")))
+    paths = [os.path.join(ROOT, "exp", "variants", f"libthrs_{v}.so") for v in a.variants] if a.variants else \
+        sorted(glob.glob(os.path.join(ROOT, "exp", "variants", "libthrs_*.so")))
     paths = [T.LIB_PATH] + [p for p in paths if os.path.exists(p)]
     libs = [(os.path.basename(p)[len("libthrs"):-3].lstrip("_") or "main", load(p)) for p in paths]
     cfg = T._CConfig(1, kt, {0: 0, 4: 0, 8: 1, 16: 2}[vb], 0)

@@ -100,7 +100,9 @@ constexpr uint64_t kSegHistA2Off = kJoint2Off + kJointBytes;
 constexpr uint64_t kRowHist2Off = kSegHistA2Off + kSegs * 256 * 4;
 constexpr uint64_t kMetaOff = kRowHist2Off + 256 * 4;             // zero: thrs_plan_rows raises its flags atomically
 constexpr uint64_t kJointZero = kMetaOff + 256;
-constexpr uint64_t kChunkOffOff = kJointZero;
+// the sampled squeeze (thrs_squeeze_sample: written whole every float sort, not zeroed)
+constexpr uint64_t kSampleOff = kJointZero;
+constexpr uint64_t kChunkOffOff = kJointZero + 256;
 constexpr uint64_t kChunkB0Off = kChunkOffOff + round_up_c((kBuckets + 1) * 4, 256);
 constexpr uint64_t kSegInfoOff = kChunkB0Off + round_up_c((kBuckets + 1) * 4, 256);  // segPos[9] | segTiles[9] ... tickets[8] at +256 B (thrs_pass_seg)
 constexpr uint64_t kSegBaseOff = kSegInfoOff + 512;   // u32 [8][256] per-segment top-digit bases
@@ -366,6 +368,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   const bool squeeze = kSqueezable<KT> && bucket && P.fullWindow && !local32 && P.segA;
   const SqueezeWords* sqw =
       squeeze ? reinterpret_cast<const SqueezeWords*>(scratch + plan.hybridOff + kMetaOff + kMetaSqueeze * 4) : nullptr;
+  SqueezeWords* sample = squeeze ? reinterpret_cast<SqueezeWords*>(scratch + plan.hybridOff + kSampleOff) : nullptr;
   KeyMap<U> km{orderMask, (U)0, 0u};
   if (ranged) {
     const U span = (U)opt.rangeHi - (U)opt.rangeLo;  // > 0 (sort_impl returns at once for 0)
@@ -502,12 +505,15 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     const uint64_t want = ((uint64_t)n + kHistThreads * 64 - 1) / (kHistThreads * 64);
     const int hgrid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cu_count() * THRS_HIST_GRID_MULT));
     if (bucket) {
+      if (squeeze)  // the sample's guess at the squeeze, for the first histogram
+        hipLaunchKernelGGL(thrs_squeeze_sample<KT>, dim3(1), dim3(kSqSampleThreads), 0, stream,
+                           static_cast<const U*>(keys), n, km, cap, sample);
       {
         ProfScope prof(stream, 0, THRS_PK_HIST_JOINT, keyBytes);
         hipLaunchKernelGGL(thrs_hist_joint<KT>, dim3(hgrid), dim3(kHistThreads), kJointLds, stream,
                          static_cast<const U*>(keys), n, km, startBits + 8 * nLow, vec, joint,
                          reinterpret_cast<uint32_t*>(hyb + kSegHistAOff), reinterpret_cast<uint32_t*>(hyb + kRowHistOff),
-                         tables, meta, nullptr);
+                         tables, meta, sample);
       }
       // single-bucket chunks: one workgroup per top digit; float keys with
       // the whole key decide the squeeze (sqMode 1) and, if it went on,
@@ -522,7 +528,8 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                            reinterpret_cast<uint32_t*>(hyb + kSegInfoAOff), reinterpret_cast<uint32_t*>(hyb + kSegBaseAOff),
                            reinterpret_cast<uint32_t*>(hyb + kBigBOff), sqMode, 8 * KB,
                            reinterpret_cast<uint32_t*>(hyb + kBigPosOff), reinterpret_cast<uint32_t*>(hyb + kBigTileOff),
-                           reinterpret_cast<uint4*>(scratch + plan.bigHistOff), nLow);
+                           reinterpret_cast<uint4*>(scratch + plan.bigHistOff), nLow,
+                           sqMode == 1 ? static_cast<const SqueezeWords*>(sample) : nullptr);
       };
       if (!local32 && squeeze) {
         plan_rows(1, 0, kSegHistAOff, kRowHistOff);

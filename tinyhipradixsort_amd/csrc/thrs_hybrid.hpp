@@ -62,6 +62,7 @@ enum {
   kMetaOr0 = 36,        // [2]: per image half, OR of their complements (16 bits)
   kMetaBigHalf = 38,    // [2]: per image half, buckets above the local capacity
   kMetaPlanDone2 = 40,  // the squeezed plan's finished workgroups
+  kMetaSqViol = 41,     // a key broke the sampled squeeze (its dropped bit differs): histogram again, plain
   kMetaSqueeze = 48,    // SqueezeWords (14 words, to 61)
 };
 static_assert(kMetaSqueeze * 4 + sizeof(SqueezeWords) <= 256, "meta is 64 words");
@@ -99,26 +100,26 @@ __device__ __forceinline__ uint32_t hj_seg_pos(uint32_t n, uint32_t G, uint32_t 
   return (uint32_t)min((uint64_t)n, first * hj_len(n, G));
 }
 
-// SQ: the second histogram of a squeezed sort (float keys; thrs_plan_rows
-// found constant bits among the bucket bits and switched the squeeze on):
-// runs only when meta[kMetaRehist] is set, under the squeezed map.
-template <int KT, bool SQ = false>
+// Float keys (the squeeze, KeyMap<U, true>): the map is sq's when sq->on.
+// First histogram (SECOND = false): sq = the sample's guess
+// (thrs_squeeze_sample); every key of a squeezed half is checked to carry the
+// dropped bit's value, and a key that does not raises meta[kMetaSqViol] (the
+// plan then takes the histogram again under the plain map).  SECOND = true:
+// the second histogram, only when meta[kMetaRehist] is set, under the map
+// the plan chose (meta's SqueezeWords, on or off).
+template <int KT, bool SECOND = false>
 __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename KeyTraits<KT>::U* __restrict__ keys,
                                                                 uint32_t n, KeyMap<typename KeyTraits<KT>::U> kmh,
                                                                 int bucketShift, int vec,
                                                                 uint32_t* __restrict__ joint,
                                                                 uint32_t* __restrict__ segHist /* [8][256] */,
                                                                 uint32_t* __restrict__ rowHist /* [256] */,
-                                                                ZeroRanges tables, const uint32_t* __restrict__ meta,
+                                                                ZeroRanges tables, uint32_t* __restrict__ meta,
                                                                 const SqueezeWords* __restrict__ sq) {
   using U = typename KeyTraits<KT>::U;
-  if constexpr (SQ) {
+  if constexpr (SECOND) {
     if (meta[kMetaRehist] == 0) return;
   }
-  const auto km = [&]() {
-    if constexpr (SQ) return with_squeeze(kmh, sq);
-    else return kmh;
-  }();
   extern __shared__ __attribute__((aligned(16))) uint32_t s_joint[];
   uint32_t* s_d2 = s_joint + kJointWords;
   uint32_t* s_log = s_d2 + kBins;
@@ -136,12 +137,23 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
   for (uint32_t i = tid; i < kJointWords + kBins; i += kHistThreads) s_joint[i] = 0;
   if (tid == 0) *s_logN = 0;
   __syncthreads();
+  with_map<KT>(kmh, sq, [&](auto km) {
+  // (a squeezed first histogram: does every key carry its half's dropped bit?)
+  constexpr bool kCheck = !SECOND && !std::is_same<decltype(km), KeyMap<U>>::value;
+  U viol = 0;
   const uint64_t len = hj_len(n, gridDim.x);
   const uint64_t lo = min((uint64_t)n, (uint64_t)blockIdx.x * len), hi = min((uint64_t)n, lo + len);
   uint32_t* segH = segHist + (blockIdx.x * kSegs / gridDim.x) * kBins;
 
   const uint32_t lane = tid & 63;
   auto bucket_of = [&](U k) -> uint32_t {
+    if constexpr (kCheck) {
+      const U y0 = ((KeyTraits<KT>::bits(k) ^ km.mask) - km.lo) << km.sh;  // the plain image
+      const bool h = (y0 >> (8 * sizeof(U) - 1)) != 0;
+      const U sbit = (h ? km.loM[1] : km.loM[0]) + 1u;  // the dropped bit (0 in an unsqueezed half)
+      const U hm = h ? km.hiM[1] : km.hiM[0];
+      viol |= (y0 & sbit & ~hm) ^ (h ? km.cst[1] : km.cst[0]);
+    }
     return (uint32_t)(kimg<KT>(km, k) >> bucketShift) & 0xFFFFu;
   };
   // Adds are wave-aggregated as in wave_count_items (sorted input would
@@ -316,6 +328,82 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
   }
   __syncthreads();
   if (tid < kBins && s_d2[tid]) atomicAdd(&segH[tid], s_d2[tid]);
+  if constexpr (kCheck) {
+    if (__ballot(viol != 0)) {
+      if (lane == 0) atomicOr(&meta[kMetaSqViol], 1u);
+    }
+  }
+  });
+}
+
+// ----------------------------------------------------- the sampled squeeze
+// Float keys over the whole key (before the first bucket histogram; one
+// 256-thread workgroup): kSqSample evenly spaced keys give, per image half,
+// the bucket bits that all of them share.  In a half whose keys would
+// overflow the local sort -- its share of n over the 2^(15 - constant bits)
+// buckets it can reach, above 7/8 of the capacity -- the highest such bit is
+// dropped (KeyMap<U, true>), so the FIRST histogram already counts the
+// squeezed buckets: the reference's own float generator (the lowest exponent
+// bit cleared, unittest.cpp:103/108) needs one read of the keys, not two.
+// A sample can miss a key that breaks the guess: the histogram checks every
+// key (meta[kMetaSqViol]) and the plan then histograms again, plainly.
+constexpr int kSqSampleThreads = 256;
+constexpr uint32_t kSqSample = 8192;
+template <int KT>
+__global__ __launch_bounds__(kSqSampleThreads) void thrs_squeeze_sample(const typename KeyTraits<KT>::U* __restrict__ keys,
+                                                                        uint32_t n, KeyMap<typename KeyTraits<KT>::U> km,
+                                                                        uint32_t cap, SqueezeWords* __restrict__ out) {
+  using U = typename KeyTraits<KT>::U;
+  constexpr int W = 8 * (int)sizeof(U);
+  __shared__ uint32_t s_o1[2], s_o0[2], s_cnt[2];
+  const uint32_t t = threadIdx.x;
+  if (t < 2) s_o1[t] = s_o0[t] = s_cnt[t] = 0;
+  __syncthreads();
+  uint32_t o1[2] = {0, 0}, o0[2] = {0, 0}, c[2] = {0, 0};
+  for (uint32_t s = t; s < kSqSample; s += kSqSampleThreads) {
+    const uint64_t i = (uint64_t)s * n / kSqSample;
+    if (i >= n) break;
+    const uint32_t b = (uint32_t)(kimg<KT>(km, keys[i]) >> (W - 16)) & 0xFFFFu;
+    const int h = b >> 15;
+    o1[h] |= b;
+    o0[h] |= ~b & 0xFFFFu;
+    ++c[h];
+  }
+  for (int h = 0; h < 2; ++h) {
+    if (c[h]) {
+      atomicOr(&s_o1[h], o1[h]);
+      atomicOr(&s_o0[h], o0[h]);
+      atomicAdd(&s_cnt[h], c[h]);
+    }
+  }
+  __syncthreads();
+  if (t != 0) return;
+  const uint32_t total = s_cnt[0] + s_cnt[1];
+  bool any = false;
+  uint64_t hiM[2], loM[2], cst[2];
+  for (int h = 0; h < 2; ++h) {
+    hiM[h] = ~0ull;
+    loM[h] = 0;
+    cst[h] = 0;
+    const uint32_t cm = ~(s_o1[h] & s_o0[h]) & 0x7FFFu;  // bucket bits every sampled key of the half shares
+    if (!s_cnt[h] || !cm) continue;
+    // keys of this half per bucket it can reach
+    const double load = (double)n * s_cnt[h] / total / (double)(1u << (15 - __builtin_popcount(cm)));
+    if (load <= 0.875 * cap) continue;
+    const int bb = 31 - __builtin_clz(cm);
+    const int b = bb + W - 16;
+    hiM[h] = ~((2ull << b) - 1ull);
+    loM[h] = (1ull << b) - 1ull;
+    cst[h] = (uint64_t)((s_o1[h] >> bb) & 1u) << b;
+    any = true;
+  }
+  for (int h = 0; h < 2; ++h) {
+    out->hiM[h] = hiM[h];
+    out->loM[h] = loM[h];
+    out->cst[h] = cst[h];
+  }
+  out->pad = 0;
+  out->on = any ? 1u : 0u;
 }
 
 // ------------------------------------------------------------- plan, rows
@@ -338,7 +426,23 @@ constexpr int kPlanRowThreads = 256;
 // are taken again under it (meta[kMetaRehist]; the flags raised by this plan
 // are cleared for the second one).  Only when some bucket would take the
 // per-bucket fallback (mode 1): an in-capacity plan is kept as it is.
-__device__ __forceinline__ void plan_squeeze(uint32_t* __restrict__ meta, int keyBits) {
+__device__ __forceinline__ void plan_squeeze(uint32_t* __restrict__ meta, int keyBits,
+                                             const SqueezeWords* __restrict__ sample) {
+  SqueezeWords* sq = reinterpret_cast<SqueezeWords*>(meta + kMetaSqueeze);
+  if (sample && sample->on) {
+    // the first histogram ran under the sample's squeeze: keep it (every later
+    // launch reads meta's copy) -- unless a key broke it: histogram again
+    // under the plain map
+    if (load_agent(&meta[kMetaSqViol]) == 0u) {
+      *sq = *sample;
+    } else {
+      meta[kMetaRehist] = 1;
+      meta[kMetaMode] = 0;
+      meta[kMetaFallback] = 0;
+      meta[kMetaBigCount] = 0;
+    }
+    return;
+  }
   if (load_agent(&meta[kMetaMode]) != 1u) return;
   uint64_t hiM[2], loM[2], cst[2];
   bool any = false;
@@ -359,7 +463,6 @@ __device__ __forceinline__ void plan_squeeze(uint32_t* __restrict__ meta, int ke
     }
   }
   if (!any) return;
-  SqueezeWords* sq = reinterpret_cast<SqueezeWords*>(meta + kMetaSqueeze);
   for (int h = 0; h < 2; ++h) {
     sq->hiM[h] = hiM[h];
     sq->loM[h] = loM[h];
@@ -429,7 +532,7 @@ __global__ __launch_bounds__(kPlanRowThreads) void thrs_plan_rows(
     uint32_t* __restrict__ segInfo, uint32_t* __restrict__ segBase, uint32_t tileKeys, uint32_t histGrid,
     uint32_t* __restrict__ segInfoA, uint32_t* __restrict__ segBaseA, uint32_t* __restrict__ bigB, int sqMode,
     int keyBits, uint32_t* __restrict__ bigPos, uint32_t* __restrict__ bigTile, uint4* __restrict__ bigHist,
-    int nLow) {
+    int nLow, const SqueezeWords* __restrict__ sample) {
   if (sqMode == 2 && meta[kMetaRehist] == 0) return;
   __shared__ uint32_t s_w[2][4], s_base, s_b2[kBins], s_sq[3], s_last;
   const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6, r = blockIdx.x;
@@ -498,7 +601,7 @@ __global__ __launch_bounds__(kPlanRowThreads) void thrs_plan_rows(
   __syncthreads();
   if (s_last) {
     __threadfence();
-    if (sqMode == 1 && t == 0) plan_squeeze(meta, keyBits);
+    if (sqMode == 1 && t == 0) plan_squeeze(meta, keyBits, sample);
     __syncthreads();
     if (!(sqMode == 1 && load_agent(&meta[kMetaRehist]) != 0u))
       plan_big_prefix(joint, meta, bigB, bigPos, bigTile, tileKeys, s_w);

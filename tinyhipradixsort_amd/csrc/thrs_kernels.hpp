@@ -94,7 +94,8 @@ template <typename U> struct KeyMap<U, true> {
   uint32_t sh;
   U hiM[2], loM[2], cst[2];
 };
-// the squeeze as thrs_plan_rows writes it (in the bucket path's meta words)
+// the squeeze as thrs_plan_rows (or the sample, thrs_squeeze_sample) writes
+// it: on, and per half the masks and the dropped bit's value (cst)
 struct SqueezeWords {
   uint32_t on, pad;
   uint64_t hiM[2], loM[2], cst[2];
