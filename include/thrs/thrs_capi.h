@@ -65,6 +65,7 @@ enum { THRS_SEG_AUTO = 0, THRS_SEG_TOP_ONLY = 1, THRS_SEG_NONE = 2 };
 enum { THRS_CLAIMS_AUTO = 0, THRS_CLAIMS_XCD_BLOCKS = 1, THRS_CLAIMS_TICKET = 2 };
 enum { THRS_RANK_AUTO = 0, THRS_RANK_ATOMIC = 1, THRS_RANK_BALLOT = 2 };
 enum { THRS_PLANES_AUTO = 0, THRS_PLANES_ON = 1, THRS_PLANES_OFF = 2 };
+enum { THRS_SQUEEZE_AUTO = 0, THRS_SQUEEZE_OFF = 1 };
 typedef struct thrs_options {
   int32_t path;          /* THRS_PATH_*: LSD = one device pass per digit; BUCKET = the
                             3-HBM-pass path wherever the key/value types and window
@@ -102,7 +103,11 @@ typedef struct thrs_options {
                             largest image, is THRS_ERROR_INVALID_VALUE on every
                             sort.  A false promise gives unspecified output.
                             0 = no range.                                          */
-  int32_t reserved;      /* zero */
+  int32_t squeeze;       /* THRS_SQUEEZE_*: float keys on the bucket path may drop a
+                            bucket bit that every key of an image half shares (the
+                            reference's float generator clears one, unittest.cpp:103,
+                            108); AUTO = when the buckets would overflow, OFF = never.
+                            Same bytes either way.                                   */
   uint64_t rangeLo;
   uint64_t rangeHi;
 } thrs_options;

@@ -365,7 +365,8 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   // the device-chosen squeeze (float keys over the whole key, single-bucket
   // chunks: thrs_plan_rows; KeyMap<U, true> in thrs_kernels.hpp)
   // (both top passes segmented: the squeeze-aware pass kernel)
-  const bool squeeze = kSqueezable<KT> && bucket && P.fullWindow && !local32 && P.segA;
+  const bool squeeze = kSqueezable<KT> && bucket && P.fullWindow && !local32 && P.segA &&
+                       opt.squeeze == THRS_SQUEEZE_AUTO;
   const SqueezeWords* sqw =
       squeeze ? reinterpret_cast<const SqueezeWords*>(scratch + plan.hybridOff + kMetaOff + kMetaSqueeze * 4) : nullptr;
   SqueezeWords* sample = squeeze ? reinterpret_cast<SqueezeWords*>(scratch + plan.hybridOff + kSampleOff) : nullptr;
