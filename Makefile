@@ -9,7 +9,9 @@ ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -fvisibility=hidden -Iinclude -Wall -Wno-unused-result -Wno-unused-function
 PKG := tinyhipradixsort_amd
 CSRC := $(PKG)/csrc
-KSRC := $(CSRC)/thrs_host.hpp $(CSRC)/thrs_kernels.hpp $(CSRC)/thrs_hybrid.hpp include/thrs/thrs_capi.h
+KSRC := $(CSRC)/thrs_host.hpp $(CSRC)/thrs_kernels.hpp $(CSRC)/thrs_hybrid.hpp $(CSRC)/thrs_fallback.hpp \
+        $(CSRC)/thrs_pipe.hpp include/thrs/thrs_capi.h
+.DEFAULT_GOAL := all
 KTS := 0 1 2 3
 
 # one object set per build flavour: $(1) = directory, $(2) = extra flags

@@ -53,6 +53,7 @@ def main():
     ap.add_argument("--iota", action="store_true",
                     help="keys = 0..n-1 (u32): every pass sees exactly T/256 keys per digit per tile")
     ap.add_argument("--nocheck", default="", help="comma list of EXPERIMENT variants whose output is knowingly wrong")
+    ap.add_argument("--no-main", action="store_true", help="time only the named variants (per-library rocprof runs)")
     ap.add_argument("variants", nargs="*")
     a = ap.parse_args()
     kt, vb, n = WL[a.workload]
@@ -60,7 +61,7 @@ def main():
     kb = 4 if kt in (0, 2) else 8
     paths = [os.path.join(ROOT, "exp", "variants", f"libthrs_{v}.so") for v in a.variants] if a.variants else \
         sorted(glob.glob(os.path.join(ROOT, "exp", "variants", "libthrs_*.so")))
-    paths = [T.LIB_PATH] + [p for p in paths if os.path.exists(p)]
+    paths = ([] if a.no_main else [T.LIB_PATH]) + [p for p in paths if os.path.exists(p)]
     libs = [(os.path.basename(p)[len("libthrs"):-3].lstrip("_") or "main", load(p)) for p in paths]
     cfg = T._CConfig(1, kt, {0: 0, 4: 0, 8: 1, 16: 2}[vb], 0)
     tmp_bytes = 0

@@ -77,10 +77,11 @@ def test_temporary_buffer_layout(kt, vt, n):
     # scratch (look-back status words) stays a modest fraction of the payload
     # (the reference's pSum region is 4*256*ceil(n/2048) = n/2 bytes, hpp:839),
     # plus a fixed ~1.1 MiB: the 3-pass path's bucket histogram and chunk table
-    # and the segmented pass's extra look-back rows; u32 keys: + the bucket
-    # path's u8 plane (n bytes: its two u16 planes fill keyOut), reserved only
-    # where the default takes that path (n in [2^28, 2^31 + 2^25])
-    plane = -(-n // 256) * 256 if kt == T.KeyType.U32 and (1 << 28) <= n <= (1 << 31) + (1 << 25) else 0
+    # and the segmented pass's extra look-back rows; u32 / f32 keys: + the
+    # bucket path's u8 plane (n bytes: its two u16 planes fill keyOut),
+    # reserved only where the default takes that path (n in [150M, 2^31 + 2^25])
+    plane = -(-n // 256) * 256 if kt in (T.KeyType.U32, T.KeyType.F32) and 150000000 <= n <= (1 << 31) + (1 << 25) \
+        else 0
     if n >= (1 << 20):
         assert d.pSumBuffer < 0.3 * d.keyOutBuffer + plane + (3 << 20) // 2
 
@@ -142,7 +143,15 @@ def test_path_info_matches_the_configs():
     c3 = info(U32, T.ValueType.U32, 1 << 30, True)
     assert (c3["path"], c3["local"]) == ("bucket", "thrs_local_pairs")
     c4 = info(F32, T.ValueType.U32, 1 << 28, False)
-    assert (c4["path"], c4["local"], c4["planes"], c4["local_cap"]) == ("bucket", "thrs_local16", False, 9216)
+    assert (c4["path"], c4["local"], c4["planes"], c4["local_cap"]) == ("bucket", "thrs_local16", True, 9216)
+    assert c4["min_bytes"] == (4 + 7 + 5 + 6) * (1 << 28)
+    # the lower bounds of the default's bucket window (docs/EXPERIMENTS.md row 87)
+    assert info(U32, T.ValueType.U32, 149999999, False)["path"] == "lsd"
+    assert info(U32, T.ValueType.U32, 150000000, False)["path"] == "bucket"
+    assert info(U32, T.ValueType.U32, 150000000, False)["planes"]
+    assert info(U32, T.ValueType.U32, 99999999, True)["path"] == "lsd"
+    assert info(U32, T.ValueType.U32, 100000000, True)["path"] == "bucket"
+    assert info(U64, T.ValueType.U32, (1 << 28) - 1, False)["path"] == "lsd"
     c5 = info(U64, T.ValueType.U64, 1 << 30, True)
     assert (c5["path"], c5["local"], c5["local_cap"]) == ("bucket", "thrs_local_kv", 17408)
     wide = info(U32, T.ValueType.U128, 1 << 30, True)

@@ -821,3 +821,44 @@ def test_reference_float_generator_stays_local(gpu, kt, vb, n):
         r = TU.check_pairs(kt, vb, orig, keys, vals, n, 0, kb * 8)
         assert r["gather_mismatch"] == 0 and r["unstable"] == 0
         assert (r["index_sum"], r["index_xor"]) == TU.expected_index_fingerprint(n)
+
+
+@pytest.mark.parametrize("desc", [False, True])
+@pytest.mark.parametrize("zeros", ["plus_only", "few_signed", "many_signed"])
+def test_f32_planes_signed_zeros(gpu, zeros, desc):
+    """f32 keys-only at 2^28 (the default bucket path with the image planes:
+    the top-digit passes carry 3 + 2 bytes of each key's image, not the key).
+    -0 and +0 share one image (kernel.cu:46-69's getKeyBits), so the planes
+    lose the zeros' signs: the bucket histogram logs up to 1024 zero keys with
+    their positions (thrs_local16 restores the signs in their stable order,
+    mode 0), and with more zeros than that a -0 sends the sort through the
+    whole-key passes (mode 3).  +0 only: nothing to restore (mode 0).
+    Checked on the GPU: sortedness, the raw-bit multiset, and the zeros' raw
+    bits in input order."""
+    torch = gpu
+    from tinyhipradixsort_amd import testutil as TU
+    n = 1 << 28
+    keys = torch.empty(4 * n, dtype=torch.uint8, device="cuda")
+    TU.fill_keys(2, keys, n, start=77 + int(desc))
+    k32 = keys.view(torch.int32)
+    k32[(k32 & 0x7FFFFFFF) == 0] = 1                      # the generator's own zeros, if any
+    # 700 zeros fit the zero log, 3000 do not; either way the zeros' bucket
+    # (4096 keys on average at 2^28) stays within its local sort (9216 keys)
+    step = n // (700 if zeros == "few_signed" else 3000) + 1
+    idx = torch.arange(5, n, step, device="cuda")
+    k32[idx] = 0
+    if zeros != "plus_only":
+        k32[idx[1::3]] = -(1 << 31)
+    zin = k32[(k32 & 0x7FFFFFFF) == 0].clone()
+    fp = TU.fingerprint(2, keys, n)
+    rs = make_sorter(2, 0, desc)
+    tmp = torch.empty(rs.getTemporaryBufferBytes(n).getTemporaryBufferBytesForSortKeys(), dtype=torch.uint8,
+                      device="cuda")
+    rs.sortKeys(keys, n, tmp, 0, 32)
+    torch.cuda.synchronize()
+    rs.checkDeviceError(tmp)
+    assert rs.debugBucketMode(tmp, n, False) == ((3, 0) if zeros == "many_signed" else (0, 0))
+    assert TU.count_unsorted(2, keys, n, 0, 32, descending=desc) == 0
+    assert TU.fingerprint(2, keys, n) == fp
+    zout = k32[(k32 & 0x7FFFFFFF) == 0]
+    assert torch.equal(zout, zin)

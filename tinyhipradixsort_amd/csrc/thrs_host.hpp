@@ -30,6 +30,7 @@
 #include "thrs_kernels.hpp"
 #include "thrs_hybrid.hpp"
 #include "thrs_fallback.hpp"
+#include "thrs_pipe.hpp"
 
 namespace thrs_host {
 using namespace thrs_dev;
@@ -37,8 +38,14 @@ using namespace thrs_dev;
 #ifndef THRS_SEG_MERGE
 #define THRS_SEG_MERGE 0  // experiment: see thrs_pass_seg ALT
 #endif
+#ifndef THRS_SEG_PIPE
+#define THRS_SEG_PIPE 0  // experiment: 4-byte keys-only top-digit passes software-pipelined (thrs_pipe.hpp)
+#endif
 
 constexpr uint64_t kAlign = 256;
+// the bucket path's lower bounds (default path; docs/EXPERIMENTS.md row 87)
+constexpr uint64_t kBucketMinKeys4 = 150000000ull;   // 4-byte keys without values
+constexpr uint64_t kBucketMinPairs4 = 100000000ull;  // 4-byte keys with 4-byte values
 constexpr uint64_t kHistOff = 0;                       // u32 [8][256]
 constexpr uint64_t kBaseOff = 8 * 256 * 4;             // u32 [8][256]
 constexpr uint64_t kCounterOff = 2 * 8 * 256 * 4;      // u32 [8]
@@ -68,6 +75,11 @@ inline uint64_t tile_keys(int kb, int vb) {
   }
 }
 
+
+// keys per tile of the bucket path's segmented passes
+inline uint64_t seg_tile_keys(int kb, int vb) {
+  return (THRS_SEG_PIPE && kb == 4 && vb == 0) ? PipeGeom::TILE : tile_keys(kb, vb);
+}
 
 struct Plan {
   int kb, vb;         // key / value bytes (vb = 0 for sortKeys)
@@ -112,7 +124,8 @@ constexpr uint64_t kSegBaseAOff = kSegInfoAOff + 512;
 constexpr uint64_t kBigBOff = kSegBaseAOff + kSegs * 256 * 4;
 constexpr uint64_t kBigPosOff = kBigBOff + round_up_c((kBuckets + 1) * 4, 256);
 constexpr uint64_t kBigTileOff = kBigPosOff + round_up_c((kBuckets + 1) * 4, 256);
-constexpr uint64_t kHybridBytes = kBigTileOff + round_up_c((kBuckets + 1) * 4, 256);
+constexpr uint64_t kZeroLogOff = kBigTileOff + round_up_c((kBuckets + 1) * 4, 256);  // f32: +-0 keys (thrs_hist_joint)
+constexpr uint64_t kHybridBytes = kZeroLogOff + round_up_c(kZeroLogCap * 4, 256);
 // the smallest local-sort capacity (LocSmall): a big chunk holds more keys
 constexpr uint64_t kMinLocalCap = LocSmall::CAP;
 // tile ids of the segmented pass: each of the 8 segments adds at most two
@@ -133,9 +146,12 @@ inline Plan make_plan(int keyType, int valueBytesOrZero, uint32_t n) {
   // status rows: a tile id per tile, + the segmented passes' extra ids (each
   // segment rounds up to a look-back group) or the fallback's (a partial tile
   // per big chunk; the fallback passes use the same two table sets)
-  const uint64_t rows = p.nTiles + std::max<uint64_t>(kSegTilePad, p.bigMax);
+  // (the segmented passes may use smaller tiles: seg_tile_keys)
+  const uint64_t segTiles = std::max<uint64_t>(p.nTiles, ((uint64_t)n + seg_tile_keys(p.kb, p.vb) - 1) /
+                                                             seg_tile_keys(p.kb, p.vb));
+  const uint64_t rows = segTiles + std::max<uint64_t>(kSegTilePad, p.bigMax);
   p.statusBytes = round_up(rows * kBins * (p.wideStatus ? 8 : 4), kAlign);
-  p.statusUsedBytes = round_up((p.nTiles + kSegTilePad) * kBins * (p.wideStatus ? 8 : 4), kAlign);
+  p.statusUsedBytes = round_up((segTiles + kSegTilePad) * kBins * (p.wideStatus ? 8 : 4), kAlign);
   const uint64_t nGroups = kGroup > 0 ? (rows + kGroup - 1) / kGroup : 0;
   p.gaBytes = round_up(nGroups * kBins * 4, kAlign);
   p.gpBytes = round_up(nGroups * kBins * (p.wideStatus ? 8 : 4), kAlign);
@@ -148,10 +164,11 @@ inline Plan make_plan(int keyType, int valueBytesOrZero, uint32_t n) {
   // the u8 plane of the planes codecs (thrs_kernels.hpp kCodecSplit): the u16
   // planes fill keyOut, which is all a sortKeys caller must allocate
   // (getTemporaryBufferBytesForSortKeys = pSumBuffer + keyOutBuffer).  Only
-  // where the default takes the bucket path with planes (u32 keys-only, n in
-  // [2^28, 2^31 + 2^25]); a forced bucket path elsewhere runs without them.
+  // where the default takes the bucket path with planes (u32 / f32 keys-only,
+  // n in [kBucketMinKeys4, 2^31 + 2^25]); a forced bucket path elsewhere runs
+  // without them.
   p.hiPlaneOff = p.scratchBytes;
-  if (keyType == THRS_KEY_U32 && valueBytesOrZero == 0 && (uint64_t)n >= (1ull << 28) &&
+  if ((keyType == THRS_KEY_U32 || keyType == THRS_KEY_F32) && valueBytesOrZero == 0 && (uint64_t)n >= kBucketMinKeys4 &&
       (uint64_t)n <= (1ull << 31) + (1ull << 25))
     p.scratchBytes += round_up(n, kAlign);
   return p;
@@ -230,7 +247,8 @@ PathSel select_path(uint32_t n, int startBits, int nPass, const thrs_options& op
   const bool fullWindow = startBits == 0 && nPass * 8 >= (int)(8 * sizeof(U));
   // Size window of the default (uniform keys: n / 65536 keys per bucket;
   // docs/EXPERIMENTS.md row 29): the local sort costs about the same per chunk
-  // whatever its size, so below 2^28 the two passes it replaces are cheaper;
+  // whatever its size, so below ~1.5e8 keys (1e8 pairs, 2^28 for the other
+  // types) the two passes it replaces are cheaper;
   // above 2^30 + 2^26 the largest of 65536 uniform buckets (mean + ~4.5 sigma)
   // outgrows the chunk capacity and big chunks would take the per-bucket
   // fallback.  THRS_PATH_BUCKET forces the path for any n (tests).
@@ -243,7 +261,12 @@ PathSel select_path(uint32_t n, int startBits, int nPass, const thrs_options& op
   // buckets are uniform whatever the global distribution) takes the bucket
   // path from 2^27 (C2's 2^30 keys over 8 GPUs; docs/EXPERIMENTS.md row 84)
   const bool rangedReq = opt.keyRange == 1 && fullWindow && !counts;
-  const uint64_t minN = rangedReq ? (1ull << 27) : (1ull << 28);
+  // lower bounds by measurement (docs/EXPERIMENTS.md row 87): 4-byte keys
+  // alone from 150M keys, with 4-byte values from 100M, the rest from 2^28
+  const uint64_t minN = rangedReq ? (1ull << 27)
+                        : kKeys4  ? kBucketMinKeys4
+                        : (KB == 4 && VB == 4) ? kBucketMinPairs4
+                                               : (1ull << 28);
   const bool sizeOk = nn >= minN && nn <= (1ull << 30) + (kKV ? (1ull << 24) : (1ull << 26));
   const bool wideOk = kKeys4 && fullWindow && nn > (1ull << 30) + (1ull << 26) && nn <= (1ull << 31) + (1ull << 25);
   // the local geometry follows the keys per USED bucket: a range whose span
@@ -280,11 +303,12 @@ PathSel select_path(uint32_t n, int startBits, int nPass, const thrs_options& op
   const bool local32 = kKeys4 && bucket && !local16;
   const bool segTop = opt.segmented != THRS_SEG_NONE;
   const bool segA = opt.segmented == THRS_SEG_AUTO;
-  // u32 local16 with both top-digit passes segmented: the passes carry the
-  // keys as planes (thrs_kernels.hpp kCodecSplit / kCodecPlanes): keyOut (4n
-  // bytes) = lo u16[n] | lo2 u16[n], the u8 plane hi[n] at the end of the
-  // scratch (f32: the local sort needs the input's -0 bits)
-  const bool planes = local16 && KT == 0 && segA && opt.planes != THRS_PLANES_OFF &&
+  // u32 / f32 local16 with both top-digit passes segmented: the passes carry
+  // the keys' IMAGES as planes (thrs_kernels.hpp kCodecSplit / kCodecPlanes):
+  // keyOut (4n bytes) = lo u16[n] | lo2 u16[n], the u8 plane hi[n] at the end
+  // of the scratch.  f32: -0 and +0 share one image, so a plan that saw a -0
+  // key (thrs_hist_joint) runs the whole-key passes instead (mode 3)
+  const bool planes = local16 && (KT == 0 || KT == 2) && segA && opt.planes != THRS_PLANES_OFF &&
                       plan.scratchBytes - plan.hiPlaneOff >= (uint64_t)n;
   // the local sort's chunk capacity (a bigger bucket is a big chunk)
   const uint32_t cap = kKV ? LocKV::CAP
@@ -370,6 +394,8 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   const SqueezeWords* sqw =
       squeeze ? reinterpret_cast<const SqueezeWords*>(scratch + plan.hybridOff + kMetaOff + kMetaSqueeze * 4) : nullptr;
   SqueezeWords* sample = squeeze ? reinterpret_cast<SqueezeWords*>(scratch + plan.hybridOff + kSampleOff) : nullptr;
+  // f32 with the image planes: the zero log (+-0 keys' positions and signs)
+  uint32_t* zeroLog = (KT == 2 && planes) ? reinterpret_cast<uint32_t*>(scratch + plan.hybridOff + kZeroLogOff) : nullptr;
   KeyMap<U> km{orderMask, (U)0, 0u};
   if (ranged) {
     const U span = (U)opt.rangeHi - (U)opt.rangeLo;  // > 0 (sort_impl returns at once for 0)
@@ -392,15 +418,30 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   auto kernelBig = atomicRank ? thrs_pass_big<KT, VB, ST, true> : thrs_pass_big<KT, VB, ST, false>;
   auto kernel = useXb ? kernelXb : (atomicRank ? thrs_pass<KT, VB, ST, true> : thrs_pass<KT, VB, ST, false>);
   auto sk = atomicRank ? thrs_pass_seg<KT, VB, ST, true> : thrs_pass_seg<KT, VB, ST, false>;
-  // plane codecs (u32 keys-only instantiations only; `planes` is false elsewhere)
-  auto skSplit = atomicRank ? thrs_pass_seg<KT, VB, ST, true, (KT == 0 && VB == 0) ? kCodecSplit : kCodecKeys>
-                            : thrs_pass_seg<KT, VB, ST, false, (KT == 0 && VB == 0) ? kCodecSplit : kCodecKeys>;
-  auto skPlanes = atomicRank ? thrs_pass_seg<KT, VB, ST, true, (KT == 0 && VB == 0) ? kCodecPlanes : kCodecKeys>
-                             : thrs_pass_seg<KT, VB, ST, false, (KT == 0 && VB == 0) ? kCodecPlanes : kCodecKeys>;
+  // plane codecs (u32 / f32 keys-only instantiations only; `planes` is false
+  // elsewhere).  The planes codec reads images (identity map): the u32 kernel
+  // serves both key types.
+  constexpr bool kPlanes4 = (KT == 0 || KT == 2) && VB == 0;
+  constexpr int kPlaneKT = kPlanes4 ? 0 : KT;
+  auto skSplit = atomicRank ? thrs_pass_seg<KT, VB, ST, true, kPlanes4 ? kCodecSplit : kCodecKeys>
+                            : thrs_pass_seg<KT, VB, ST, false, kPlanes4 ? kCodecSplit : kCodecKeys>;
+  auto skPlanes = atomicRank ? thrs_pass_seg<kPlaneKT, VB, ST, true, kPlanes4 ? kCodecPlanes : kCodecKeys>
+                             : thrs_pass_seg<kPlaneKT, VB, ST, false, kPlanes4 ? kCodecPlanes : kCodecKeys>;
   // THRS_SEG_MERGE: the plane codecs and their whole-key alternative (mode 1)
   // in one launch each (thrs_pass_seg ALT)
+  // THRS_SEG_PIPE: the pipelined segmented pass (u32 / f32 keys without values)
+  constexpr bool kPipe = THRS_SEG_PIPE && (KT == 0 || KT == 2) && VB == 0;
+  constexpr int kPipeKT = kPipe ? KT : 0;  // (instantiated for u32 / f32 only)
+  auto pipeKeys = atomicRank ? thrs_pass_seg_pipe<kPipeKT, ST, true, kCodecKeys>
+                             : thrs_pass_seg_pipe<kPipeKT, ST, false, kCodecKeys>;
+  auto pipeSplit = atomicRank ? thrs_pass_seg_pipe<kPipeKT, ST, true, kCodecSplit>
+                              : thrs_pass_seg_pipe<kPipeKT, ST, false, kCodecSplit>;
+  auto pipePlanes = atomicRank ? thrs_pass_seg_pipe<0, ST, true, kCodecPlanes>
+                               : thrs_pass_seg_pipe<0, ST, false, kCodecPlanes>;
+  const uint32_t segTileKeys = (uint32_t)seg_tile_keys(KB, VB);
   // (other key / value types: the plain keys kernel, never launched merged)
-  constexpr int kAltM = (KT == 0 && VB == 0 && THRS_SEG_MERGE) ? kCodecKeys : -1;
+  constexpr bool kMerge = THRS_SEG_MERGE && KT == 0 && VB == 0;  // (u32 only)
+  constexpr int kAltM = kMerge ? kCodecKeys : -1;
   auto skSplitM = atomicRank ? thrs_pass_seg<KT, VB, ST, true, (KT == 0 && VB == 0) ? kCodecSplit : kCodecKeys, kAltM>
                              : thrs_pass_seg<KT, VB, ST, false, (KT == 0 && VB == 0) ? kCodecSplit : kCodecKeys, kAltM>;
   auto skPlanesM = atomicRank
@@ -417,6 +458,10 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
       return THRS_ERROR_HIP;
     if (planes && (allow_lds(skSplit, lds) != hipSuccess || allow_lds(skPlanes, lds) != hipSuccess ||
                    allow_lds(skSplitM, lds) != hipSuccess || allow_lds(skPlanesM, lds) != hipSuccess))
+      return THRS_ERROR_HIP;
+    if (kPipe && (allow_lds(pipeKeys, PipeGeom::LDS_BYTES) != hipSuccess ||
+                  allow_lds(pipeSplit, PipeGeom::LDS_BYTES) != hipSuccess ||
+                  allow_lds(pipePlanes, PipeGeom::LDS_BYTES) != hipSuccess))
       return THRS_ERROR_HIP;
     if constexpr (kKV) {
       if (allow_lds(atomicRank ? thrs_local_kv<KT, VB, true> : thrs_local_kv<KT, VB, false>, LocKV::LDS) != hipSuccess)
@@ -514,7 +559,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
         hipLaunchKernelGGL(thrs_hist_joint<KT>, dim3(hgrid), dim3(kHistThreads), kJointLds, stream,
                          static_cast<const U*>(keys), n, km, startBits + 8 * nLow, vec, joint,
                          reinterpret_cast<uint32_t*>(hyb + kSegHistAOff), reinterpret_cast<uint32_t*>(hyb + kRowHistOff),
-                         tables, meta, sample);
+                         tables, meta, sample, zeroLog);
       }
       // single-bucket chunks: one workgroup per top digit; float keys with
       // the whole key decide the squeeze (sqMode 1) and, if it went on,
@@ -525,7 +570,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                            reinterpret_cast<const uint32_t*>(hyb + jOff), reinterpret_cast<const uint32_t*>(hyb + rOff),
                            reinterpret_cast<const uint32_t*>(hyb + sOff), n, cap, base + nLow * kBins,
                            chunkOff, chunkB0, meta, reinterpret_cast<uint32_t*>(hyb + kSegInfoOff),
-                           reinterpret_cast<uint32_t*>(hyb + kSegBaseOff), (uint32_t)G::TILE, (uint32_t)hgrid,
+                           reinterpret_cast<uint32_t*>(hyb + kSegBaseOff), segTileKeys, (uint32_t)hgrid,
                            reinterpret_cast<uint32_t*>(hyb + kSegInfoAOff), reinterpret_cast<uint32_t*>(hyb + kSegBaseAOff),
                            reinterpret_cast<uint32_t*>(hyb + kBigBOff), sqMode, 8 * KB,
                            reinterpret_cast<uint32_t*>(hyb + kBigPosOff), reinterpret_cast<uint32_t*>(hyb + kBigTileOff),
@@ -539,7 +584,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
           hipLaunchKernelGGL((thrs_hist_joint<KT, true>), dim3(hgrid), dim3(kHistThreads), kJointLds, stream,
                              static_cast<const U*>(keys), n, km, startBits + 8 * nLow, vec,
                              reinterpret_cast<uint32_t*>(hyb + kJoint2Off), reinterpret_cast<uint32_t*>(hyb + kSegHistA2Off),
-                             reinterpret_cast<uint32_t*>(hyb + kRowHist2Off), ZeroRanges{}, meta, sqw);
+                             reinterpret_cast<uint32_t*>(hyb + kRowHist2Off), ZeroRanges{}, meta, sqw, nullptr);
         }
         plan_rows(2, kJoint2Off, kSegHistA2Off, kRowHist2Off);
       } else if (!local32) {
@@ -550,7 +595,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
         hipLaunchKernelGGL(thrs_plan, dim3(1), dim3(kPlanThreads), 0, stream, joint, n, base + nLow * kBins, chunkOff,
                            chunkB0, meta, cap, smallLocal ? kLocSmallLogT : kLocLogT,
                            reinterpret_cast<uint32_t*>(hyb + kSegInfoOff), reinterpret_cast<uint32_t*>(hyb + kSegBaseOff),
-                           (uint32_t)G::TILE, reinterpret_cast<const uint32_t*>(hyb + kSegHistAOff), (uint32_t)hgrid,
+                           segTileKeys, reinterpret_cast<const uint32_t*>(hyb + kSegHistAOff), (uint32_t)hgrid,
                            reinterpret_cast<uint32_t*>(hyb + kSegInfoAOff), reinterpret_cast<uint32_t*>(hyb + kSegBaseAOff),
                            reinterpret_cast<uint32_t*>(hyb + kBigBOff));
       }
@@ -623,6 +668,14 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     auto launch_seg = [&](int p, U* kin, U* kout, VW* vin, VW* vout, uint64_t infoOff, uint64_t baseOff,
                           const uint32_t* gate, uint32_t gateMask, int codec = kCodecKeys) {
       ProfScope prof(stream, 1, THRS_PK_PASS_SEG, moveBytes);
+      if constexpr (kPipe) {
+        auto pk = codec == kCodecSplit ? pipeSplit : codec == kCodecPlanes ? pipePlanes : pipeKeys;
+        hipLaunchKernelGGL(pk, dim3((uint32_t)cu_count()), dim3(PipeGeom::THREADS), PipeGeom::LDS_BYTES, stream,
+                           kin, kout, codec == kCodecPlanes ? kid : km, codec == kCodecPlanes ? 16 : startBits + 8 * p,
+                           reinterpret_cast<uint32_t*>(hyb + infoOff), reinterpret_cast<const uint32_t*>(hyb + baseOff),
+                           status[p & 1], err, grp[p & 1], gate, gateMask, hiP, sqw);
+        return;
+      }
       auto kern = codec == kCodecSplit ? skSplit : codec == kCodecPlanes ? skPlanes : sk;
       // kCodecPlanes: image-space input (identity map), digit at bits 16-23 of k'
       hipLaunchKernelGGL(kern, dim3((uint32_t)segPerCU * cu_count()), dim3(G::THREADS), lds, stream, kin, kout, vin,
@@ -656,17 +709,17 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     if (segA) {
       // Both table sets are clean (zeroed up front); the segmented passes'
       // extra tile ids (rows past nTiles) are touched by nothing else.
-      if (planes && THRS_SEG_MERGE) {
+      if (planes && kMerge) {
         launch_seg_merged(nLow, false);
       } else if (planes) {
         launch_seg(nLow, K, reinterpret_cast<U*>(loP), V, valOut, kSegInfoAOff, kSegBaseAOff, mode, kGateMode0,
                    kCodecSplit);
-        launch_seg(nLow, K, keyOut, V, valOut, kSegInfoAOff, kSegBaseAOff, mode, kGateMode1);
+        launch_seg(nLow, K, keyOut, V, valOut, kSegInfoAOff, kSegBaseAOff, mode, kGateMode1 | kGateMode3);
       } else {
-        launch_seg(nLow, K, keyOut, V, valOut, kSegInfoAOff, kSegBaseAOff, mode, kGateMode0 | kGateMode1);
+        launch_seg(nLow, K, keyOut, V, valOut, kSegInfoAOff, kSegBaseAOff, mode, kGateMode0 | kGateMode1 | kGateMode3);
       }
     } else {
-      launch_pass(nLow, K, keyOut, V, valOut, mode, kGateMode0 | kGateMode1);
+      launch_pass(nLow, K, keyOut, V, valOut, mode, kGateMode0 | kGateMode1 | kGateMode3);
       // the segmented pass's tile ids reach past nTiles (per-segment
       // rounding): clear those rows (pass nLow cleared rows [0, nTiles))
       const uint64_t nGroups0 = (plan.nTiles + kGroup - 1) / kGroup;
@@ -678,16 +731,16 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                          stream) != hipSuccess)
         return THRS_ERROR_HIP;
     }
-    if (planes && THRS_SEG_MERGE) {
+    if (planes && kMerge) {
       launch_seg_merged(nLow + 1, true);
-    } else if (planes) {  // mode 0: planes -> lo2; mode 1 (big chunks): keys
+    } else if (planes) {  // mode 0: planes -> lo2; mode 1 (big chunks) / 3 (f32 -0): keys
       launch_seg(nLow + 1, reinterpret_cast<U*>(loP), reinterpret_cast<U*>(lo2P), valOut, V, kSegInfoOff, kSegBaseOff,
                  mode, kGateMode0, kCodecPlanes);
-      launch_seg(nLow + 1, keyOut, K, valOut, V, kSegInfoOff, kSegBaseOff, mode, kGateMode1);
+      launch_seg(nLow + 1, keyOut, K, valOut, V, kSegInfoOff, kSegBaseOff, mode, kGateMode1 | kGateMode3);
     } else if (segTop)
-      launch_seg(nLow + 1, keyOut, K, valOut, V, kSegInfoOff, kSegBaseOff, mode, kGateMode0 | kGateMode1);
+      launch_seg(nLow + 1, keyOut, K, valOut, V, kSegInfoOff, kSegBaseOff, mode, kGateMode0 | kGateMode1 | kGateMode3);
     else
-      launch_pass(nLow + 1, keyOut, K, valOut, V, mode, kGateMode0 | kGateMode1);
+      launch_pass(nLow + 1, keyOut, K, valOut, V, mode, kGateMode0 | kGateMode1 | kGateMode3);
     {
       ProfScope prof(stream, 2,
                      kKV ? THRS_PK_LOCAL_KV
@@ -720,7 +773,8 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
           using LG = decltype(geom);
           auto lk = atomicRank ? thrs_local16<KT, true, LG> : thrs_local16<KT, false, LG>;
           hipLaunchKernelGGL(lk, lgrid, dim3(LG::THREADS), LG::LDS, stream, reinterpret_cast<uint32_t*>(K), km32,
-                             chunkOff, chunkB0, meta, planes ? static_cast<const uint16_t*>(lo2P) : nullptr, sqw);
+                             chunkOff, chunkB0, meta, planes ? static_cast<const uint16_t*>(lo2P) : nullptr, sqw,
+                             zeroLog);
         };
         auto launch32 = [&](auto geom) {
           using LG = decltype(geom);

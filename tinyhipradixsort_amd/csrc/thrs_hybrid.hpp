@@ -43,7 +43,11 @@ constexpr uint32_t kBuckets = 65536;  // 16-bit bucket = the window's top two di
 // meta[kMetaMode]: 0 = local path (no bucket above the local capacity);
 // 1 = some big chunks (the per-bucket fallback, thrs_fallback.hpp); 2 = ONE
 // bucket holds every key, so both top digits are constant and their passes
-// are identities (skipped).  meta[kMetaBigCount]: big chunks listed in bigB.
+// are identities (skipped); 3 = as 0, but the top-digit passes move whole
+// keys, not the image planes (f32 keys-only with planes: -0 and +0 share one
+// image, so the planes lose the zeros' signs; up to kZeroLogCap zero keys the
+// zero log restores them, past that a -0 key means mode 3).
+// meta[kMetaBigCount]: big chunks listed in bigB.
 // The fallback's own words follow (thrs_fallback.hpp).
 enum {
   kMetaChunks = 0,
@@ -63,11 +67,17 @@ enum {
   kMetaBigHalf = 38,    // [2]: per image half, buckets above the local capacity
   kMetaPlanDone2 = 40,  // the squeezed plan's finished workgroups
   kMetaSqViol = 41,     // a key broke the sampled squeeze (its dropped bit differs): histogram again, plain
+  kMetaNegZero = 42,    // f32: some key is -0 (thrs_hist_joint)
+  kMetaZeroCount = 43,  // f32: keys that are +-0 (their first kZeroLogCap positions in the zero log)
   kMetaSqueeze = 48,    // SqueezeWords (14 words, to 61)
 };
 static_assert(kMetaSqueeze * 4 + sizeof(SqueezeWords) <= 256, "meta is 64 words");
 // gate masks of the gated launches: bit v set = run when the gate word is v
-constexpr uint32_t kGateMode0 = 1u << 0, kGateMode1 = 1u << 1, kGateMode2 = 1u << 2;  // on meta[kMetaMode]
+constexpr uint32_t kGateMode0 = 1u << 0, kGateMode1 = 1u << 1, kGateMode2 = 1u << 2,
+                   kGateMode3 = 1u << 3;  // on meta[kMetaMode]
+// f32 zero log (thrs_hist_joint -> thrs_local16): input position | sign << 31
+// of the first kZeroLogCap keys that are +0 or -0
+constexpr uint32_t kZeroLogCap = 1024;
 
 // ------------------------------------------------------------ joint histogram
 // LDS: bucket counts as 15-bit fields, two per word (bits 0-14 | guard 15 |
@@ -115,7 +125,8 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
                                                                 uint32_t* __restrict__ segHist /* [8][256] */,
                                                                 uint32_t* __restrict__ rowHist /* [256] */,
                                                                 ZeroRanges tables, uint32_t* __restrict__ meta,
-                                                                const SqueezeWords* __restrict__ sq) {
+                                                                const SqueezeWords* __restrict__ sq,
+                                                                uint32_t* __restrict__ zeroLog) {
   using U = typename KeyTraits<KT>::U;
   if constexpr (SECOND) {
     if (meta[kMetaRehist] == 0) return;
@@ -146,7 +157,25 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
   uint32_t* segH = segHist + (blockIdx.x * kSegs / gridDim.x) * kBins;
 
   const uint32_t lane = tid & 63;
+  // f32 (first histogram, zeroLog set: the image planes): keys that are +0
+  // or -0 share one image, so the planes lose their signs.  Each wave notes
+  // (a ballot, scalar registers) whether an iteration met any; only then are
+  // that iteration's keys read again and the zeros logged with their
+  // positions (zero_log), and a -0 flagged.
+  constexpr bool kZeros = KT == 2 && !SECOND;
+  uint64_t zany = 0;
+  bool zfull = false;  // (this thread saw the log full: only the -0 flag from then on)
+  auto log_zero = [&](U k, uint64_t pos) {
+    if ((k & (U)0x7FFFFFFFu) != 0) return;
+    const bool neg = k != 0;
+    if (neg) atomicOr(&meta[kMetaNegZero], 1u);
+    if (zfull) return;
+    const uint32_t slot = atomicAdd(&meta[kMetaZeroCount], 1u);
+    if (slot < kZeroLogCap) zeroLog[slot] = (uint32_t)pos | (neg ? 0x80000000u : 0u);
+    else zfull = true;
+  };
   auto bucket_of = [&](U k) -> uint32_t {
+    if constexpr (kZeros) zany |= __ballot((k & (U)0x7FFFFFFFu) == 0);
     if constexpr (kCheck) {
       const U y0 = ((KeyTraits<KT>::bits(k) ^ km.mask) - km.lo) << km.sh;  // the plain image
       const bool h = (y0 >> (8 * sizeof(U) - 1)) != 0;
@@ -196,7 +225,12 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
   uint64_t tailStart = lo;
   if (vec) {  // 16-byte loads, UN in flight per lane (keys base 16-B aligned, checked on host)
     constexpr int PER = 16 / sizeof(U);
-    constexpr int UN = kHjUnroll;
+    // (the squeeze check's extra registers: two 16-byte loads in flight, not
+    // four, or the 128-VGPR budget spills ~40 registers -- 4x slower)
+#ifndef THRS_HJ_CHECK_UN
+#define THRS_HJ_CHECK_UN 2
+#endif
+    constexpr int UN = kCheck ? THRS_HJ_CHECK_UN : kHjUnroll;
     constexpr uint32_t ITERS_PER_EPOCH = kEpoch / (kHistThreads * UN * PER);
     static_assert(ITERS_PER_EPOCH >= 1, "one iteration must fit an epoch");
     const uint64_t v0 = lo / PER, nv = hi / PER;   // lo is a multiple of 4 (hj_len)
@@ -233,6 +267,22 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
         }
       }
       constexpr int E = UN * PER;
+      if constexpr (kZeros) {
+        if (zany && zeroLog) {  // (rare) this iteration's zeros: read its keys again
+#pragma unroll 1
+          for (int u = 0; u < UN; ++u) {
+            const uint64_t v = i + u * gstride;
+            if (v < nv) {
+              const uint4 x = kv[v];
+              log_zero(x.x, 4 * v);
+              log_zero(x.y, 4 * v + 1);
+              log_zero(x.z, 4 * v + 2);
+              log_zero(x.w, 4 * v + 3);
+            }
+          }
+        }
+        zany = 0;
+      }
       if (v0 + (it + 1) * UN * gstride <= nv) {  // every element of every lane is in the range
         uint32_t b0;
         const uint32_t mode = wave_mode<E>([&](int e) { return b[e]; }, E, b0);
@@ -272,8 +322,12 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
     for (uint64_t it = 0; it < nIter; ++it) {
       const uint64_t i = tailStart + it * gstride + tid;
       if (i < hi) {
-        const uint32_t b = bucket_of(keys[i]);
+        const U k = keys[i];
+        const uint32_t b = bucket_of(k);
         check(b, add(b, 1u), 1u);
+        if constexpr (kZeros) {
+          if (zeroLog) log_zero(k, i);
+        }
       }
       if ((it + 1) % ITERS_PER_EPOCH == 0) lds_barrier();
     }
@@ -338,17 +392,17 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
 
 // ----------------------------------------------------- the sampled squeeze
 // Float keys over the whole key (before the first bucket histogram; one
-// 256-thread workgroup): kSqSample evenly spaced keys give, per image half,
-// the bucket bits that all of them share.  In a half whose keys would
-// overflow the local sort -- its share of n over the 2^(15 - constant bits)
-// buckets it can reach, above 7/8 of the capacity -- the highest such bit is
+// 256-thread workgroup): kSqSample keys (32 evenly spaced runs) give, per
+// image half, the bucket bits that all of them share.  In a half whose keys
+// would overflow the local sort -- its share of n over the 2^(15 - constant
+// bits) buckets it can reach, mean + 4.5 sigma above the capacity -- the highest such bit is
 // dropped (KeyMap<U, true>), so the FIRST histogram already counts the
 // squeezed buckets: the reference's own float generator (the lowest exponent
 // bit cleared, unittest.cpp:103/108) needs one read of the keys, not two.
 // A sample can miss a key that breaks the guess: the histogram checks every
 // key (meta[kMetaSqViol]) and the plan then histograms again, plainly.
 constexpr int kSqSampleThreads = 256;
-constexpr uint32_t kSqSample = 8192;
+constexpr uint32_t kSqSample = 8192;  // keys sampled (kSqSample / 256 runs of 256)
 template <int KT>
 __global__ __launch_bounds__(kSqSampleThreads) void thrs_squeeze_sample(const typename KeyTraits<KT>::U* __restrict__ keys,
                                                                         uint32_t n, KeyMap<typename KeyTraits<KT>::U> km,
@@ -360,10 +414,18 @@ __global__ __launch_bounds__(kSqSampleThreads) void thrs_squeeze_sample(const ty
   if (t < 2) s_o1[t] = s_o0[t] = s_cnt[t] = 0;
   __syncthreads();
   uint32_t o1[2] = {0, 0}, o0[2] = {0, 0}, c[2] = {0, 0};
-  for (uint32_t s = t; s < kSqSample; s += kSqSampleThreads) {
-    const uint64_t i = (uint64_t)s * n / kSqSample;
-    if (i >= n) break;
-    const uint32_t b = (uint32_t)(kimg<KT>(km, keys[i]) >> (W - 16)) & 0xFFFFu;
+  // kSqBlocks runs of kSqSampleThreads consecutive keys, evenly spaced: one
+  // address translation per run (single keys 2^17 apart missed the TLB once
+  // each: ~3 ms at 2^30, docs/EXPERIMENTS.md row 86), loads all in flight
+  constexpr uint32_t kSqBlocks = kSqSample / kSqSampleThreads;
+  U kk[kSqBlocks];
+#pragma unroll
+  for (uint32_t j = 0; j < kSqBlocks; ++j) {
+    const uint64_t i = (uint64_t)j * n / kSqBlocks + t;
+    kk[j] = keys[min(i, (uint64_t)n - 1)];
+  }
+  for (uint32_t j = 0; j < kSqBlocks; ++j) {
+    const uint32_t b = (uint32_t)(kimg<KT>(km, kk[j]) >> (W - 16)) & 0xFFFFu;
     const int h = b >> 15;
     o1[h] |= b;
     o0[h] |= ~b & 0xFFFFu;
@@ -387,9 +449,10 @@ __global__ __launch_bounds__(kSqSampleThreads) void thrs_squeeze_sample(const ty
     cst[h] = 0;
     const uint32_t cm = ~(s_o1[h] & s_o0[h]) & 0x7FFFu;  // bucket bits every sampled key of the half shares
     if (!s_cnt[h] || !cm) continue;
-    // keys of this half per bucket it can reach
+    // keys of this half per bucket it can reach: squeeze only if the fullest
+    // such bucket (mean + 4.5 sigma) would overflow the local sort
     const double load = (double)n * s_cnt[h] / total / (double)(1u << (15 - __builtin_popcount(cm)));
-    if (load <= 0.875 * cap) continue;
+    if (1.02 * load + 4.5 * sqrt(load) <= (double)cap) continue;
     const int bb = 31 - __builtin_clz(cm);
     const int b = bb + W - 16;
     hiM[h] = ~((2ull << b) - 1ull);
@@ -603,8 +666,15 @@ __global__ __launch_bounds__(kPlanRowThreads) void thrs_plan_rows(
     __threadfence();
     if (sqMode == 1 && t == 0) plan_squeeze(meta, keyBits, sample);
     __syncthreads();
-    if (!(sqMode == 1 && load_agent(&meta[kMetaRehist]) != 0u))
+    if (!(sqMode == 1 && load_agent(&meta[kMetaRehist]) != 0u)) {
       plan_big_prefix(joint, meta, bigB, bigPos, bigTile, tileKeys, s_w);
+      // f32 with a -0 key: whole keys through the top-digit passes (mode 3)
+      // (more zeros than the zero log holds: thrs_local16 could not restore
+      // the -0 signs from the planes)
+      if (t == 0 && load_agent(&meta[kMetaNegZero]) != 0u && load_agent(&meta[kMetaZeroCount]) > kZeroLogCap &&
+          load_agent(&meta[kMetaMode]) == 0u)
+        meta[kMetaMode] = 3;
+    }
     __syncthreads();  // s_w is reused below
   }
   if (r != 0) return;
@@ -1285,13 +1355,59 @@ __device__ __attribute__((noinline)) void loc16_write_zero_chunk(uint32_t* __res
   }
 }
 
+// The same chunk when the keys came as image planes (mode 0) and a -0 was
+// seen (at most kZeroLogCap zeros, thrs_plan_rows): the zeros' signs come from
+// the zero log (input positions, any order).  A -0's rank among the zeros is
+// the number of logged zeros at smaller positions (their stable order).
+template <typename LG, typename KM>
+__device__ __attribute__((noinline)) void loc16_write_zero_log(uint32_t* __restrict__ keys, KM km, uint32_t start,
+                                                               uint32_t size, uint32_t hiBits, unsigned char* smem,
+                                                               const uint32_t* __restrict__ zlog, uint32_t z) {
+  constexpr int KPT = LG::KPT;
+  constexpr uint32_t CHUNK = 64 * KPT;
+  static_assert(kZeroLogCap / 32 + 1 <= (uint32_t)LG::WAVES * kBins, "sign bits fit the counters' LDS");
+  const uint16_t* stage = reinterpret_cast<const uint16_t*>(smem);
+  uint32_t* negBits = reinterpret_cast<uint32_t*>(smem + LG::STAGE_BYTES);  // [kZeroLogCap / 32]
+  uint32_t* s_s0 = negBits + kZeroLogCap / 32;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint32_t zlo = kimg<2>(km, 0u) & 0xFFFFu;
+  for (uint32_t i = tid; i < kZeroLogCap / 32 + 1; i += LG::THREADS) negBits[i] = 0;
+  lds_barrier();
+  const uint16_t* stw = stage + w * KPT * LG::ROW + lane;
+  const int32_t lim = (int32_t)size - (int32_t)(w * CHUNK + lane);
+  uint32_t below = 0;  // sorted items below the zeros' item: the run's start s0
+  for (int j = 0; j < KPT; ++j)
+    if (j * 64 < lim) below += (uint32_t)stw[j * LG::ROW] < zlo ? 1u : 0u;
+  atomicAdd(s_s0, below);
+  for (uint32_t e = tid; e < z; e += LG::THREADS) {
+    const uint32_t x = zlog[e];
+    if (x >> 31) {
+      const uint32_t p = x & 0x7FFFFFFFu;
+      uint32_t r = 0;
+      for (uint32_t f = 0; f < z; ++f) r += (zlog[f] & 0x7FFFFFFFu) < p ? 1u : 0u;
+      atomicOr(&negBits[r >> 5], 1u << (r & 31));
+    }
+  }
+  lds_barrier();
+  const uint32_t s0 = *s_s0;
+  uint32_t* dst = keys + start + w * CHUNK + lane;
+  for (int j = 0; j < KPT; ++j) {
+    if (j * 64 < lim) {
+      const uint32_t r = w * CHUNK + 64 * j + lane - s0;
+      dst[j * 64] = r < z ? (((negBits[r >> 5] >> (r & 31)) & 1u) ? 0x80000000u : 0u)
+                          : kinv<2>(km, hiBits | (uint32_t)stw[j * LG::ROW]);
+    }
+  }
+}
+
 template <int KT, bool ATOMIC_RANK, typename LG>
 __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(LG::WPE))) void thrs_local16(uint32_t* __restrict__ keys, KeyMap<uint32_t> kmh,
                                                             const uint32_t* __restrict__ chunkOff,
                                                             const uint32_t* __restrict__ chunkB0,
                                                             const uint32_t* __restrict__ meta,
                                                             const uint16_t* __restrict__ lo,
-                                                            const SqueezeWords* __restrict__ sq) {
+                                                            const SqueezeWords* __restrict__ sq,
+                                                            const uint32_t* __restrict__ zeroLog) {
   constexpr int KPT = LG::KPT, NP = LG::NP;
   constexpr uint32_t CHUNK = 64 * KPT;
   const uint32_t c = blockIdx.x;
@@ -1438,9 +1554,18 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(LG:
   if constexpr (KT == 2) {
     // f32: +0 and -0 share one image Z, so the chunk of Z's bucket takes its
     // zeros' bit patterns from the input, in input order (their stable order)
+    // -- unless the keys came as planes (mode 0): then the signs of up to
+    // kZeroLogCap zeros are in the zero log (none -0: every zero is +0, as
+    // kinv rebuilds it)
     if ((kimg<2>(km, 0u) >> 16) == chunkB0[c]) {
-      loc16_write_zero_chunk<LG>(keys, km, start, size, hiBits, smem);
-      return;
+      if (!(lo && meta[kMetaMode] == 0)) {
+        loc16_write_zero_chunk<LG>(keys, km, start, size, hiBits, smem);
+        return;
+      }
+      if (zeroLog && meta[kMetaNegZero]) {
+        loc16_write_zero_log<LG>(keys, km, start, size, hiBits, smem, zeroLog, meta[kMetaZeroCount]);
+        return;
+      }
     }
   }
   // every stage read first (in bounds for all lanes), then the lane-conditional

@@ -1426,7 +1426,7 @@ constexpr int kSegs = 8;
 // tiles counted from pos every wave load of u16 keys would straddle two
 // lines); the first tile (and the last) may be partial.
 #ifndef THRS_SEG_ALIGN
-#define THRS_SEG_ALIGN 1
+#define THRS_SEG_ALIGN 0  // measured slower (docs/EXPERIMENTS.md row 85): off
 #endif
 __host__ __device__ __forceinline__ uint64_t seg_tile_base(uint32_t pos, uint32_t T) {
   return THRS_SEG_ALIGN ? (uint64_t)pos / T * T : (uint64_t)pos;
@@ -1527,10 +1527,6 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
     const typename KeyTraits<KT>::U* __restrict__ keysIn2 = nullptr,
     typename KeyTraits<KT>::U* __restrict__ keysOut2 = nullptr, KeyMap<typename KeyTraits<KT>::U> km2 = {},
     int shift2 = 0) {
-  using U = typename KeyTraits<KT>::U;
-  using VW = typename ValueWord<VB>::T;
-  using G = PassGeom<sizeof(U), VB>;
-  constexpr uint32_t T = G::TILE;
   if constexpr (ALT >= 0) {
     const uint32_t m = *gate;
     if (!((gateMask >> m) & 1u)) {
