@@ -431,13 +431,19 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   // in one launch each (thrs_pass_seg ALT)
   // THRS_SEG_PIPE: the pipelined segmented pass (u32 / f32 keys without values)
   constexpr bool kPipe = THRS_SEG_PIPE && (KT == 0 || KT == 2) && VB == 0;
-  constexpr int kPipeKT = kPipe ? KT : 0;  // (instantiated for u32 / f32 only)
-  auto pipeKeys = atomicRank ? thrs_pass_seg_pipe<kPipeKT, ST, true, kCodecKeys>
-                             : thrs_pass_seg_pipe<kPipeKT, ST, false, kCodecKeys>;
-  auto pipeSplit = atomicRank ? thrs_pass_seg_pipe<kPipeKT, ST, true, kCodecSplit>
-                              : thrs_pass_seg_pipe<kPipeKT, ST, false, kCodecSplit>;
-  auto pipePlanes = atomicRank ? thrs_pass_seg_pipe<0, ST, true, kCodecPlanes>
-                               : thrs_pass_seg_pipe<0, ST, false, kCodecPlanes>;
+  // (instantiated only in THRS_SEG_PIPE builds, u32 / f32 keys-only)
+  auto pipe_kernel = [&](int codec) {
+    if constexpr (kPipe) {
+      if (codec == kCodecSplit) return atomicRank ? thrs_pass_seg_pipe<KT, ST, true, kCodecSplit>
+                                                  : thrs_pass_seg_pipe<KT, ST, false, kCodecSplit>;
+      if (codec == kCodecPlanes) return atomicRank ? thrs_pass_seg_pipe<0, ST, true, kCodecPlanes>
+                                                   : thrs_pass_seg_pipe<0, ST, false, kCodecPlanes>;
+      return atomicRank ? thrs_pass_seg_pipe<KT, ST, true, kCodecKeys> : thrs_pass_seg_pipe<KT, ST, false, kCodecKeys>;
+    } else {
+      (void)codec;
+      return nullptr;
+    }
+  };
   const uint32_t segTileKeys = (uint32_t)seg_tile_keys(KB, VB);
   // (other key / value types: the plain keys kernel, never launched merged)
   constexpr bool kMerge = THRS_SEG_MERGE && KT == 0 && VB == 0;  // (u32 only)
@@ -459,10 +465,12 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     if (planes && (allow_lds(skSplit, lds) != hipSuccess || allow_lds(skPlanes, lds) != hipSuccess ||
                    allow_lds(skSplitM, lds) != hipSuccess || allow_lds(skPlanesM, lds) != hipSuccess))
       return THRS_ERROR_HIP;
-    if (kPipe && (allow_lds(pipeKeys, PipeGeom::LDS_BYTES) != hipSuccess ||
-                  allow_lds(pipeSplit, PipeGeom::LDS_BYTES) != hipSuccess ||
-                  allow_lds(pipePlanes, PipeGeom::LDS_BYTES) != hipSuccess))
-      return THRS_ERROR_HIP;
+    if constexpr (kPipe) {
+      if (allow_lds(pipe_kernel(kCodecKeys), PipeGeom::LDS_BYTES) != hipSuccess ||
+          allow_lds(pipe_kernel(kCodecSplit), PipeGeom::LDS_BYTES) != hipSuccess ||
+          allow_lds(pipe_kernel(kCodecPlanes), PipeGeom::LDS_BYTES) != hipSuccess)
+        return THRS_ERROR_HIP;
+    }
     if constexpr (kKV) {
       if (allow_lds(atomicRank ? thrs_local_kv<KT, VB, true> : thrs_local_kv<KT, VB, false>, LocKV::LDS) != hipSuccess)
         return THRS_ERROR_HIP;
@@ -669,7 +677,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                           const uint32_t* gate, uint32_t gateMask, int codec = kCodecKeys) {
       ProfScope prof(stream, 1, THRS_PK_PASS_SEG, moveBytes);
       if constexpr (kPipe) {
-        auto pk = codec == kCodecSplit ? pipeSplit : codec == kCodecPlanes ? pipePlanes : pipeKeys;
+        auto pk = pipe_kernel(codec);
         hipLaunchKernelGGL(pk, dim3((uint32_t)cu_count()), dim3(PipeGeom::THREADS), PipeGeom::LDS_BYTES, stream,
                            kin, kout, codec == kCodecPlanes ? kid : km, codec == kCodecPlanes ? 16 : startBits + 8 * p,
                            reinterpret_cast<uint32_t*>(hyb + infoOff), reinterpret_cast<const uint32_t*>(hyb + baseOff),

@@ -225,10 +225,10 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
   uint64_t tailStart = lo;
   if (vec) {  // 16-byte loads, UN in flight per lane (keys base 16-B aligned, checked on host)
     constexpr int PER = 16 / sizeof(U);
-    // (the squeeze check's extra registers: two 16-byte loads in flight, not
-    // four, or the 128-VGPR budget spills ~40 registers -- 4x slower)
+    // (the squeeze check's extra registers: three 16-byte loads in flight,
+    // not four, or the 128-VGPR budget spills ~35 registers -- 4x slower)
 #ifndef THRS_HJ_CHECK_UN
-#define THRS_HJ_CHECK_UN 2
+#define THRS_HJ_CHECK_UN 3
 #endif
     constexpr int UN = kCheck ? THRS_HJ_CHECK_UN : kHjUnroll;
     constexpr uint32_t ITERS_PER_EPOCH = kEpoch / (kHistThreads * UN * PER);
@@ -240,15 +240,19 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
     // it's LDS adds, so every wave keeps UN loads in flight while it counts.
     // Loads past the range read the range's last word (clamped, unconditional:
     // a lane-conditional load would make the compiler wait for all of them).
+    // (the thread index re-pinned every iteration: no lane-dependent address
+    // is hoisted out of the loop into a long-lived register)
+    uint32_t tidv = tid;
     auto load_iter = [&](uint64_t it, uint4 (&q)[UN]) {
-      const uint64_t i = v0 + it * UN * gstride + tid;
+      const uint64_t i = v0 + it * UN * gstride + tidv;
 #pragma unroll
       for (int u = 0; u < UN; ++u) q[u] = kv[min(i + u * gstride, nv - 1)];
     };
     uint4 qn[UN];
     if (nIter) load_iter(0, qn);
     for (uint64_t it = 0; it < nIter; ++it) {
-      const uint64_t i = v0 + it * UN * gstride + tid;
+      pin(tidv);
+      const uint64_t i = v0 + it * UN * gstride + tidv;
       uint4 q[UN];
 #pragma unroll
       for (int u = 0; u < UN; ++u) q[u] = qn[u];
@@ -1306,7 +1310,7 @@ using Loc16Wide = Loc16G<THRS_WIDE_W, THRS_WIDE_K, 4, THRS_WIDE_K / 2>;
 template <typename LG, typename KM>
 __device__ __attribute__((noinline)) void loc16_write_zero_chunk(uint32_t* __restrict__ keys, KM km,
                                                                  uint32_t start, uint32_t size, uint32_t hiBits,
-                                                                 unsigned char* smem) {
+                                                                 unsigned char* smem, uint32_t ish) {
   constexpr int KPT = LG::KPT;
   constexpr uint32_t CHUNK = 64 * KPT;
   static_assert(LG::CAP / 32 + LG::WAVES + 1 <= (uint32_t)LG::WAVES * kBins, "sign bits fit the counters' LDS");
@@ -1350,7 +1354,7 @@ __device__ __attribute__((noinline)) void loc16_write_zero_chunk(uint32_t* __res
     if (j * 64 < lim) {
       const uint32_t slot = w * CHUNK + 64 * j + lane, r = slot - s0;
       dst[j * 64] = r < z ? (((negBits[r >> 5] >> (r & 31)) & 1u) ? 0x80000000u : 0u)
-                          : kinv<2>(km, hiBits | (uint32_t)stw[j * LG::ROW]);
+                          : kinv<2>(km, hiBits | ((uint32_t)stw[j * LG::ROW] << ish));
     }
   }
 }
@@ -1362,7 +1366,8 @@ __device__ __attribute__((noinline)) void loc16_write_zero_chunk(uint32_t* __res
 template <typename LG, typename KM>
 __device__ __attribute__((noinline)) void loc16_write_zero_log(uint32_t* __restrict__ keys, KM km, uint32_t start,
                                                                uint32_t size, uint32_t hiBits, unsigned char* smem,
-                                                               const uint32_t* __restrict__ zlog, uint32_t z) {
+                                                               const uint32_t* __restrict__ zlog, uint32_t z,
+                                                               uint32_t ish) {
   constexpr int KPT = LG::KPT;
   constexpr uint32_t CHUNK = 64 * KPT;
   static_assert(kZeroLogCap / 32 + 1 <= (uint32_t)LG::WAVES * kBins, "sign bits fit the counters' LDS");
@@ -1377,7 +1382,7 @@ __device__ __attribute__((noinline)) void loc16_write_zero_log(uint32_t* __restr
   const int32_t lim = (int32_t)size - (int32_t)(w * CHUNK + lane);
   uint32_t below = 0;  // sorted items below the zeros' item: the run's start s0
   for (int j = 0; j < KPT; ++j)
-    if (j * 64 < lim) below += (uint32_t)stw[j * LG::ROW] < zlo ? 1u : 0u;
+    if (j * 64 < lim) below += (uint32_t)stw[j * LG::ROW] < (zlo >> ish) ? 1u : 0u;
   atomicAdd(s_s0, below);
   for (uint32_t e = tid; e < z; e += LG::THREADS) {
     const uint32_t x = zlog[e];
@@ -1395,7 +1400,7 @@ __device__ __attribute__((noinline)) void loc16_write_zero_log(uint32_t* __restr
     if (j * 64 < lim) {
       const uint32_t r = w * CHUNK + 64 * j + lane - s0;
       dst[j * 64] = r < z ? (((negBits[r >> 5] >> (r & 31)) & 1u) ? 0x80000000u : 0u)
-                          : kinv<2>(km, hiBits | (uint32_t)stw[j * LG::ROW]);
+                          : kinv<2>(km, hiBits | ((uint32_t)stw[j * LG::ROW] << ish));
     }
   }
 }
@@ -1417,6 +1422,13 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(LG:
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   with_map<KT>(kmh, sq, [&](auto km) {
   const uint32_t hiBits = chunkB0[c] << 16;  // the bucket: the image's top 16 bits
+  // A squeezed image half (KeyMap<U, true>) has bit 0 clear in every image:
+  // its items drop that bit (15-bit items), so both LSD rounds count over
+  // contiguous digits (even digits only would leave half the counters' banks
+  // idle and double the conflicts on the others)
+  uint32_t ish = 0;
+  if constexpr (!std::is_same<decltype(km), KeyMap<uint32_t>>::value)
+    ish = ((hiBits >> 31) ? km.loM[1] : km.loM[0]) != 0 ? 1u : 0u;
   uint16_t* stage = reinterpret_cast<uint16_t*>(smem);
   uint32_t* s_cnt = reinterpret_cast<uint32_t*>(smem + LG::STAGE_BYTES);  // [waves][256]
   const uint32_t tid = threadIdx.x, lane = tid & 63;
@@ -1448,8 +1460,8 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(LG:
 #pragma unroll
       for (int jj = 0; jj < LB; jj += 2) {
         const int j = h + jj;
-        const uint32_t a = (j * 64 < lim) ? (uint32_t)raw[jj] : 0xFFFFu;
-        const uint32_t b = (j + 1 < KPT && (j + 1) * 64 < lim) ? (uint32_t)raw[jj + 1] : 0xFFFFu;
+        const uint32_t a = (j * 64 < lim) ? (uint32_t)raw[jj] >> ish : 0xFFFFu;
+        const uint32_t b = (j + 1 < KPT && (j + 1) * 64 < lim) ? (uint32_t)raw[jj + 1] >> ish : 0xFFFFu;
         it[j >> 1] = a | (b << 16);
       }
     }
@@ -1461,8 +1473,9 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(LG:
 #pragma unroll
       for (int jj = 0; jj < LB; jj += 2) {
         const int j = h + jj;
-        const uint32_t a = (j * 64 < lim) ? (kimg<KT>(km, raw[jj]) & 0xFFFFu) : 0xFFFFu;
-        const uint32_t b = (j + 1 < KPT && (j + 1) * 64 < lim) ? (kimg<KT>(km, raw[jj + 1]) & 0xFFFFu) : 0xFFFFu;
+        const uint32_t a = (j * 64 < lim) ? (kimg<KT>(km, raw[jj]) & 0xFFFFu) >> ish : 0xFFFFu;
+        const uint32_t b =
+            (j + 1 < KPT && (j + 1) * 64 < lim) ? (kimg<KT>(km, raw[jj + 1]) & 0xFFFFu) >> ish : 0xFFFFu;
         it[j >> 1] = a | (b << 16);
       }
     }
@@ -1559,11 +1572,11 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(LG:
     // kinv rebuilds it)
     if ((kimg<2>(km, 0u) >> 16) == chunkB0[c]) {
       if (!(lo && meta[kMetaMode] == 0)) {
-        loc16_write_zero_chunk<LG>(keys, km, start, size, hiBits, smem);
+        loc16_write_zero_chunk<LG>(keys, km, start, size, hiBits, smem, ish);
         return;
       }
       if (zeroLog && meta[kMetaNegZero]) {
-        loc16_write_zero_log<LG>(keys, km, start, size, hiBits, smem, zeroLog, meta[kMetaZeroCount]);
+        loc16_write_zero_log<LG>(keys, km, start, size, hiBits, smem, zeroLog, meta[kMetaZeroCount], ish);
         return;
       }
     }
@@ -1577,7 +1590,7 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(LG:
     for (int jj = 0; jj < LB; ++jj) o[jj] = stw[(h + jj) * LG::ROW];
 #pragma unroll
     for (int jj = 0; jj < LB; ++jj)
-      if ((h + jj) * 64 < lim) src[(h + jj) * 64] = kinv<KT>(km, hiBits | o[jj]);
+      if ((h + jj) * 64 < lim) src[(h + jj) * 64] = kinv<KT>(km, hiBits | (o[jj] << ish));
   }
   });
 }
@@ -1830,10 +1843,17 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(4))
   uint32_t it[KPT];
   load_run<KPT>(it, keys + ch.start, myOff, ch.size, avail);
   with_map<KT>(km, sq, [&](auto kmx) {  // (the squeeze, f32 keys: only the items' images depend on it)
+    // (a squeezed half: image bit 0 is always clear -- dropped from the items,
+    // as in thrs_local16, so that the first round's digits are contiguous;
+    // f32 keys travel by position, so nothing is rebuilt from the items)
+    uint32_t ish = 0;
+    if constexpr (!std::is_same<decltype(kmx), KeyMap<uint32_t>>::value)
+      ish = ((hiImg >> 31) ? kmx.loM[1] : kmx.loM[0]) != 0 ? 1u : 0u;
 #pragma unroll
     for (int j = 0; j < KPT; ++j) {
       const uint32_t pos = myOff + j * 64;
-      it[j] = (j * 64 < lim) ? ((kimg<KT>(kmx, it[j]) << 16) | pos) : 0xFFFF0000u;  // padding: digits 255
+      it[j] = (j * 64 < lim) ? ((((uint32_t)kimg<KT>(kmx, it[j]) & 0xFFFFu) >> ish) << 16 | pos)
+                             : 0xFFFF0000u;  // padding: digits 255
     }
   });
   loc_rounds<0, ATOMIC_RANK, LG>(it, ch, KeyMap<uint32_t>{0u, 0u, 0u}, 16, 2, smem, nullptr);

@@ -921,8 +921,20 @@ __device__ __forceinline__ void pass_tile(
   // per-item positions are never hoisted into 32 live registers)
   int32_t lim = (int32_t)valid - (int32_t)(w * CHUNK + lane);
   pin(reinterpret_cast<uint32_t&>(lim));
+  // The split codec writes images: the keys become their images once, here,
+  // and the count, rank and write-out read them as they are (float keys under
+  // a key range or the squeeze: one map per key instead of four)
+  constexpr bool kImg = CODEC == kCodecSplit;
+  if constexpr (kImg) {
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) k[j] = kimg<KT>(km, k[j]);
+  }
+  auto img_of = [&](U key) -> U {
+    if constexpr (kImg) return key;
+    else return kimg<KT>(km, key);
+  };
   auto digit_of = [&](U key, int j) -> uint32_t {
-    uint32_t dd = (uint32_t)(kimg<KT>(km, key) >> shift) & 0xFFu;
+    uint32_t dd = (uint32_t)(img_of(key) >> shift) & 0xFFu;
     if (!full) dd = (j * 64 < lim) ? dd : 0xFFu;  // padding sorts after every real key
     return dd;
   };
@@ -1162,7 +1174,7 @@ __device__ __forceinline__ void pass_tile(
     auto put = [&](U key, uint32_t i, uint32_t off, const VW& vv) __attribute__((always_inline)) {
       const uint32_t dst = off + (uint32_t)r * STAGE + i;
       if constexpr (CODEC == kCodecSplit) {
-        const uint32_t img = (uint32_t)kimg<KT>(km, key);
+        const uint32_t img = (uint32_t)key;  // (an image already)
         reinterpret_cast<uint16_t*>(keysOut)[dst] = (uint16_t)img;
         hiOut[dst] = (uint8_t)(img >> 24);
       } else if constexpr (CODEC == kCodecPlanes) {
@@ -1190,7 +1202,7 @@ __device__ __forceinline__ void pass_tile(
           }
 #pragma unroll
         for (int b = 0; b < WB; ++b)
-          if (j0 + b < NS) off[b] = s_gofs[(uint32_t)(kimg<KT>(km, key[b]) >> shift) & 0xFFu];
+          if (j0 + b < NS) off[b] = s_gofs[(uint32_t)(img_of(key[b]) >> shift) & 0xFFu];
 #pragma unroll
         for (int b = 0; b < WB; ++b)
           if (j0 + b < NS) put(key[b], (j0 + b) * THREADS + tid, off[b], val[VB ? b : 0]);
@@ -1203,7 +1215,7 @@ __device__ __forceinline__ void pass_tile(
       const uint32_t slot = (uint32_t)r * STAGE + i;
       if (full || slot < valid) {
         const U key = stage_k[i];
-        const uint32_t dd = (uint32_t)(kimg<KT>(km, key) >> shift) & 0xFFu;
+        const uint32_t dd = (uint32_t)(img_of(key) >> shift) & 0xFFu;
         VW vv{};
         if constexpr (VB != 0) vv = stage_v[i];
         put(key, i, s_gofs[dd], vv);
