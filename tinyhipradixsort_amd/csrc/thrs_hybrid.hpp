@@ -354,9 +354,14 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
       atomicAdd(&rowHist[b >> 8], mult * 0x8000u);
     }
   }
-  for (uint32_t i = tid; i < kBuckets; i += kHistThreads) {
-    const uint32_t c = (s_joint[i >> 1] >> ((i & 1u) << 4)) & 0xFFFFu;
-    if (c) atomicAdd(&joint[i], c);
+  // the flush: one 64-bit add per LDS word (its two buckets are neighbours
+  // in joint, and no bucket's total reaches 2^32: no carry crosses them) --
+  // half the global atomics of one add per bucket
+  for (uint32_t wi = tid; wi < kJointWords; wi += kHistThreads) {
+    const uint32_t x = s_joint[wi];
+    if (x)
+      atomicAdd(reinterpret_cast<unsigned long long*>(joint) + wi,
+                (unsigned long long)(x & 0xFFFFu) | ((unsigned long long)(x >> 16) << 32));
   }
   // the range's second-digit counts (column sums; lanes d, d+1 share a word)
   static_assert(kHistThreads == 4 * kBins, "four top-digit quarters per second digit");
