@@ -150,7 +150,10 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
   __syncthreads();
   with_map<KT>(kmh, sq, [&](auto km) {
   // (a squeezed first histogram: does every key carry its half's dropped bit?)
-  constexpr bool kCheck = !SECOND && !std::is_same<decltype(km), KeyMap<U>>::value;
+#ifndef THRS_HJ_NOCHECK
+#define THRS_HJ_NOCHECK 0  // EXPERIMENT only (the check's cost): a wrong guess then goes unnoticed
+#endif
+  constexpr bool kCheck = !SECOND && !std::is_same<decltype(km), KeyMap<U>>::value && !THRS_HJ_NOCHECK;
   U viol = 0;
   const uint64_t len = hj_len(n, gridDim.x);
   const uint64_t lo = min((uint64_t)n, (uint64_t)blockIdx.x * len), hi = min((uint64_t)n, lo + len);
@@ -231,7 +234,11 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
 #define THRS_HJ_CHECK_UN 3
 #endif
     constexpr int UN = kCheck ? THRS_HJ_CHECK_UN : kHjUnroll;
-    constexpr uint32_t ITERS_PER_EPOCH = kEpoch / (kHistThreads * UN * PER);
+#ifndef THRS_HJ_CHECK_EPOCH
+#define THRS_HJ_CHECK_EPOCH THRS_HJ_EPOCH
+#endif
+    constexpr uint32_t ITERS_PER_EPOCH = (kCheck ? (uint32_t)THRS_HJ_CHECK_EPOCH : kEpoch) / (kHistThreads * UN * PER);
+    static_assert((kCheck ? (uint32_t)THRS_HJ_CHECK_EPOCH : kEpoch) <= 32768u, "exactness bound");
     static_assert(ITERS_PER_EPOCH >= 1, "one iteration must fit an epoch");
     const uint64_t v0 = lo / PER, nv = hi / PER;   // lo is a multiple of 4 (hj_len)
     const uint4* kv = reinterpret_cast<const uint4*>(keys);
@@ -1586,6 +1593,19 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(LG:
       }
     }
   }
+  // the inverse map on this chunk: its bucket fixes the image half, so a
+  // squeezed map's masks are the chunk's (scalars: no per-key selects)
+  auto inv = [&](uint32_t y) -> uint32_t {
+    if constexpr (!std::is_same<decltype(km), KeyMap<uint32_t>>::value) {
+      const bool hc = (__builtin_amdgcn_readfirstlane(hiBits) >> 31) != 0;
+      const uint32_t hm = hc ? km.hiM[1] : km.hiM[0], lm = hc ? km.loM[1] : km.loM[0],
+                     cs = hc ? km.cst[1] : km.cst[0];
+      y = (y & hm) | ((y >> 1) & lm) | cs;
+      return unbits32<KT>(((y >> km.sh) + km.lo) ^ km.mask);
+    } else {
+      return kinv<KT>(km, y);
+    }
+  };
   // every stage read first (in bounds for all lanes), then the lane-conditional
   // stores: a read inside the condition would be waited for one at a time
 #pragma unroll
@@ -1595,7 +1615,7 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(LG:
     for (int jj = 0; jj < LB; ++jj) o[jj] = stw[(h + jj) * LG::ROW];
 #pragma unroll
     for (int jj = 0; jj < LB; ++jj)
-      if ((h + jj) * 64 < lim) src[(h + jj) * 64] = kinv<KT>(km, hiBits | (o[jj] << ish));
+      if ((h + jj) * 64 < lim) src[(h + jj) * 64] = inv(hiBits | (o[jj] << ish));
   }
   });
 }
