@@ -133,7 +133,7 @@ __global__ __launch_bounds__(kHistThreads) void thrs_big_hist(
   const uint32_t len = (total + G - 1) / G;
   const uint32_t lo = min(total, blockIdx.x * len), hi = min(total, lo + len);
   uint32_t* my = s_h + (tid % kBigCopies);
-  if (lo < hi) with_map<KT>(kmh, sq, [&](auto km) {
+  if (lo < hi) with_map<KT>(kmh, sq, [&](auto km) __attribute__((always_inline)) {
     for (uint32_t c = big_find(bigPos, M, lo); c < M && bigPos[c] < hi; ++c) {
       const uint32_t p0 = bigPos[c], a = max(lo, p0), b = min(hi, bigPos[c + 1]);
       const uint32_t start = chunkOff[bigB[c]], size = bigPos[c + 1] - p0;
@@ -223,7 +223,7 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
   ST* statusNext = p + 1 < nLow ? (par ? status0 : status1) : nullptr;
   const uint32_t M = meta[kMetaBigCount], nTiles = bigTile[M];
   const uint32_t tid = threadIdx.x;
-  with_map<KT>(km, sq, [&](auto kmx) {
+  with_map<KT>(km, sq, [&](auto kmx) __attribute__((always_inline)) {
   U k[G::KPT];
   VW v[VB ? G::KPT : 1];
   for (;;) {

@@ -148,7 +148,7 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
   for (uint32_t i = tid; i < kJointWords + kBins; i += kHistThreads) s_joint[i] = 0;
   if (tid == 0) *s_logN = 0;
   __syncthreads();
-  with_map<KT>(kmh, sq, [&](auto km) {
+  with_map<KT>(kmh, sq, [&](auto km) __attribute__((always_inline)) {
   // (a squeezed first histogram: does every key carry its half's dropped bit?)
 #ifndef THRS_HJ_NOCHECK
 #define THRS_HJ_NOCHECK 0  // EXPERIMENT only (the check's cost): a wrong guess then goes unnoticed
@@ -1432,7 +1432,7 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(LG:
   const uint32_t start = chunkOff[c], size = chunkOff[c + 1] - start;
   if (size == 0 || size > LG::CAP) return;  // big chunk: the per-bucket fallback sorts it
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  with_map<KT>(kmh, sq, [&](auto km) {
+  with_map<KT>(kmh, sq, [&](auto km) __attribute__((always_inline)) {
   const uint32_t hiBits = chunkB0[c] << 16;  // the bucket: the image's top 16 bits
   // A squeezed image half (KeyMap<U, true>) has bit 0 clear in every image:
   // its items drop that bit (15-bit items), so both LSD rounds count over
@@ -1838,6 +1838,24 @@ __global__ __launch_bounds__(LocCount::THREADS) void thrs_local_count16(
 // rebuilt from the bucket and written, and the values are permuted through
 // the same LDS stage by the carried positions.  f32 keys (+0 and -0 share one
 // image, so they cannot be rebuilt bit-exactly) are permuted the same way.
+// thrs_local_pairs' items: low 16 image bits << 16 | chunk position.  A
+// squeezed half's images all have bit 0 clear -- dropped from the items, as
+// in thrs_local16, so the first round's digits are contiguous (f32 keys
+// travel by position: nothing is rebuilt from the items).  (A function, not
+// a with_map lambda: the closure costs registers.)
+template <int KT, int KPT, typename KM>
+__device__ __forceinline__ void pairs_items(uint32_t (&it)[KPT], KM km, uint32_t myOff, int32_t lim, uint32_t hiImg) {
+  uint32_t ish = 0;
+  if constexpr (!std::is_same<KM, KeyMap<uint32_t>>::value)
+    ish = ((hiImg >> 31) ? km.loM[1] : km.loM[0]) != 0 ? 1u : 0u;
+#pragma unroll
+  for (int j = 0; j < KPT; ++j) {
+    const uint32_t pos = myOff + j * 64;
+    it[j] = (j * 64 < lim) ? ((((uint32_t)kimg<KT>(km, it[j]) & 0xFFFFu) >> ish) << 16 | pos)
+                           : 0xFFFF0000u;  // padding: digits 255
+  }
+}
+
 template <int KT, bool ATOMIC_RANK, typename LG>
 __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(4))) void thrs_local_pairs(
     uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, KeyMap<uint32_t> km,
@@ -1867,20 +1885,13 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(4))
   const int32_t avail = __builtin_amdgcn_readfirstlane((int32_t)ch.size - (int32_t)(w * CHUNK));
   uint32_t it[KPT];
   load_run<KPT>(it, keys + ch.start, myOff, ch.size, avail);
-  with_map<KT>(km, sq, [&](auto kmx) {  // (the squeeze, f32 keys: only the items' images depend on it)
-    // (a squeezed half: image bit 0 is always clear -- dropped from the items,
-    // as in thrs_local16, so that the first round's digits are contiguous;
-    // f32 keys travel by position, so nothing is rebuilt from the items)
-    uint32_t ish = 0;
-    if constexpr (!std::is_same<decltype(kmx), KeyMap<uint32_t>>::value)
-      ish = ((hiImg >> 31) ? kmx.loM[1] : kmx.loM[0]) != 0 ? 1u : 0u;
-#pragma unroll
-    for (int j = 0; j < KPT; ++j) {
-      const uint32_t pos = myOff + j * 64;
-      it[j] = (j * 64 < lim) ? ((((uint32_t)kimg<KT>(kmx, it[j]) & 0xFFFFu) >> ish) << 16 | pos)
-                             : 0xFFFF0000u;  // padding: digits 255
-    }
-  });
+  // (the squeeze, f32 keys: only the items' images depend on it)
+  if constexpr (kSqueezable<KT>) {
+    if (sq && sq->on) pairs_items<KT, KPT>(it, with_squeeze(km, sq), myOff, lim, hiImg);
+    else pairs_items<KT, KPT>(it, km, myOff, lim, hiImg);
+  } else {
+    pairs_items<KT, KPT>(it, km, myOff, lim, hiImg);
+  }
   loc_rounds<0, ATOMIC_RANK, LG>(it, ch, KeyMap<uint32_t>{0u, 0u, 0u}, 16, 2, smem, nullptr);
   pin(reinterpret_cast<uint32_t&>(lim));
   // values of this thread's positions (the item registers are free again;
@@ -2081,27 +2092,20 @@ __device__ __noinline__ void kv8_six_rounds(unsigned char* smem, uint32_t size) 
   }
 }
 
-template <int KT, int VB, bool ATOMIC_RANK>
-__global__ __launch_bounds__(LocKV::THREADS) void thrs_local_kv(typename KeyTraits<KT>::U* __restrict__ keys,
-                                                                typename ValueWord<VB>::T* __restrict__ vals,
-                                                                KeyMap<typename KeyTraits<KT>::U> kmh,
-                                                                const uint32_t* __restrict__ chunkOff,
-                                                                const uint32_t* __restrict__ chunkB0,
-                                                                const uint32_t* __restrict__ meta,
-                                                                const SqueezeWords* __restrict__ sq) {
+// One chunk of thrs_local_kv under the key map km (plain, or the squeeze).
+// A device function, not a lambda handed to with_map: the closure cost the
+// 8-byte-key kernel 12 spilled VGPRs (C5 shape local sort 9.6 -> 11.1 ms).
+template <int KT, int VB, bool ATOMIC_RANK, typename KM>
+__device__ __forceinline__ void local_kv_chunk(typename KeyTraits<KT>::U* __restrict__ keys,
+                                               typename ValueWord<VB>::T* __restrict__ vals, KM km, uint32_t c,
+                                               uint32_t start, uint32_t size, const uint32_t* __restrict__ chunkB0) {
   using U = typename KeyTraits<KT>::U;
   constexpr int KB = (int)sizeof(U);
   using Item = typename std::conditional<KB == 4, uint32_t, uint64_t>::type;
-  static_assert(KB == 8 || VB >= 8, "4-byte keys with 0 / 4-byte values: thrs_local16 / thrs_local / thrs_local_pairs");
   constexpr int KPT = LocKV::KPT;
   constexpr uint32_t CHUNK = 64 * KPT;
   constexpr bool PERMUTE_KEYS = KT == 2 || KT == 3;  // floats travel by position (their -0 is not rebuilt)
-  const uint32_t c = blockIdx.x;
-  if (c >= meta[kMetaChunks]) return;
-  const uint32_t start = chunkOff[c], size = chunkOff[c + 1] - start;
-  if (size == 0 || size > LocKV::CAP) return;  // big chunk: the per-bucket fallback sorts it
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  with_map<KT>(kmh, sq, [&](auto km) {
   const U hiImg = (U)chunkB0[c] << (8 * KB - 16);  // the bucket: the image's top 16 bits
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -2291,7 +2295,30 @@ __global__ __launch_bounds__(LocKV::THREADS) void thrs_local_kv(typename KeyTrai
       if (j * 64 < lim) vdst[j * 64] = make_uint4((uint32_t)o[j], (uint32_t)(o[j] >> 32), (uint32_t)h, (uint32_t)(h >> 32));
     }
   }
-  });
+}
+
+template <int KT, int VB, bool ATOMIC_RANK>
+__global__ __launch_bounds__(LocKV::THREADS) void thrs_local_kv(typename KeyTraits<KT>::U* __restrict__ keys,
+                                                                typename ValueWord<VB>::T* __restrict__ vals,
+                                                                KeyMap<typename KeyTraits<KT>::U> kmh,
+                                                                const uint32_t* __restrict__ chunkOff,
+                                                                const uint32_t* __restrict__ chunkB0,
+                                                                const uint32_t* __restrict__ meta,
+                                                                const SqueezeWords* __restrict__ sq) {
+  using U = typename KeyTraits<KT>::U;
+  constexpr int KB = (int)sizeof(U);
+  static_assert(KB == 8 || VB >= 8, "4-byte keys with 0 / 4-byte values: thrs_local16 / thrs_local / thrs_local_pairs");
+  const uint32_t c = blockIdx.x;
+  if (c >= meta[kMetaChunks]) return;
+  const uint32_t start = chunkOff[c], size = chunkOff[c + 1] - start;
+  if (size == 0 || size > LocKV::CAP) return;  // big chunk: the per-bucket fallback sorts it
+  if constexpr (kSqueezable<KT>) {
+    if (sq && sq->on) {
+      local_kv_chunk<KT, VB, ATOMIC_RANK>(keys, vals, with_squeeze(kmh, sq), c, start, size, chunkB0);
+      return;
+    }
+  }
+  local_kv_chunk<KT, VB, ATOMIC_RANK>(keys, vals, kmh, c, start, size, chunkB0);
 }
 
 }  // namespace

@@ -1514,7 +1514,7 @@ __device__ __forceinline__ void thrs_pass_seg_body(
   if (tid < 2 * (kSegs + 1)) (tid <= (uint32_t)kSegs ? segPos[tid] : segTiles[tid - kSegs - 1]) = segInfo[tid];
   __syncthreads();
   const uint32_t home = xcc_id() & (kSegs - 1);
-  with_map<KT>(km, sq, [&](auto kmx) {
+  with_map<KT>(km, sq, [&](auto kmx) __attribute__((always_inline)) {
   uint32_t done = 0;  // thread 0: segments found exhausted
   U k[G::KPT];
   VW v[VB ? G::KPT : 1];

@@ -85,7 +85,7 @@ __global__ __launch_bounds__(PipeGeom::THREADS) __attribute__((amdgpu_waves_per_
   const uint32_t home = xcc_id() & (kSegs - 1);
   const uint32_t outEnd = segPos[kSegs];
 
-  with_map<KT>(km, sq, [&](auto kmx) {
+  with_map<KT>(km, sq, [&](auto kmx) __attribute__((always_inline)) {
     uint32_t done = 0;  // thread 0: segments found exhausted
     auto claim = [&]() {  // thread 0: the next tile (seg = kSegs: none left)
       uint32_t seg = kSegs, t = 0;
