@@ -27,7 +27,7 @@ FAMILIES = ["thrs_pass_seg", "thrs_pass_xb", "thrs_pass", "thrs_hist_joint", "th
 WIDTH16 = {"thrs_hist": True, "thrs_hist_joint": True, "k_copy_u128": True}
 # launches of the 3-HBM-pass path that exit at once unless the fallback flag
 # is set (the low-digit passes and their histogram): reported apart
-GATED = ("thrs_pass", "thrs_hist", "thrs_pass_seg")  # pass_seg: the fallback-only (mode 1) launch
+GATED = ("thrs_pass", "thrs_hist", "thrs_pass_seg", "thrs_hist_joint")  # pass_seg: the fallback-only (mode 1) launch; hist_joint: the squeeze's second histogram
 GATED_NS = 100_000           # shorter than this = a gated launch that exited
 GATED_KIB = 1024             # FETCH_SIZE / WRITE_SIZE below 1 MiB = the same
 GIB = 1 << 30
