@@ -394,8 +394,11 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   const SqueezeWords* sqw =
       squeeze ? reinterpret_cast<const SqueezeWords*>(scratch + plan.hybridOff + kMetaOff + kMetaSqueeze * 4) : nullptr;
   SqueezeWords* sample = squeeze ? reinterpret_cast<SqueezeWords*>(scratch + plan.hybridOff + kSampleOff) : nullptr;
-  // f32 with the image planes: the zero log (+-0 keys' positions and signs)
-  uint32_t* zeroLog = (KT == 2 && planes) ? reinterpret_cast<uint32_t*>(scratch + plan.hybridOff + kZeroLogOff) : nullptr;
+  // f32 on the bucket path: the zero log (+-0 keys' positions and signs;
+  // the planes restore the signs from it) and the -0 flag (pairs rebuild
+  // their keys from the images unless it is set)
+  uint32_t* zeroLog = (KT == 2 && bucket && !local32) ? reinterpret_cast<uint32_t*>(scratch + plan.hybridOff + kZeroLogOff)
+                                                     : nullptr;
   KeyMap<U> km{orderMask, (U)0, 0u};
   if (ranged) {
     const U span = (U)opt.rangeHi - (U)opt.rangeLo;  // > 0 (sort_impl returns at once for 0)
@@ -583,7 +586,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                            reinterpret_cast<uint32_t*>(hyb + kBigBOff), sqMode, 8 * KB,
                            reinterpret_cast<uint32_t*>(hyb + kBigPosOff), reinterpret_cast<uint32_t*>(hyb + kBigTileOff),
                            reinterpret_cast<uint4*>(scratch + plan.bigHistOff), nLow,
-                           sqMode == 1 ? static_cast<const SqueezeWords*>(sample) : nullptr);
+                           sqMode == 1 ? static_cast<const SqueezeWords*>(sample) : nullptr, planes ? 1 : 0);
       };
       if (!local32 && squeeze) {
         plan_rows(1, 0, kSegHistAOff, kRowHistOff);
@@ -772,7 +775,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
           auto lk = atomicRank ? thrs_local_pairs<KT, true, LG> : thrs_local_pairs<KT, false, LG>;
           hipLaunchKernelGGL(lk, lgrid, dim3(LG::THREADS), LG::template lds<U>(), stream,
                              reinterpret_cast<uint32_t*>(K), reinterpret_cast<uint32_t*>(V), km32, chunkOff, chunkB0,
-                             meta, sqw);
+                             meta, sqw, zeroLog ? meta + kMetaNegZero : nullptr);
         };
         if (smallLocal) launch_pairs(LocSmall{});
         else launch_pairs(LocBig{});

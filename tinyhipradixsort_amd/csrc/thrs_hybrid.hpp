@@ -173,6 +173,11 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
     const bool neg = k != 0;
     if (neg) atomicOr(&meta[kMetaNegZero], 1u);
     if (zfull) return;
+    if (pos >> 31) {  // (a position past 2^31 does not fit the log's 31 bits: the log counts as full)
+      atomicMax(&meta[kMetaZeroCount], kZeroLogCap + 1);
+      zfull = true;
+      return;
+    }
     const uint32_t slot = atomicAdd(&meta[kMetaZeroCount], 1u);
     if (slot < kZeroLogCap) zeroLog[slot] = (uint32_t)pos | (neg ? 0x80000000u : 0u);
     else zfull = true;
@@ -611,7 +616,7 @@ __global__ __launch_bounds__(kPlanRowThreads) void thrs_plan_rows(
     uint32_t* __restrict__ segInfo, uint32_t* __restrict__ segBase, uint32_t tileKeys, uint32_t histGrid,
     uint32_t* __restrict__ segInfoA, uint32_t* __restrict__ segBaseA, uint32_t* __restrict__ bigB, int sqMode,
     int keyBits, uint32_t* __restrict__ bigPos, uint32_t* __restrict__ bigTile, uint4* __restrict__ bigHist,
-    int nLow, const SqueezeWords* __restrict__ sample) {
+    int nLow, const SqueezeWords* __restrict__ sample, int planes) {
   if (sqMode == 2 && meta[kMetaRehist] == 0) return;
   __shared__ uint32_t s_w[2][4], s_base, s_b2[kBins], s_sq[3], s_last;
   const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6, r = blockIdx.x;
@@ -687,8 +692,8 @@ __global__ __launch_bounds__(kPlanRowThreads) void thrs_plan_rows(
       // f32 with a -0 key: whole keys through the top-digit passes (mode 3)
       // (more zeros than the zero log holds: thrs_local16 could not restore
       // the -0 signs from the planes)
-      if (t == 0 && load_agent(&meta[kMetaNegZero]) != 0u && load_agent(&meta[kMetaZeroCount]) > kZeroLogCap &&
-          load_agent(&meta[kMetaMode]) == 0u)
+      if (t == 0 && planes && load_agent(&meta[kMetaNegZero]) != 0u &&
+          load_agent(&meta[kMetaZeroCount]) > kZeroLogCap && load_agent(&meta[kMetaMode]) == 0u)
         meta[kMetaMode] = 3;
     }
     __syncthreads();  // s_w is reused below
@@ -1597,7 +1602,7 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(LG:
   // squeezed map's masks are the chunk's (scalars: no per-key selects)
   auto inv = [&](uint32_t y) -> uint32_t {
     if constexpr (!std::is_same<decltype(km), KeyMap<uint32_t>>::value) {
-      const bool hc = (__builtin_amdgcn_readfirstlane(hiBits) >> 31) != 0;
+      const bool hc = ((uint32_t)__builtin_amdgcn_readfirstlane((int)hiBits) >> 31) != 0;
       const uint32_t hm = hc ? km.hiM[1] : km.hiM[0], lm = hc ? km.loM[1] : km.loM[0],
                      cs = hc ? km.cst[1] : km.cst[0];
       y = (y & hm) | ((y >> 1) & lm) | cs;
@@ -1860,7 +1865,7 @@ template <int KT, bool ATOMIC_RANK, typename LG>
 __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(4))) void thrs_local_pairs(
     uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, KeyMap<uint32_t> km,
     const uint32_t* __restrict__ chunkOff, const uint32_t* __restrict__ chunkB0, const uint32_t* __restrict__ meta,
-    const SqueezeWords* __restrict__ sq) {
+    const SqueezeWords* __restrict__ sq, const uint32_t* __restrict__ zeroFlag) {
   constexpr int KPT = LG::KPT;
   constexpr uint32_t CHUNK = 64 * KPT;
   const uint32_t c = blockIdx.x;
@@ -1899,6 +1904,25 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(4))
   load_run<KPT>(it, vals + ch.start, myOff, ch.size, avail);
   uint32_t* stage = reinterpret_cast<uint32_t*>(smem);
   const uint32_t* stw = stage + w * CHUNK + lane;
+  // f32 keys: rebuilt from the bucket and the items, like u32 keys, unless
+  // the input holds a -0 (thrs_hist_joint's flag; +0 and -0 share one image):
+  // then they travel by position like the values.  The chunk's image half
+  // fixes the squeeze's masks (scalars).
+  const bool f32Rebuild = KT == 2 && zeroFlag && load_agent(zeroFlag) == 0u;
+  uint32_t hm2 = ~0u, lm2 = 0u, cs2 = 0u, ish2 = 0u;
+  if constexpr (KT == 2) {
+    if (sq && sq->on) {
+      const int hh = (int)((uint32_t)__builtin_amdgcn_readfirstlane((int)hiImg) >> 31);
+      hm2 = (uint32_t)sq->hiM[hh];
+      lm2 = (uint32_t)sq->loM[hh];
+      cs2 = (uint32_t)sq->cst[hh];
+      ish2 = lm2 != 0u ? 1u : 0u;
+    }
+  }
+  auto f32_key = [&](uint32_t y) -> uint32_t {
+    y = (y & hm2) | ((y >> 1) & lm2) | cs2;
+    return unbits32<2>(((y >> km.sh) + km.lo) ^ km.mask);
+  };
   uint32_t id[(KPT + 1) / 2];  // carried positions, two 16-bit halves per register
 #pragma unroll
   for (int j = 0; j < (KPT + 1) / 2; ++j) id[j] = 0;
@@ -1916,6 +1940,7 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(4))
       if (j < KPT) {
         id[j / 2] |= (j * 64 < lim ? (o[jj] & 0xFFFFu) : 0u) << (16 * (j & 1));
         if (KT == 0 && j * 64 < lim) ksrc[j * 64] = kinv_int(km, hiImg | (o[jj] >> 16));
+        if (KT == 2 && f32Rebuild && j * 64 < lim) ksrc[j * 64] = f32_key(hiImg | ((o[jj] >> 16) << ish2));
       }
     }
   }
@@ -1934,7 +1959,7 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(4))
     for (int jj = 0; jj < BR; ++jj)
       if (j0 + jj < KPT && (j0 + jj) * 64 < lim) vsrc[(j0 + jj) * 64] = o[jj];
   }
-  if constexpr (KT == 2) {
+  if (KT == 2 && !f32Rebuild) {
     // f32 keys travel by position like the values (+0 and -0 share one image)
     load_run<KPT>(it, keys + ch.start, myOff, ch.size, avail);
     lds_barrier();  // every value read from the stage
