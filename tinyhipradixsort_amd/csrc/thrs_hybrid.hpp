@@ -1327,7 +1327,7 @@ using Loc16Wide = Loc16G<THRS_WIDE_W, THRS_WIDE_K, 4, THRS_WIDE_K / 2>;
 template <typename LG, typename KM>
 __device__ __attribute__((noinline)) void loc16_write_zero_chunk(uint32_t* __restrict__ keys, KM km,
                                                                  uint32_t start, uint32_t size, uint32_t hiBits,
-                                                                 unsigned char* smem, uint32_t ish) {
+                                                                 unsigned char* smem) {
   constexpr int KPT = LG::KPT;
   constexpr uint32_t CHUNK = 64 * KPT;
   static_assert(LG::CAP / 32 + LG::WAVES + 1 <= (uint32_t)LG::WAVES * kBins, "sign bits fit the counters' LDS");
@@ -1371,7 +1371,7 @@ __device__ __attribute__((noinline)) void loc16_write_zero_chunk(uint32_t* __res
     if (j * 64 < lim) {
       const uint32_t slot = w * CHUNK + 64 * j + lane, r = slot - s0;
       dst[j * 64] = r < z ? (((negBits[r >> 5] >> (r & 31)) & 1u) ? 0x80000000u : 0u)
-                          : kinv<2>(km, hiBits | ((uint32_t)stw[j * LG::ROW] << ish));
+                          : kinv<2>(km, hiBits | (uint32_t)stw[j * LG::ROW]);
     }
   }
 }
@@ -1383,8 +1383,7 @@ __device__ __attribute__((noinline)) void loc16_write_zero_chunk(uint32_t* __res
 template <typename LG, typename KM>
 __device__ __attribute__((noinline)) void loc16_write_zero_log(uint32_t* __restrict__ keys, KM km, uint32_t start,
                                                                uint32_t size, uint32_t hiBits, unsigned char* smem,
-                                                               const uint32_t* __restrict__ zlog, uint32_t z,
-                                                               uint32_t ish) {
+                                                               const uint32_t* __restrict__ zlog, uint32_t z) {
   constexpr int KPT = LG::KPT;
   constexpr uint32_t CHUNK = 64 * KPT;
   static_assert(kZeroLogCap / 32 + 1 <= (uint32_t)LG::WAVES * kBins, "sign bits fit the counters' LDS");
@@ -1399,7 +1398,7 @@ __device__ __attribute__((noinline)) void loc16_write_zero_log(uint32_t* __restr
   const int32_t lim = (int32_t)size - (int32_t)(w * CHUNK + lane);
   uint32_t below = 0;  // sorted items below the zeros' item: the run's start s0
   for (int j = 0; j < KPT; ++j)
-    if (j * 64 < lim) below += (uint32_t)stw[j * LG::ROW] < (zlo >> ish) ? 1u : 0u;
+    if (j * 64 < lim) below += (uint32_t)stw[j * LG::ROW] < zlo ? 1u : 0u;
   atomicAdd(s_s0, below);
   for (uint32_t e = tid; e < z; e += LG::THREADS) {
     const uint32_t x = zlog[e];
@@ -1417,35 +1416,24 @@ __device__ __attribute__((noinline)) void loc16_write_zero_log(uint32_t* __restr
     if (j * 64 < lim) {
       const uint32_t r = w * CHUNK + 64 * j + lane - s0;
       dst[j * 64] = r < z ? (((negBits[r >> 5] >> (r & 31)) & 1u) ? 0x80000000u : 0u)
-                          : kinv<2>(km, hiBits | ((uint32_t)stw[j * LG::ROW] << ish));
+                          : kinv<2>(km, hiBits | (uint32_t)stw[j * LG::ROW]);
     }
   }
 }
 
-template <int KT, bool ATOMIC_RANK, typename LG>
-__global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(LG::WPE))) void thrs_local16(uint32_t* __restrict__ keys, KeyMap<uint32_t> kmh,
-                                                            const uint32_t* __restrict__ chunkOff,
-                                                            const uint32_t* __restrict__ chunkB0,
-                                                            const uint32_t* __restrict__ meta,
-                                                            const uint16_t* __restrict__ lo,
-                                                            const SqueezeWords* __restrict__ sq,
-                                                            const uint32_t* __restrict__ zeroLog) {
+// One chunk of thrs_local16 under the key map km: the plain map, or the
+// squeeze fixed to the chunk's image half (KeyMapHalf).  A device function on
+// a plain branch, not a with_map lambda: the closure and the two-half map
+// spilled the f32 kernel at its 80-VGPR budget (docs/EXPERIMENTS.md row 96).
+template <int KT, bool ATOMIC_RANK, typename LG, typename KM>
+__device__ __forceinline__ void local16_chunk(uint32_t* __restrict__ keys, KM km, uint32_t c, uint32_t start,
+                                              uint32_t size, const uint32_t* __restrict__ chunkB0,
+                                              const uint32_t* __restrict__ meta, const uint16_t* __restrict__ lo,
+                                              const uint32_t* __restrict__ zeroLog) {
   constexpr int KPT = LG::KPT, NP = LG::NP;
   constexpr uint32_t CHUNK = 64 * KPT;
-  const uint32_t c = blockIdx.x;
-  if (c >= meta[kMetaChunks]) return;
-  const uint32_t start = chunkOff[c], size = chunkOff[c + 1] - start;
-  if (size == 0 || size > LG::CAP) return;  // big chunk: the per-bucket fallback sorts it
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  with_map<KT>(kmh, sq, [&](auto km) __attribute__((always_inline)) {
   const uint32_t hiBits = chunkB0[c] << 16;  // the bucket: the image's top 16 bits
-  // A squeezed image half (KeyMap<U, true>) has bit 0 clear in every image:
-  // its items drop that bit (15-bit items), so both LSD rounds count over
-  // contiguous digits (even digits only would leave half the counters' banks
-  // idle and double the conflicts on the others)
-  uint32_t ish = 0;
-  if constexpr (!std::is_same<decltype(km), KeyMap<uint32_t>>::value)
-    ish = ((hiBits >> 31) ? km.loM[1] : km.loM[0]) != 0 ? 1u : 0u;
   uint16_t* stage = reinterpret_cast<uint16_t*>(smem);
   uint32_t* s_cnt = reinterpret_cast<uint32_t*>(smem + LG::STAGE_BYTES);  // [waves][256]
   const uint32_t tid = threadIdx.x, lane = tid & 63;
@@ -1477,8 +1465,8 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(LG:
 #pragma unroll
       for (int jj = 0; jj < LB; jj += 2) {
         const int j = h + jj;
-        const uint32_t a = (j * 64 < lim) ? (uint32_t)raw[jj] >> ish : 0xFFFFu;
-        const uint32_t b = (j + 1 < KPT && (j + 1) * 64 < lim) ? (uint32_t)raw[jj + 1] >> ish : 0xFFFFu;
+        const uint32_t a = (j * 64 < lim) ? (uint32_t)raw[jj] : 0xFFFFu;
+        const uint32_t b = (j + 1 < KPT && (j + 1) * 64 < lim) ? (uint32_t)raw[jj + 1] : 0xFFFFu;
         it[j >> 1] = a | (b << 16);
       }
     }
@@ -1490,9 +1478,9 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(LG:
 #pragma unroll
       for (int jj = 0; jj < LB; jj += 2) {
         const int j = h + jj;
-        const uint32_t a = (j * 64 < lim) ? (kimg<KT>(km, raw[jj]) & 0xFFFFu) >> ish : 0xFFFFu;
+        const uint32_t a = (j * 64 < lim) ? (kimg<KT>(km, raw[jj]) & 0xFFFFu) : 0xFFFFu;
         const uint32_t b =
-            (j + 1 < KPT && (j + 1) * 64 < lim) ? (kimg<KT>(km, raw[jj + 1]) & 0xFFFFu) >> ish : 0xFFFFu;
+            (j + 1 < KPT && (j + 1) * 64 < lim) ? (kimg<KT>(km, raw[jj + 1]) & 0xFFFFu) : 0xFFFFu;
         it[j >> 1] = a | (b << 16);
       }
     }
@@ -1589,40 +1577,76 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(LG:
     // kinv rebuilds it)
     if ((kimg<2>(km, 0u) >> 16) == chunkB0[c]) {
       if (!(lo && meta[kMetaMode] == 0)) {
-        loc16_write_zero_chunk<LG>(keys, km, start, size, hiBits, smem, ish);
+        loc16_write_zero_chunk<LG>(keys, km, start, size, hiBits, smem);
         return;
       }
       if (zeroLog && meta[kMetaNegZero]) {
-        loc16_write_zero_log<LG>(keys, km, start, size, hiBits, smem, zeroLog, meta[kMetaZeroCount], ish);
+        loc16_write_zero_log<LG>(keys, km, start, size, hiBits, smem, zeroLog, meta[kMetaZeroCount]);
         return;
       }
     }
   }
-  // the inverse map on this chunk: its bucket fixes the image half, so a
-  // squeezed map's masks are the chunk's (scalars: no per-key selects)
-  auto inv = [&](uint32_t y) -> uint32_t {
-    if constexpr (!std::is_same<decltype(km), KeyMap<uint32_t>>::value) {
-      const bool hc = ((uint32_t)__builtin_amdgcn_readfirstlane((int)hiBits) >> 31) != 0;
-      const uint32_t hm = hc ? km.hiM[1] : km.hiM[0], lm = hc ? km.loM[1] : km.loM[0],
-                     cs = hc ? km.cst[1] : km.cst[0];
-      y = (y & hm) | ((y >> 1) & lm) | cs;
-      return unbits32<KT>(((y >> km.sh) + km.lo) ^ km.mask);
-    } else {
-      return kinv<KT>(km, y);
-    }
-  };
   // every stage read first (in bounds for all lanes), then the lane-conditional
-  // stores: a read inside the condition would be waited for one at a time
+  // stores: a read inside the condition would be waited for one at a time.
+  // f32 without a key range: the inverse map on one chunk is linear in the
+  // item -- key = k0 ^ item (k0 = the key of item 0), or k0 ^ (item >> 1) in
+  // a squeezed half (its items keep bit 0 clear; the bits below the dropped
+  // one move down by one): one or two operations per key instead of the
+  // float transform and the squeeze.  (u32: the general inverse, already one
+  // to three operations, in a loop of its own -- a lambda costs registers.)
+  if constexpr (KT != 2) {
 #pragma unroll
-  for (int h = 0; h < KPT; h += LB) {
-    uint32_t o[LB];
+    for (int h = 0; h < KPT; h += LB) {
+      uint32_t o[LB];
 #pragma unroll
-    for (int jj = 0; jj < LB; ++jj) o[jj] = stw[(h + jj) * LG::ROW];
+      for (int jj = 0; jj < LB; ++jj) o[jj] = stw[(h + jj) * LG::ROW];
 #pragma unroll
-    for (int jj = 0; jj < LB; ++jj)
-      if ((h + jj) * 64 < lim) src[(h + jj) * 64] = inv(hiBits | (o[jj] << ish));
+      for (int jj = 0; jj < LB; ++jj)
+        if ((h + jj) * 64 < lim) src[(h + jj) * 64] = kinv<KT>(km, hiBits | o[jj]);
+    }
+  } else {
+    auto write_all = [&](auto mode) __attribute__((always_inline)) {
+      constexpr int MODE = decltype(mode)::value;  // 0: general, 1: k0 ^ item, 2: k0 ^ (item >> 1)
+      const uint32_t k0 = kinv<KT>(km, hiBits);
+#pragma unroll
+      for (int h = 0; h < KPT; h += LB) {
+        uint32_t o[LB];
+#pragma unroll
+        for (int jj = 0; jj < LB; ++jj) o[jj] = stw[(h + jj) * LG::ROW];
+#pragma unroll
+        for (int jj = 0; jj < LB; ++jj)
+          if ((h + jj) * 64 < lim)
+            src[(h + jj) * 64] = MODE == 0 ? kinv<KT>(km, hiBits | o[jj]) : MODE == 1 ? k0 ^ o[jj] : k0 ^ (o[jj] >> 1);
+      }
+    };
+    bool sqh = false;
+    if constexpr (!std::is_same<KM, KeyMap<uint32_t>>::value) sqh = km.lm != 0u;
+    if (km.sh != 0u || km.lo != 0u) write_all(std::integral_constant<int, 0>{});
+    else if (sqh) write_all(std::integral_constant<int, 2>{});
+    else write_all(std::integral_constant<int, 1>{});
   }
-  });
+}
+
+template <int KT, bool ATOMIC_RANK, typename LG>
+__global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(LG::WPE))) void thrs_local16(uint32_t* __restrict__ keys, KeyMap<uint32_t> kmh,
+                                                            const uint32_t* __restrict__ chunkOff,
+                                                            const uint32_t* __restrict__ chunkB0,
+                                                            const uint32_t* __restrict__ meta,
+                                                            const uint16_t* __restrict__ lo,
+                                                            const SqueezeWords* __restrict__ sq,
+                                                            const uint32_t* __restrict__ zeroLog) {
+  const uint32_t c = blockIdx.x;
+  if (c >= meta[kMetaChunks]) return;
+  const uint32_t start = chunkOff[c], size = chunkOff[c + 1] - start;
+  if (size == 0 || size > LG::CAP) return;  // big chunk: the per-bucket fallback sorts it
+  if constexpr (kSqueezable<KT>) {
+    if (sq && sq->on) {
+      const int h = (int)(chunkB0[c] >> 15);  // the chunk's image half
+      local16_chunk<KT, ATOMIC_RANK, LG>(keys, half_map(kmh, sq, h), c, start, size, chunkB0, meta, lo, zeroLog);
+      return;
+    }
+  }
+  local16_chunk<KT, ATOMIC_RANK, LG>(keys, kmh, c, start, size, chunkB0, meta, lo, zeroLog);
 }
 
 // ------------------------------------------- local sort, counting (keys only)
@@ -1843,21 +1867,14 @@ __global__ __launch_bounds__(LocCount::THREADS) void thrs_local_count16(
 // rebuilt from the bucket and written, and the values are permuted through
 // the same LDS stage by the carried positions.  f32 keys (+0 and -0 share one
 // image, so they cannot be rebuilt bit-exactly) are permuted the same way.
-// thrs_local_pairs' items: low 16 image bits << 16 | chunk position.  A
-// squeezed half's images all have bit 0 clear -- dropped from the items, as
-// in thrs_local16, so the first round's digits are contiguous (f32 keys
-// travel by position: nothing is rebuilt from the items).  (A function, not
-// a with_map lambda: the closure costs registers.)
+// thrs_local_pairs' items: low 16 image bits << 16 | chunk position.  (A
+// function, not a with_map lambda: the closure costs registers.)
 template <int KT, int KPT, typename KM>
-__device__ __forceinline__ void pairs_items(uint32_t (&it)[KPT], KM km, uint32_t myOff, int32_t lim, uint32_t hiImg) {
-  uint32_t ish = 0;
-  if constexpr (!std::is_same<KM, KeyMap<uint32_t>>::value)
-    ish = ((hiImg >> 31) ? km.loM[1] : km.loM[0]) != 0 ? 1u : 0u;
+__device__ __forceinline__ void pairs_items(uint32_t (&it)[KPT], KM km, uint32_t myOff, int32_t lim) {
 #pragma unroll
   for (int j = 0; j < KPT; ++j) {
     const uint32_t pos = myOff + j * 64;
-    it[j] = (j * 64 < lim) ? ((((uint32_t)kimg<KT>(km, it[j]) & 0xFFFFu) >> ish) << 16 | pos)
-                           : 0xFFFF0000u;  // padding: digits 255
+    it[j] = (j * 64 < lim) ? (((uint32_t)kimg<KT>(km, it[j]) << 16) | pos) : 0xFFFF0000u;  // padding: digits 255
   }
 }
 
@@ -1892,10 +1909,10 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(4))
   load_run<KPT>(it, keys + ch.start, myOff, ch.size, avail);
   // (the squeeze, f32 keys: only the items' images depend on it)
   if constexpr (kSqueezable<KT>) {
-    if (sq && sq->on) pairs_items<KT, KPT>(it, with_squeeze(km, sq), myOff, lim, hiImg);
-    else pairs_items<KT, KPT>(it, km, myOff, lim, hiImg);
+    if (sq && sq->on) pairs_items<KT, KPT>(it, half_map(km, sq, (int)(hiImg >> 31)), myOff, lim);
+    else pairs_items<KT, KPT>(it, km, myOff, lim);
   } else {
-    pairs_items<KT, KPT>(it, km, myOff, lim, hiImg);
+    pairs_items<KT, KPT>(it, km, myOff, lim);
   }
   loc_rounds<0, ATOMIC_RANK, LG>(it, ch, KeyMap<uint32_t>{0u, 0u, 0u}, 16, 2, smem, nullptr);
   pin(reinterpret_cast<uint32_t&>(lim));
@@ -1909,14 +1926,13 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(4))
   // then they travel by position like the values.  The chunk's image half
   // fixes the squeeze's masks (scalars).
   const bool f32Rebuild = KT == 2 && zeroFlag && load_agent(zeroFlag) == 0u;
-  uint32_t hm2 = ~0u, lm2 = 0u, cs2 = 0u, ish2 = 0u;
+  uint32_t hm2 = ~0u, lm2 = 0u, cs2 = 0u;
   if constexpr (KT == 2) {
     if (sq && sq->on) {
-      const int hh = (int)((uint32_t)__builtin_amdgcn_readfirstlane((int)hiImg) >> 31);
+      const int hh = (int)(hiImg >> 31);
       hm2 = (uint32_t)sq->hiM[hh];
       lm2 = (uint32_t)sq->loM[hh];
       cs2 = (uint32_t)sq->cst[hh];
-      ish2 = lm2 != 0u ? 1u : 0u;
     }
   }
   auto f32_key = [&](uint32_t y) -> uint32_t {
@@ -1940,7 +1956,7 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(4))
       if (j < KPT) {
         id[j / 2] |= (j * 64 < lim ? (o[jj] & 0xFFFFu) : 0u) << (16 * (j & 1));
         if (KT == 0 && j * 64 < lim) ksrc[j * 64] = kinv_int(km, hiImg | (o[jj] >> 16));
-        if (KT == 2 && f32Rebuild && j * 64 < lim) ksrc[j * 64] = f32_key(hiImg | ((o[jj] >> 16) << ish2));
+        if (KT == 2 && f32Rebuild && j * 64 < lim) ksrc[j * 64] = f32_key(hiImg | (o[jj] >> 16));
       }
     }
   }

@@ -146,6 +146,37 @@ template <typename U, bool SQ> __device__ __forceinline__ U kinv_int(const KeyMa
   }
   return ((y >> m.sh) + m.lo) ^ m.mask;
 }
+// The squeeze fixed to ONE image half (a local sort's chunk lies in one
+// half: its bucket holds the half bit): scalars instead of per-key selects
+// between the halves' masks, and fewer of them (the 80-VGPR local sort
+// spilled with the two-half map's scalars, docs/EXPERIMENTS.md row 96).
+template <typename U> struct KeyMapHalf {
+  U mask;
+  U lo;
+  uint32_t sh;
+  U hm, lm, cs;  // the half's hiM, loM, cst
+};
+template <typename U> __device__ __forceinline__ KeyMapHalf<U> half_map(const KeyMap<U>& m, const SqueezeWords* s, int h) {
+  KeyMapHalf<U> r;
+  r.mask = m.mask;
+  r.lo = m.lo;
+  r.sh = m.sh;
+  r.hm = (U)(h ? s->hiM[1] : s->hiM[0]);
+  r.lm = (U)(h ? s->loM[1] : s->loM[0]);
+  r.cs = (U)(h ? s->cst[1] : s->cst[0]);
+  return r;
+}
+template <int KT>
+__device__ __forceinline__ typename KeyTraits<KT>::U kimg(const KeyMapHalf<typename KeyTraits<KT>::U>& m,
+                                                          typename KeyTraits<KT>::U k) {
+  using U = typename KeyTraits<KT>::U;
+  const U y = ((KeyTraits<KT>::bits(k) ^ m.mask) - m.lo) << m.sh;
+  return (y & m.hm) | ((y & m.lm) << 1);
+}
+template <typename U> __device__ __forceinline__ U kinv_int(const KeyMapHalf<U>& m, U y) {
+  y = (y & m.hm) | ((y >> 1) & m.lm) | m.cs;
+  return ((y >> m.sh) + m.lo) ^ m.mask;
+}
 // raw 4-byte key whose getKeyBits image is y (inverse of KeyTraits::bits, for
 // images that do not come from -0: -0 and +0 have one image, this gives +0)
 template <int KT> __device__ __forceinline__ uint32_t unbits32(uint32_t y) {
@@ -154,6 +185,9 @@ template <int KT> __device__ __forceinline__ uint32_t unbits32(uint32_t y) {
 }
 // the 4-byte key whose image (under m) is y
 template <int KT, bool SQ> __device__ __forceinline__ uint32_t kinv(const KeyMap<uint32_t, SQ>& m, uint32_t y) {
+  return unbits32<KT>(kinv_int(m, y));
+}
+template <int KT> __device__ __forceinline__ uint32_t kinv(const KeyMapHalf<uint32_t>& m, uint32_t y) {
   return unbits32<KT>(kinv_int(m, y));
 }
 
