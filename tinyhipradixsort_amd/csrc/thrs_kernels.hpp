@@ -1037,12 +1037,31 @@ __device__ __forceinline__ void pass_tile(
     for (int j = 0; j < KPT; ++j) diff |= digit_of(k[j], j) ^ d0;
     allU = __ballot(diff != 0) == 0;
   }
+  // Float keys: the count's digits, four per register, for the rank
+  // (THRS_DIGIT_CACHE): a float key under the squeeze takes ~15 operations to
+  // map, its cached digit two to unpack (kf32v32 -0.19 ms; integer keys map
+  // in one to three operations, and the cache measured neutral to slower
+  // there: docs/EXPERIMENTS.md row 98).
+#ifndef THRS_DIGIT_CACHE
+#define THRS_DIGIT_CACHE 1
+#endif
+  constexpr bool kDC = THRS_DIGIT_CACHE != 0 && !kImg && kSqueezable<KT>;
+  uint32_t dg[kDC ? (KPT + 3) / 4 : 1];
+#pragma unroll
+  for (int q = 0; q < (kDC ? (KPT + 3) / 4 : 1); ++q) dg[q] = 0;
+  auto cached_digit = [&](int j) -> uint32_t {
+    if constexpr (kDC) return (dg[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+    else return digit_of(k[j], j);
+  };
   if (allU) {
     if (lane == 0) __hip_atomic_fetch_add(&cnt[d0], 64u * KPT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   } else {
 #pragma unroll
-    for (int j = 0; j < KPT; ++j)
-      __hip_atomic_fetch_add(&cnt[digit_of(k[j], j)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    for (int j = 0; j < KPT; ++j) {
+      const uint32_t dd = digit_of(k[j], j);
+      if constexpr (kDC) dg[j >> 2] |= dd << (8 * (j & 3));
+      __hip_atomic_fetch_add(&cnt[dd], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
   }
   lds_barrier();
   THRS_STAMP(2);
@@ -1121,7 +1140,7 @@ __device__ __forceinline__ void pass_tile(
   // every item waited a full LDS round trip
   constexpr int RP = THRS_RANK_PIPE;
   auto rank_atomic = [&](int j) -> uint32_t {
-    return __hip_atomic_fetch_add(&cnt[digit_of(k[j], j)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return __hip_atomic_fetch_add(&cnt[cached_digit(j)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   };
   auto place = [&](int j, uint32_t slot) __attribute__((always_inline)) {
     if constexpr (ROUNDS == 1) {
@@ -1160,7 +1179,7 @@ __device__ __forceinline__ void pass_tile(
         }
       } else {
         pin(k[j]);  // keep item j's digit/address math inside iteration j (register pressure)
-        slot = wave_rank<false>(cnt, digit_of(k[j], j), lane, false);
+        slot = wave_rank<false>(cnt, cached_digit(j), lane, false);
       }
       place(j, slot);
       __builtin_amdgcn_sched_barrier(0);
