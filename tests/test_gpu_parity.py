@@ -862,3 +862,47 @@ def test_f32_planes_signed_zeros(gpu, zeros, desc):
     assert TU.fingerprint(2, keys, n) == fp
     zout = k32[(k32 & 0x7FFFFFFF) == 0]
     assert torch.equal(zout, zin)
+
+
+@pytest.mark.parametrize("desc", [False, True])
+def test_f32_planes_with_key_range(gpu, desc):
+    """The multi-GPU finish's shape for f32 keys: 2^28 keys with a keyRange
+    (thrs_options.keyRange, the split's [lo, hi]) on the image planes, with
+    +0 / -0 keys inside the range (the zero log) -- the local sort then takes
+    the general inverse map (the linear per-chunk rebuild needs no range).
+    Checked on the GPU: mode 0, sortedness, the raw-bit multiset and the
+    zeros' raw bits in input order."""
+    torch = gpu
+    from tinyhipradixsort_amd import testutil as TU
+    n = 1 << 28
+    g = torch.Generator(device="cuda")
+    g.manual_seed(4242 + int(desc))
+    # images uniform in [0x7F000000, 0x81000000): floats on both sides of zero
+    # (down to the denormals), uniform in the range's image space as the
+    # split of a uniform distribution is
+    im = torch.randint(0, 1 << 25, (n,), device="cuda", generator=g, dtype=torch.int64) + 0x7F000000
+    raw = torch.where(im >= 0x80000000, im ^ 0x80000000, im ^ 0xFFFFFFFF)
+    k32 = torch.where(raw >= 0x80000000, raw - (1 << 32), raw).to(torch.int32)
+    idx = torch.arange(11, n, n // 600 + 1, device="cuda")
+    k32[idx] = 0
+    k32[idx[::4]] = -(1 << 31)
+    keys = k32.view(torch.uint8)
+    zin = k32[(k32 & 0x7FFFFFFF) == 0].clone()
+    b = k32.to(torch.int64) & 0xFFFFFFFF
+    b = torch.where((b & 0x7FFFFFFF) == 0, torch.zeros_like(b), b)       # getKeyBits: -0 -> +0
+    img = torch.where(b >= 0x80000000, b ^ 0xFFFFFFFF, b ^ 0x80000000)
+    if desc:
+        img = img ^ 0xFFFFFFFF
+    lo, hi = int(img.min().item()), int(img.max().item())
+    fp = TU.fingerprint(2, keys, n)
+    rs = make_sorter(2, 0, desc, keyRange=(lo, hi))
+    assert rs.pathInfo(n, 0, 32, False)["planes"]
+    tmp = torch.empty(rs.getTemporaryBufferBytes(n).getTemporaryBufferBytesForSortKeys(), dtype=torch.uint8,
+                      device="cuda")
+    rs.sortKeys(keys, n, tmp, 0, 32)
+    torch.cuda.synchronize()
+    rs.checkDeviceError(tmp)
+    assert rs.debugBucketMode(tmp, n, False) == (0, 0)
+    assert TU.count_unsorted(2, keys, n, 0, 32, descending=desc) == 0
+    assert TU.fingerprint(2, keys, n) == fp
+    assert torch.equal(k32[(k32 & 0x7FFFFFFF) == 0], zin)
