@@ -563,8 +563,8 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     const int hgrid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cu_count() * THRS_HIST_GRID_MULT));
     if (bucket) {
       if (squeeze)  // the sample's guess at the squeeze, for the first histogram
-        hipLaunchKernelGGL(thrs_squeeze_sample<KT>, dim3(1), dim3(kSqSampleThreads), 0, stream,
-                           static_cast<const U*>(keys), n, km, cap, sample);
+        hipLaunchKernelGGL(thrs_squeeze_sample<KT>, dim3(kSqBlocks), dim3(kSqSampleThreads), 0, stream,
+                           static_cast<const U*>(keys), n, km, cap, sample, meta);
       {
         ProfScope prof(stream, 0, THRS_PK_HIST_JOINT, keyBytes);
         hipLaunchKernelGGL(thrs_hist_joint<KT>, dim3(hgrid), dim3(kHistThreads), kJointLds, stream,

@@ -69,6 +69,10 @@ enum {
   kMetaSqViol = 41,     // a key broke the sampled squeeze (its dropped bit differs): histogram again, plain
   kMetaNegZero = 42,    // f32: some key is -0 (thrs_hist_joint)
   kMetaZeroCount = 43,  // f32: keys that are +-0 (their first kZeroLogCap positions in the zero log)
+  kMetaSqO1 = 44,       // [2]: the sample's per-half OR of bucket indices (thrs_squeeze_sample)
+  kMetaSqO0 = 46,       // [2]: ... and of their complements
+  kMetaSqCnt = 30,      // [2]: ... and its keys per half
+  kMetaSqDone = 62,     // the sample's finished workgroups (the last one decides)
   kMetaSqueeze = 48,    // SqueezeWords (14 words, to 61)
 };
 static_assert(kMetaSqueeze * 4 + sizeof(SqueezeWords) <= 256, "meta is 64 words");
@@ -108,6 +112,34 @@ __device__ __forceinline__ uint64_t hj_len(uint32_t n, uint32_t G) {
 __device__ __forceinline__ uint32_t hj_seg_pos(uint32_t n, uint32_t G, uint32_t s) {
   const uint64_t first = ((uint64_t)s * G + kSegs - 1) / kSegs;
   return (uint32_t)min((uint64_t)n, first * hj_len(n, G));
+}
+
+// The zero log's rare path (f32, thrs_hist_joint): the +-0 keys among the
+// 4 * un words kv[i + u * gstride] (u < un, below nv), with their positions
+// and signs.  Not inlined: its registers must not count against the
+// histogram's loop (128 VGPRs).
+__device__ __attribute__((noinline)) void hist_log_zeros(const uint4* __restrict__ kv, uint64_t i, uint64_t gstride,
+                                                         uint64_t nv, int un, uint32_t* __restrict__ meta,
+                                                         uint32_t* __restrict__ zeroLog) {
+  for (int u = 0; u < un; ++u) {
+    const uint64_t v = i + u * gstride;
+    if (v >= nv) continue;
+    const uint4 x = kv[v];
+    const uint32_t w4[4] = {x.x, x.y, x.z, x.w};
+    for (int c = 0; c < 4; ++c) {
+      const uint32_t k = w4[c];
+      const uint64_t pos = 4 * v + c;
+      if ((k & 0x7FFFFFFFu) != 0) continue;
+      const bool neg = k != 0;
+      if (neg) atomicOr(&meta[kMetaNegZero], 1u);
+      if (pos >> 31) {  // (a position past 2^31 does not fit the log's 31 bits: the log counts as full)
+        atomicMax(&meta[kMetaZeroCount], kZeroLogCap + 1);
+        continue;
+      }
+      const uint32_t slot = atomicAdd(&meta[kMetaZeroCount], 1u);
+      if (slot < kZeroLogCap) zeroLog[slot] = (uint32_t)pos | (neg ? 0x80000000u : 0u);
+    }
+  }
 }
 
 // Float keys (the squeeze, KeyMap<U, true>): the map is sq's when sq->on.
@@ -284,19 +316,7 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
       }
       constexpr int E = UN * PER;
       if constexpr (kZeros) {
-        if (zany && zeroLog) {  // (rare) this iteration's zeros: read its keys again
-#pragma unroll 1
-          for (int u = 0; u < UN; ++u) {
-            const uint64_t v = i + u * gstride;
-            if (v < nv) {
-              const uint4 x = kv[v];
-              log_zero(x.x, 4 * v);
-              log_zero(x.y, 4 * v + 1);
-              log_zero(x.z, 4 * v + 2);
-              log_zero(x.w, 4 * v + 3);
-            }
-          }
-        }
+        if (zany && zeroLog) hist_log_zeros(kv, i, gstride, nv, UN, meta, zeroLog);  // (rare) read again
         zany = 0;
       }
       if (v0 + (it + 1) * UN * gstride <= nv) {  // every element of every lane is in the range
@@ -424,43 +444,49 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
 // key (meta[kMetaSqViol]) and the plan then histograms again, plainly.
 constexpr int kSqSampleThreads = 256;
 constexpr uint32_t kSqSample = 8192;  // keys sampled (kSqSample / 256 runs of 256)
+// One workgroup per run (kSqBlocks = 32 runs of 256 consecutive keys, evenly
+// spaced): the runs' address translations and loads proceed on 32 CUs at
+// once (one workgroup loading all 32 took ~17 us); partial ORs and counts go
+// to meta (zeroed with it), the last workgroup decides.
+constexpr uint32_t kSqBlocks = kSqSample / kSqSampleThreads;
 template <int KT>
 __global__ __launch_bounds__(kSqSampleThreads) void thrs_squeeze_sample(const typename KeyTraits<KT>::U* __restrict__ keys,
                                                                         uint32_t n, KeyMap<typename KeyTraits<KT>::U> km,
-                                                                        uint32_t cap, SqueezeWords* __restrict__ out) {
+                                                                        uint32_t cap, SqueezeWords* __restrict__ out,
+                                                                        uint32_t* __restrict__ meta) {
   using U = typename KeyTraits<KT>::U;
   constexpr int W = 8 * (int)sizeof(U);
-  __shared__ uint32_t s_o1[2], s_o0[2], s_cnt[2];
-  const uint32_t t = threadIdx.x;
+  __shared__ uint32_t s_o1[2], s_o0[2], s_cnt[2], s_last;
+  const uint32_t t = threadIdx.x, j = blockIdx.x;
   if (t < 2) s_o1[t] = s_o0[t] = s_cnt[t] = 0;
   __syncthreads();
-  uint32_t o1[2] = {0, 0}, o0[2] = {0, 0}, c[2] = {0, 0};
-  // kSqBlocks runs of kSqSampleThreads consecutive keys, evenly spaced: one
-  // address translation per run (single keys 2^17 apart missed the TLB once
-  // each: ~3 ms at 2^30, docs/EXPERIMENTS.md row 86), loads all in flight
-  constexpr uint32_t kSqBlocks = kSqSample / kSqSampleThreads;
-  U kk[kSqBlocks];
-#pragma unroll
-  for (uint32_t j = 0; j < kSqBlocks; ++j) {
+  {
     const uint64_t i = (uint64_t)j * n / kSqBlocks + t;
-    kk[j] = keys[min(i, (uint64_t)n - 1)];
-  }
-  for (uint32_t j = 0; j < kSqBlocks; ++j) {
-    const uint32_t b = (uint32_t)(kimg<KT>(km, kk[j]) >> (W - 16)) & 0xFFFFu;
+    const uint32_t b = (uint32_t)(kimg<KT>(km, keys[min(i, (uint64_t)n - 1)]) >> (W - 16)) & 0xFFFFu;
     const int h = b >> 15;
-    o1[h] |= b;
-    o0[h] |= ~b & 0xFFFFu;
-    ++c[h];
-  }
-  for (int h = 0; h < 2; ++h) {
-    if (c[h]) {
-      atomicOr(&s_o1[h], o1[h]);
-      atomicOr(&s_o0[h], o0[h]);
-      atomicAdd(&s_cnt[h], c[h]);
-    }
+    atomicOr(&s_o1[h], b);
+    atomicOr(&s_o0[h], ~b & 0xFFFFu);
+    atomicAdd(&s_cnt[h], 1u);
   }
   __syncthreads();
-  if (t != 0) return;
+  if (t < 2 && s_cnt[t]) {
+    atomicOr(&meta[kMetaSqO1 + t], s_o1[t]);
+    atomicOr(&meta[kMetaSqO0 + t], s_o0[t]);
+    atomicAdd(&meta[kMetaSqCnt + t], s_cnt[t]);
+  }
+  __syncthreads();  // (both threads' contributions before thread 0's arrival)
+  if (t == 0) {
+    __threadfence();
+    s_last = atomicAdd(&meta[kMetaSqDone], 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (t != 0 || !s_last) return;
+  __threadfence();
+  for (int h = 0; h < 2; ++h) {
+    s_o1[h] = load_agent(&meta[kMetaSqO1 + h]);
+    s_o0[h] = load_agent(&meta[kMetaSqO0 + h]);
+    s_cnt[h] = load_agent(&meta[kMetaSqCnt + h]);
+  }
   const uint32_t total = s_cnt[0] + s_cnt[1];
   bool any = false;
   uint64_t hiM[2], loM[2], cst[2];
