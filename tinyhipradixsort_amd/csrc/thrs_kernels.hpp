@@ -622,7 +622,7 @@ template <> struct PassCfg<4, 0> {
 #define THRS_K4V16_CFG 16, 8, 2, 4
 #endif
 #ifndef THRS_K8V0_CFG
-#define THRS_K8V0_CFG 16, 16, 2, 4
+#define THRS_K8V0_CFG 16, 16, 1, 4
 #endif
 #ifndef THRS_K8V4_CFG
 #define THRS_K8V4_CFG 16, 16, 4, 4
