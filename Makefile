@@ -10,7 +10,7 @@ HIPFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -fvisibility=hidden -Iin
 PKG := tinyhipradixsort_amd
 CSRC := $(PKG)/csrc
 KSRC := $(CSRC)/thrs_host.hpp $(CSRC)/thrs_kernels.hpp $(CSRC)/thrs_hybrid.hpp $(CSRC)/thrs_fallback.hpp \
-        $(CSRC)/thrs_pipe.hpp include/thrs/thrs_capi.h
+        include/thrs/thrs_capi.h
 .DEFAULT_GOAL := all
 KTS := 0 1 2 3
 
@@ -28,8 +28,9 @@ OBJ := build/obj
 OBJ_SPIN0 := build/obj_spin0
 $(eval $(call objset,$(OBJ),))
 # fault-injection build for the error-path tests only: every look-back /
-# claim wait gives up at its first unpublished predecessor (THRS_SPIN_MAX=0)
-$(eval $(call objset,$(OBJ_SPIN0),-DTHRS_SPIN_MAX=0))
+# claim wait gives up at its first unpublished predecessor (THRS_SPIN_MAX=0),
+# and thrs_debug_inject can make a plan's big-chunk list stale (THRS_FAULT_INJECT)
+$(eval $(call objset,$(OBJ_SPIN0),-DTHRS_SPIN_MAX=0 -DTHRS_FAULT_INJECT))
 
 all: $(PKG)/libthrs.so $(PKG)/libthrs_testutil.so $(PKG)/libthrs_vendor.so $(PKG)/libthrs_spin0.so \
      tests/cpp/unittest_thrs examples/helloworld oracle

@@ -483,6 +483,10 @@ def main():
             gen(keys[i], i)
             if vb:
                 TU.iota(vb, vals[i], n)
+        # keys-only: an order-independent fingerprint of every timed input
+        # (checked against its output after the timed region: a dropped or
+        # duplicated key cannot pass as sorted output)
+        fps = [TU.fingerprint(kt, keys[i], n) for i in range(steps)] if not vb and not args.unchecked else None
         torch.cuda.synchronize()
         T.profile_enable(True)
         barrier()
@@ -503,6 +507,10 @@ def main():
         bad = 0 if args.unchecked else TU.count_unsorted(kt, keys[last], n, 0, kb * 8)
         if bad:
             raise SystemExit(f"bench: output of the last step is not sorted ({bad} inversions)")
+        if fps is not None:
+            lost = [i for i in range(steps) if TU.fingerprint(kt, keys[i], n) != fps[i]]
+            if lost:
+                raise SystemExit(f"bench: steps {lost} lost or duplicated keys (multiset fingerprint differs)")
         if vb and not args.unchecked:
             chk = TU.check_pairs(kt, vb, keys_in0, keys[last], vals[last], n, 0, kb * 8)
             if chk["gather_mismatch"] or chk["unstable"]:

@@ -28,7 +28,7 @@ extern "C" {
 typedef struct ihipStream_t* hipStream_t; /* identical to HIP's own typedef */
 #endif
 
-#define THRS_ABI_VERSION 4
+#define THRS_ABI_VERSION 5
 
 typedef enum thrs_status {
   THRS_SUCCESS = 0,
@@ -36,7 +36,10 @@ typedef enum thrs_status {
   THRS_ERROR_BIT_RANGE = -2,       /* (endBits-startBits)%8 != 0 (hpp:856)    */
   THRS_ERROR_HIP = -3,             /* a HIP runtime call failed               */
   THRS_ERROR_OUT_OF_MEMORY = -4,   /* thrs_malloc failed                      */
-  THRS_ERROR_LOOKBACK_TIMEOUT = -5 /* device look-back spin bound hit         */
+  THRS_ERROR_LOOKBACK_TIMEOUT = -5, /* device look-back spin bound hit        */
+  THRS_ERROR_DEVICE_CHECK = -6     /* a device-side range check failed: a
+                                      digit run or bucket id past its table
+                                      was clamped (output is wrong)         */
 } thrs_status;
 
 /* == thrs::KeyType / ValueType / SortOrder (tinyhipradixsort.hpp:638-683) */
@@ -66,6 +69,7 @@ enum { THRS_CLAIMS_AUTO = 0, THRS_CLAIMS_XCD_BLOCKS = 1, THRS_CLAIMS_TICKET = 2 
 enum { THRS_RANK_AUTO = 0, THRS_RANK_ATOMIC = 1, THRS_RANK_BALLOT = 2 };
 enum { THRS_PLANES_AUTO = 0, THRS_PLANES_ON = 1, THRS_PLANES_OFF = 2 };
 enum { THRS_SQUEEZE_AUTO = 0, THRS_SQUEEZE_OFF = 1 };
+enum { THRS_OFFSETS_AUTO = 0, THRS_OFFSETS_LOOKBACK = 1, THRS_OFFSETS_RESERVE = 2, THRS_OFFSETS_RESERVE_FIRST = 3 };
 typedef struct thrs_options {
   int32_t path;          /* THRS_PATH_*: LSD = one device pass per digit; BUCKET = the
                             3-HBM-pass path wherever the key/value types and window
@@ -108,6 +112,15 @@ typedef struct thrs_options {
                             reference's float generator clears one, unittest.cpp:103,
                             108); AUTO = when the buckets would overflow, OFF = never.
                             Same bytes either way.                                   */
+  int32_t offsets;       /* THRS_OFFSETS_*: how a keys-only top-digit pass of the
+                            bucket path places a tile's digit runs: LOOKBACK = the
+                            decoupled look-back chain (stable); RESERVE = one
+                            atomic reservation per digit on its segment's cursor
+                            (no chain; equal keys of a keys-only sort are
+                            identical, so the output bytes are the same);
+                            RESERVE_FIRST = only the first of the two passes.
+                            AUTO = LOOKBACK (measured faster).                 */
+  int32_t pad0;          /* must be 0 */
   uint64_t rangeLo;
   uint64_t rangeHi;
 } thrs_options;
@@ -202,8 +215,10 @@ int thrs_digit_histogram_batch(const thrs_config* config, const void* keys, cons
  * keyRange holding one key) launches no kernel and clears the word, so its
  * check reports success.
  *   thrs_check_device_error         synchronises `stream`; returns
- *                                   THRS_ERROR_LOOKBACK_TIMEOUT if the last sort
- *                                   on `temporaryBuffer` failed;
+ *                                   THRS_ERROR_LOOKBACK_TIMEOUT (a wait gave up)
+ *                                   or THRS_ERROR_DEVICE_CHECK (a range check
+ *                                   clamped a run) if the last sort on
+ *                                   `temporaryBuffer` failed;
  *   thrs_accumulate_device_error    stream-ordered, no synchronisation:
  *                                   *acc |= that sort's error word (device
  *                                   memory, u32), so a sequence of sorts on one
@@ -245,7 +260,8 @@ int thrs_profile_read_launches(int kind, double* ms, int cap, int* count);
 enum { THRS_PK_ZERO = 0, THRS_PK_HIST = 1, THRS_PK_SCAN = 2, THRS_PK_HIST_JOINT = 3, THRS_PK_PLAN = 4,
        THRS_PK_PASS = 5, THRS_PK_PASS_XB = 6, THRS_PK_PASS_SEG = 7, THRS_PK_LOCAL16 = 8, THRS_PK_LOCAL = 9,
        THRS_PK_LOCAL_PAIRS = 10, THRS_PK_LOCAL_KV = 11, THRS_PK_LOCAL_COUNT16 = 12, THRS_PK_BIG_PLAN = 13,
-       THRS_PK_BIG_HIST = 14, THRS_PK_PASS_BIG = 15, THRS_PK_BIG_COPY = 16, THRS_PK_COPY = 17 };
+       THRS_PK_BIG_HIST = 14, THRS_PK_PASS_BIG = 15, THRS_PK_BIG_COPY = 16, THRS_PK_COPY = 17,
+       THRS_PK_SQUEEZE_SAMPLE = 18 };
 int thrs_profile_read_launch_kernels(int kind, int32_t* kernel, uint64_t* bytes, int cap, int* count);
 /* The kernel function's name for a THRS_PK_* id ("" for an unknown id). */
 const char* thrs_profile_kernel_name(int kernel);

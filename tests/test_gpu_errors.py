@@ -196,3 +196,65 @@ def test_forced_timeout_on_the_bucket_path_stays_in_bounds():
     assert res["sorts"] == 7 and res["guards_ok"] == 7, res
     assert res["failed"] >= 1 and res["reported"] == res["failed"], res
     assert res["other_ok"], res
+
+
+INJECT = r"""
+import sys, ctypes, torch
+import numpy as np
+sys.path.insert(0, {root!r})
+import tinyhipradixsort_amd as T
+from tinyhipradixsort_amd import testutil as TU
+T.LIB_PATH = {lib!r}
+torch.cuda.set_device(0)
+L = T.lib()
+L.thrs_debug_inject.argtypes = [ctypes.c_int]
+GUARD = 1 << 20
+def guarded(nbytes):
+    buf = torch.full((nbytes + 2 * GUARD,), 0xA5, dtype=torch.uint8, device="cuda")
+    return buf, buf[GUARD:GUARD + nbytes]
+def guards_ok(buf):
+    return bool((buf[:GUARD] == 0xA5).all().item()) and bool((buf[-GUARD:] == 0xA5).all().item())
+# two buckets of 15000 keys each (above the small local sort's 9216): the plan
+# lists two big chunks; every tile chain is one tile long, so nothing spins
+n = 30000
+rng = np.random.default_rng(5)
+host = ((np.arange(n, dtype=np.uint32) % 2) << 16) | rng.integers(0, 1 << 16, n, dtype=np.uint32)
+rs = T.RadixSort([], T.RadixSort.Config(), T.Options(path="bucket"))
+tbytes = rs.getTemporaryBufferBytes(n).getTemporaryBufferBytesForSortKeys()
+res = {{}}
+for inject in (1, 0):
+    L.thrs_debug_inject(inject)
+    kbuf, keys = guarded(4 * n)
+    tbuf, tmp = guarded(tbytes)
+    keys.copy_(torch.from_numpy(host.view(np.uint8)).cuda())
+    acc = torch.zeros(1, dtype=torch.int32, device="cuda")
+    status = 0
+    try:
+        rs.sortKeys(keys, n, tmp, 0, 32, checked=True)
+    except T.ThrsError as e:
+        status = e.status
+    rs.accumulateDeviceError(tmp, acc)
+    torch.cuda.synchronize()
+    out = keys.cpu().numpy().view(np.uint32)
+    res[inject] = dict(status=status, word=int(acc.item()), guards=guards_ok(kbuf) and guards_ok(tbuf),
+                       exact=bool(np.array_equal(out, np.sort(host))))
+    try:
+        T.take_device_error()
+    except T.ThrsError:
+        pass
+print(res)
+"""
+
+
+def test_stale_big_chunk_entry_is_reported():
+    """a stale entry in the plan's big-chunk list (the
+    round-4 ordering bug's shape) is caught by thrs_plan_rows's check, never
+    addresses past a table, and reaches the caller as THRS_ERROR_DEVICE_CHECK
+    (error word bit 1, no timeout bit).  The same sort without the injection
+    is exact.  (libthrs_spin0.so: built with THRS_FAULT_INJECT.)"""
+    lib = os.path.join(ROOT, "tinyhipradixsort_amd", "libthrs_spin0.so")
+    assert os.path.exists(lib), "build it first (make)"
+    res = _run(INJECT.format(root=ROOT, lib=lib))
+    print(res)
+    assert res[1]["status"] == -6 and res[1]["word"] == 2 and res[1]["guards"], res
+    assert res[0] == dict(status=0, word=0, guards=True, exact=True), res

@@ -783,6 +783,48 @@ def test_squeeze_vs_oracle(gpu, kt, vb, desc, fits):
     assert mode == (0 if fits else 1), (mode, big)
 
 
+@pytest.mark.parametrize("kt,vb", [(O.F32, 0), (O.F32, 4), (O.F64, 0), (O.F64, 8)])
+@pytest.mark.parametrize("desc", [False, True])
+def test_squeeze_sample_violation(gpu, kt, vb, desc):
+    """the SAMPLED squeeze guessed wrong.  thrs_squeeze_sample
+    reads 32 evenly spaced runs of 256 keys (thrs_hybrid.hpp kSqBlocks); keys
+    outside those runs flip the bucket bit the sample finds constant (the
+    highest constant bit of each half), so the first histogram's check raises
+    meta[kMetaSqViol], the plan drops the guess and the keys are histogrammed
+    again under the PLAIN map.  Bit-exact with the oracle, and the plan's mode
+    is the one the plain map implies (its overflowing buckets: mode 1)."""
+    torch = gpu
+    kb = O.KEY_BYTES[kt]
+    kdt = O.KEY_DTYPE[kt]
+    W = 8 * kb
+    n = (1 << 20) + 333
+    kv = kb == 8 or vb >= 8
+    keys = _squeeze_case_keys(kt, n, desc, 5 if kv else 6, 97 * kb + vb + (5 if desc else 0))
+    img = O.key_bits_np(kt, keys, desc).astype(kdt)
+    # the sampled runs: [j n / 32, j n / 32 + 256), j < 32; one violator in
+    # every gap, its field bit 14 (constant 0 or 1 per half in both
+    # constructions) flipped
+    pos = np.array([j * n // 32 + 4096 + 7 * j for j in range(32)])
+    img[pos] ^= kdt(1) << kdt(W - 2)
+    keys = _float_keys_from_images(kt, img, desc)
+    assert np.array_equal(O.key_bits_np(kt, keys, desc).astype(kdt), img)
+    vals = None
+    if vb:
+        vals = (np.arange(n * vb // 4, dtype=np.uint32) * np.uint32(2654435761)).view(
+            {4: np.uint32, 8: np.uint64}[vb])
+    ek, ev = O.lsd_sort(kt, keys, vals, 0, W, desc)
+    rs = make_sorter(kt, vb, desc, path="bucket")
+    cap = rs.pathInfo(n, 0, W, bool(vb))["local_cap"]
+    cnt = np.bincount((img.astype(np.uint64) >> np.uint64(W - 16)).astype(np.int64), minlength=65536)
+    ebig = int((cnt > cap).sum())
+    assert ebig > 0
+    (mode, big), k, v = _mode_after(torch, rs, keys, vals, kt, vb)
+    assert np.array_equal(k.view(kdt), ek.view(kdt)), (mode, big)
+    if vb:
+        assert np.array_equal(v, ev)
+    assert (mode, big) == (1, ebig), (mode, big, ebig)
+
+
 @pytest.mark.large
 @pytest.mark.parametrize("kt,vb,n", [(O.F32, 0, 1 << 30),    # f32 keys-only, the reference's generator
                                      (O.F32, 4, 1 << 30),    # SortPairs.KF32V32's distribution (unittest.cpp:433-439)

@@ -71,6 +71,7 @@ void prof_end(hipEvent_t a, hipStream_t s, int kind, int kernel, uint64_t bytes)
 }
 
 uint64_t* g_stamps = nullptr;
+int g_inject = 0;
 uint64_t* g_lstamps = nullptr;
 
 // Per-device result of thrs_probe_lds_order: 1 = lane-ordered LDS atomics
@@ -154,12 +155,19 @@ uint32_t take_sticky() {
 }
 
 namespace {
+// the error word's bits (thrs_kernels.hpp kErrSpin / kErrRunClamped) -> status
+int status_of_error_word(uint32_t e) {
+  if (e & thrs_dev::kErrSpin) return THRS_ERROR_LOOKBACK_TIMEOUT;
+  return e ? THRS_ERROR_DEVICE_CHECK : THRS_SUCCESS;
+}
+
 bool valid_options(const thrs_options& o) {
   return o.path >= THRS_PATH_AUTO && o.path <= THRS_PATH_BUCKET && o.localGeometry >= THRS_LOCAL_AUTO &&
          o.localGeometry <= THRS_LOCAL_WIDE16 && o.segmented >= THRS_SEG_AUTO && o.segmented <= THRS_SEG_NONE &&
          o.tileClaims >= THRS_CLAIMS_AUTO && o.tileClaims <= THRS_CLAIMS_TICKET && o.rank >= THRS_RANK_AUTO &&
          o.rank <= THRS_RANK_BALLOT && o.planes >= THRS_PLANES_AUTO && o.planes <= THRS_PLANES_OFF &&
-         (o.squeeze == THRS_SQUEEZE_AUTO || o.squeeze == THRS_SQUEEZE_OFF) &&
+         (o.squeeze == THRS_SQUEEZE_AUTO || o.squeeze == THRS_SQUEEZE_OFF) && o.offsets >= THRS_OFFSETS_AUTO &&
+         o.offsets <= THRS_OFFSETS_RESERVE_FIRST && o.pad0 == 0 &&
          (o.keyRange == 0 || (o.keyRange == 1 && o.rangeLo <= o.rangeHi));
 }
 
@@ -268,6 +276,7 @@ THRS_API const char* thrs_status_string(int s) {
     case THRS_ERROR_HIP: return "THRS_ERROR_HIP";
     case THRS_ERROR_OUT_OF_MEMORY: return "THRS_ERROR_OUT_OF_MEMORY";
     case THRS_ERROR_LOOKBACK_TIMEOUT: return "THRS_ERROR_LOOKBACK_TIMEOUT";
+    case THRS_ERROR_DEVICE_CHECK: return "THRS_ERROR_DEVICE_CHECK: a device-side range check clamped a run";
   }
   return "THRS_UNKNOWN_STATUS";
 }
@@ -384,7 +393,9 @@ THRS_API int thrs_debug_big_keys(const void* tmp, int keyType, int valueBytes, u
     return THRS_ERROR_HIP;
   *keys = 0;
   const uint32_t m = meta[kMetaBigCount];
-  if (meta[kMetaMode] != 1 || m == 0 || m > kBuckets) return THRS_SUCCESS;
+  // (mode 1: big chunks beside local ones; mode 2: one bucket holds every key
+  // and is the one big chunk -- the fallback sorts all n keys)
+  if ((meta[kMetaMode] != 1 && meta[kMetaMode] != 2) || m == 0 || m > kBuckets) return THRS_SUCCESS;
   uint32_t total = 0;
   if (hipMemcpyAsync(&total, hyb + kBigPosOff + (uint64_t)m * 4, 4, hipMemcpyDeviceToHost, stream) != hipSuccess ||
       hipStreamSynchronize(stream) != hipSuccess)
@@ -400,7 +411,7 @@ THRS_API int thrs_check_device_error(void* tmp, hipStream_t stream) {
           hipSuccess ||
       hipStreamSynchronize(stream) != hipSuccess)
     return THRS_ERROR_HIP;
-  return err ? THRS_ERROR_LOOKBACK_TIMEOUT : THRS_SUCCESS;
+  return status_of_error_word(err);
 }
 
 THRS_API int thrs_accumulate_device_error(const void* tmp, uint32_t* acc, hipStream_t stream) {
@@ -410,7 +421,7 @@ THRS_API int thrs_accumulate_device_error(const void* tmp, uint32_t* acc, hipStr
   return hipGetLastError() == hipSuccess ? THRS_SUCCESS : THRS_ERROR_HIP;
 }
 
-THRS_API int thrs_take_device_error(void) { return take_sticky() ? THRS_ERROR_LOOKBACK_TIMEOUT : THRS_SUCCESS; }
+THRS_API int thrs_take_device_error(void) { return status_of_error_word(take_sticky()); }
 
 THRS_API int thrs_profile_enable(int enable) {
   std::lock_guard<std::mutex> g(g_prof_mu);
@@ -477,7 +488,8 @@ THRS_API const char* thrs_profile_kernel_name(int kernel) {
   static const char* names[] = {"thrs_zero_ranges", "thrs_hist", "thrs_scan", "thrs_hist_joint", "thrs_plan",
                                 "thrs_pass", "thrs_pass_xb", "thrs_pass_seg", "thrs_local16", "thrs_local",
                                 "thrs_local_pairs", "thrs_local_kv", "thrs_local_count16", "thrs_big_plan",
-                                "thrs_big_hist", "thrs_pass_big", "thrs_big_copy", "copy-back"};
+                                "thrs_big_hist", "thrs_pass_big", "thrs_big_copy", "copy-back",
+                                "thrs_squeeze_sample"};
   return kernel >= 0 && kernel < (int)(sizeof(names) / sizeof(names[0])) ? names[kernel] : "";
 }
 
@@ -545,6 +557,16 @@ THRS_API int thrs_debug_set_stamps(void* buf) {
   g_stamps = static_cast<uint64_t*>(buf);
   return THRS_SUCCESS;
 }
+
+#ifdef THRS_FAULT_INJECT
+// Fault-injection builds only (libthrs_spin0.so; not in libthrs.so): bit 0 =
+// every bucket-path plan with big chunks gets a stale first entry, which its
+// check must catch (THRS_ERROR_DEVICE_CHECK, no out-of-bounds access).
+THRS_API int thrs_debug_inject(int what) {
+  g_inject = what;
+  return THRS_SUCCESS;
+}
+#endif
 
 // Diagnostic hook: in -DTHRS_STAMPS builds the local sort kernel writes
 // per-chunk phase timestamps to buf[chunk*8+i] (thrs_hybrid.hpp loc_stamp).

@@ -30,17 +30,10 @@
 #include "thrs_kernels.hpp"
 #include "thrs_hybrid.hpp"
 #include "thrs_fallback.hpp"
-#include "thrs_pipe.hpp"
 
 namespace thrs_host {
 using namespace thrs_dev;
 
-#ifndef THRS_SEG_MERGE
-#define THRS_SEG_MERGE 0  // experiment: see thrs_pass_seg ALT
-#endif
-#ifndef THRS_SEG_PIPE
-#define THRS_SEG_PIPE 0  // experiment: 4-byte keys-only top-digit passes software-pipelined (thrs_pipe.hpp)
-#endif
 
 constexpr uint64_t kAlign = 256;
 // the bucket path's lower bounds (default path; docs/EXPERIMENTS.md row 87)
@@ -78,7 +71,7 @@ inline uint64_t tile_keys(int kb, int vb) {
 
 // keys per tile of the bucket path's segmented passes
 inline uint64_t seg_tile_keys(int kb, int vb) {
-  return (THRS_SEG_PIPE && kb == 4 && vb == 0) ? PipeGeom::TILE : tile_keys(kb, vb);
+  return tile_keys(kb, vb);
 }
 
 struct Plan {
@@ -125,13 +118,19 @@ constexpr uint64_t kBigBOff = kSegBaseAOff + kSegs * 256 * 4;
 constexpr uint64_t kBigPosOff = kBigBOff + round_up_c((kBuckets + 1) * 4, 256);
 constexpr uint64_t kBigTileOff = kBigPosOff + round_up_c((kBuckets + 1) * 4, 256);
 constexpr uint64_t kZeroLogOff = kBigTileOff + round_up_c((kBuckets + 1) * 4, 256);  // f32: +-0 keys (thrs_hist_joint)
-constexpr uint64_t kHybridBytes = kZeroLogOff + round_up_c(kZeroLogCap * 4, 256);
+// reserved runs (thrs_options.offsets RESERVE): per top-digit pass, one
+// cursor line per (segment, digit), set to the segment bases by thrs_plan_rows
+constexpr uint64_t kCursorAOff = kZeroLogOff + round_up_c(kZeroLogCap * 4, 256);  // second-digit pass: [8][256]
+constexpr uint64_t kCursorBOff = kCursorAOff + (uint64_t)kSegs * 256 * kCursorStrideA * 4;  // top-digit: [256][256]
+constexpr uint64_t kRegTileOff = kCursorBOff + (uint64_t)256 * 256 * kCursorStrideB * 4;   // u32 [257]
+constexpr uint64_t kHybridBytes = kRegTileOff + round_up_c(257 * 4, 256);
 // the smallest local-sort capacity (LocSmall): a big chunk holds more keys
 constexpr uint64_t kMinLocalCap = LocSmall::CAP;
 // tile ids of the segmented pass: each of the 8 segments adds at most two
 // partial tiles (its first and last: seg_tiles) and rounds its id range up
 // to a multiple of kGroup
-constexpr uint64_t kSegTilePad = kSegs * (kGroup + 1);
+// (+ 256: the reserved top-digit pass tiles every second-digit region on its own)
+constexpr uint64_t kSegTilePad = kSegs * (kGroup + 1) + 256;
 
 inline Plan make_plan(int keyType, int valueBytesOrZero, uint32_t n) {
   Plan p{};
@@ -193,6 +192,9 @@ struct ProfScope {
   }
 };
 extern uint64_t* g_stamps;   // THRS_STAMPS diagnostic builds only (thrs_debug_set_stamps)
+// fault injection (THRS_FAULT_INJECT builds only, thrs_debug_inject; else 0):
+// bit 0 = the plan's first big-chunk entry is made stale
+extern int g_inject;
 extern uint64_t* g_lstamps;  // same, local sort: [chunk][8] (thrs_debug_set_local_stamps)
 // 1 = lane-ordered LDS atomics on this device (fast rank), 0 = ballot match
 int probe_rank_mode(hipStream_t stream);
@@ -223,7 +225,8 @@ hipError_t allow_lds(F kernel, size_t bytes) {
 // The path one sort takes (host decision, no device work): run_sort and
 // thrs_path_info (thrs_capi.hip) share it.
 struct PathSel {
-  bool bucket, fullWindow, smallLocal, local16, wide16, small16, count16, local32, segTop, segA, planes, ranged, useXb;
+  bool bucket, fullWindow, smallLocal, local16, wide16, small16, count16, local32, segTop, segA, planes, reserve, ranged,
+      useXb, reserveB;
   int nLow;
   uint32_t cap;
 };
@@ -263,7 +266,9 @@ PathSel select_path(uint32_t n, int startBits, int nPass, const thrs_options& op
   const bool rangedReq = opt.keyRange == 1 && fullWindow && !counts;
   // lower bounds by measurement (docs/EXPERIMENTS.md row 87): 4-byte keys
   // alone from 150M keys, with 4-byte values from 100M, the rest from 2^28
-  const uint64_t minN = rangedReq ? (1ull << 27)
+  // (the 2^27 bound of a ranged finish is measured for 4-byte keys without
+  // values, the C2 finish; other key / value types keep their own bounds)
+  const uint64_t minN = (rangedReq && kKeys4) ? (1ull << 27)
                         : kKeys4  ? kBucketMinKeys4
                         : (KB == 4 && VB == 4) ? kBucketMinPairs4
                                                : (1ull << 28);
@@ -338,6 +343,12 @@ PathSel select_path(uint32_t n, int startBits, int nPass, const thrs_options& op
   P.planes = planes;
   P.ranged = ranged;
   P.useXb = useXb;
+  // the image-plane passes (keys only) place their runs by reservation
+  // instead of the look-back chain when asked (measured no faster: the
+  // reservation's device-scope atomics take ~6 us to return under the pass's
+  // own HBM load, longer than the walk they replace; docs/EXPERIMENTS.md)
+  P.reserve = planes && (opt.offsets == THRS_OFFSETS_RESERVE || opt.offsets == THRS_OFFSETS_RESERVE_FIRST);
+  P.reserveB = P.reserve && opt.offsets != THRS_OFFSETS_RESERVE_FIRST;
   P.nLow = nLow;
   P.cap = cap;
   return P;
@@ -383,7 +394,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   const PathSel P = select_path<KT, VB>(n, startBits, nPass, opt, plan, counts != nullptr);
   const bool bucket = P.bucket, smallLocal = P.smallLocal, local16 = P.local16, wide16 = P.wide16;
   const bool small16 = P.small16, count16 = P.count16, local32 = P.local32, segTop = P.segTop, segA = P.segA;
-  const bool planes = P.planes, ranged = P.ranged, useXb = P.useXb;
+  const bool planes = P.planes, ranged = P.ranged, useXb = P.useXb, reserve = P.reserve;
   const int nLow = P.nLow;
   const uint32_t cap = P.cap;
   // the device-chosen squeeze (float keys over the whole key, single-bucket
@@ -430,32 +441,13 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                             : thrs_pass_seg<KT, VB, ST, false, kPlanes4 ? kCodecSplit : kCodecKeys>;
   auto skPlanes = atomicRank ? thrs_pass_seg<kPlaneKT, VB, ST, true, kPlanes4 ? kCodecPlanes : kCodecKeys>
                              : thrs_pass_seg<kPlaneKT, VB, ST, false, kPlanes4 ? kCodecPlanes : kCodecKeys>;
-  // THRS_SEG_MERGE: the plane codecs and their whole-key alternative (mode 1)
-  // in one launch each (thrs_pass_seg ALT)
-  // THRS_SEG_PIPE: the pipelined segmented pass (u32 / f32 keys without values)
-  constexpr bool kPipe = THRS_SEG_PIPE && (KT == 0 || KT == 2) && VB == 0;
-  // (instantiated only in THRS_SEG_PIPE builds, u32 / f32 keys-only)
-  auto pipe_kernel = [&](int codec) {
-    if constexpr (kPipe) {
-      if (codec == kCodecSplit) return atomicRank ? thrs_pass_seg_pipe<KT, ST, true, kCodecSplit>
-                                                  : thrs_pass_seg_pipe<KT, ST, false, kCodecSplit>;
-      if (codec == kCodecPlanes) return atomicRank ? thrs_pass_seg_pipe<0, ST, true, kCodecPlanes>
-                                                   : thrs_pass_seg_pipe<0, ST, false, kCodecPlanes>;
-      return atomicRank ? thrs_pass_seg_pipe<KT, ST, true, kCodecKeys> : thrs_pass_seg_pipe<KT, ST, false, kCodecKeys>;
-    } else {
-      (void)codec;
-      return nullptr;
-    }
-  };
+  // ... with reserved runs (keys only: with values these are the kernels
+  // above, never launched reserved)
+  auto skSplitR = atomicRank ? thrs_pass_seg<KT, VB, ST, true, kPlanes4 ? kCodecSplit : kCodecKeys, VB == 0>
+                             : thrs_pass_seg<KT, VB, ST, false, kPlanes4 ? kCodecSplit : kCodecKeys, VB == 0>;
+  auto skPlanesR = atomicRank ? thrs_pass_seg<kPlaneKT, VB, ST, true, kPlanes4 ? kCodecPlanes : kCodecKeys, VB == 0>
+                              : thrs_pass_seg<kPlaneKT, VB, ST, false, kPlanes4 ? kCodecPlanes : kCodecKeys, VB == 0>;
   const uint32_t segTileKeys = (uint32_t)seg_tile_keys(KB, VB);
-  // (other key / value types: the plain keys kernel, never launched merged)
-  constexpr bool kMerge = THRS_SEG_MERGE && KT == 0 && VB == 0;  // (u32 only)
-  constexpr int kAltM = kMerge ? kCodecKeys : -1;
-  auto skSplitM = atomicRank ? thrs_pass_seg<KT, VB, ST, true, (KT == 0 && VB == 0) ? kCodecSplit : kCodecKeys, kAltM>
-                             : thrs_pass_seg<KT, VB, ST, false, (KT == 0 && VB == 0) ? kCodecSplit : kCodecKeys, kAltM>;
-  auto skPlanesM = atomicRank
-                       ? thrs_pass_seg<KT, VB, ST, true, (KT == 0 && VB == 0) ? kCodecPlanes : kCodecKeys, kAltM>
-                       : thrs_pass_seg<KT, VB, ST, false, (KT == 0 && VB == 0) ? kCodecPlanes : kCodecKeys, kAltM>;
   const int histPasses = nPass;
   const size_t histLds = (size_t)histPasses * kBins * hist_copies<(int)sizeof(U)>() * 4;
   if (allow_lds(thrs_hist<KT>, histLds) != hipSuccess || allow_lds(kernel, lds) != hipSuccess ||
@@ -466,14 +458,8 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
         (squeeze && allow_lds(thrs_hist_joint<KT, true>, kJointLds) != hipSuccess))
       return THRS_ERROR_HIP;
     if (planes && (allow_lds(skSplit, lds) != hipSuccess || allow_lds(skPlanes, lds) != hipSuccess ||
-                   allow_lds(skSplitM, lds) != hipSuccess || allow_lds(skPlanesM, lds) != hipSuccess))
+                   allow_lds(skSplitR, lds) != hipSuccess || allow_lds(skPlanesR, lds) != hipSuccess))
       return THRS_ERROR_HIP;
-    if constexpr (kPipe) {
-      if (allow_lds(pipe_kernel(kCodecKeys), PipeGeom::LDS_BYTES) != hipSuccess ||
-          allow_lds(pipe_kernel(kCodecSplit), PipeGeom::LDS_BYTES) != hipSuccess ||
-          allow_lds(pipe_kernel(kCodecPlanes), PipeGeom::LDS_BYTES) != hipSuccess)
-        return THRS_ERROR_HIP;
-    }
     if constexpr (kKV) {
       if (allow_lds(atomicRank ? thrs_local_kv<KT, VB, true> : thrs_local_kv<KT, VB, false>, LocKV::LDS) != hipSuccess)
         return THRS_ERROR_HIP;
@@ -552,6 +538,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
         z.words[2] = (uint64_t)nPass * plan.claimBytes / 16;
       }
     }
+    ProfScope prof(stream, 0, THRS_PK_ZERO, 16 * (z.words[0] + z.words[1] + z.words[2]));
     hipLaunchKernelGGL(thrs_zero_ranges, dim3(std::min<uint32_t>(2048, 8 * cu_count())), dim3(256), 0, stream, z);
   }
   char* claim = scratch + kHeaderBytes + 2 * plan.setBytes;  // 8 per-pass claim areas
@@ -562,9 +549,11 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     const uint64_t want = ((uint64_t)n + kHistThreads * 64 - 1) / (kHistThreads * 64);
     const int hgrid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cu_count() * THRS_HIST_GRID_MULT));
     if (bucket) {
-      if (squeeze)  // the sample's guess at the squeeze, for the first histogram
+      if (squeeze) {  // the sample's guess at the squeeze, for the first histogram
+        ProfScope prof(stream, 0, THRS_PK_SQUEEZE_SAMPLE, (uint64_t)kSqSample * sizeof(U));
         hipLaunchKernelGGL(thrs_squeeze_sample<KT>, dim3(kSqBlocks), dim3(kSqSampleThreads), 0, stream,
                            static_cast<const U*>(keys), n, km, cap, sample, meta);
+      }
       {
         ProfScope prof(stream, 0, THRS_PK_HIST_JOINT, keyBytes);
         hipLaunchKernelGGL(thrs_hist_joint<KT>, dim3(hgrid), dim3(kHistThreads), kJointLds, stream,
@@ -586,7 +575,10 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                            reinterpret_cast<uint32_t*>(hyb + kBigBOff), sqMode, 8 * KB,
                            reinterpret_cast<uint32_t*>(hyb + kBigPosOff), reinterpret_cast<uint32_t*>(hyb + kBigTileOff),
                            reinterpret_cast<uint4*>(scratch + plan.bigHistOff), nLow,
-                           sqMode == 1 ? static_cast<const SqueezeWords*>(sample) : nullptr, planes ? 1 : 0);
+                           sqMode == 1 ? static_cast<const SqueezeWords*>(sample) : nullptr, planes ? 1 : 0,
+                           reserve ? reinterpret_cast<uint32_t*>(hyb + kCursorAOff) : nullptr,
+                           reserve ? reinterpret_cast<uint32_t*>(hyb + kCursorBOff) : nullptr,
+                           reserve ? reinterpret_cast<uint32_t*>(hyb + kRegTileOff) : nullptr, err, g_inject);
       };
       if (!local32 && squeeze) {
         plan_rows(1, 0, kSegHistAOff, kRowHistOff);
@@ -677,17 +669,12 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     // every key: both top digits constant) neither -- both are identities,
     // and skipping both keeps the keys in K.
     auto launch_seg = [&](int p, U* kin, U* kout, VW* vin, VW* vout, uint64_t infoOff, uint64_t baseOff,
-                          const uint32_t* gate, uint32_t gateMask, int codec = kCodecKeys) {
+                          const uint32_t* gate, uint32_t gateMask, int codec = kCodecKeys, uint64_t curOff = 0) {
       ProfScope prof(stream, 1, THRS_PK_PASS_SEG, moveBytes);
-      if constexpr (kPipe) {
-        auto pk = pipe_kernel(codec);
-        hipLaunchKernelGGL(pk, dim3((uint32_t)cu_count()), dim3(PipeGeom::THREADS), PipeGeom::LDS_BYTES, stream,
-                           kin, kout, codec == kCodecPlanes ? kid : km, codec == kCodecPlanes ? 16 : startBits + 8 * p,
-                           reinterpret_cast<uint32_t*>(hyb + infoOff), reinterpret_cast<const uint32_t*>(hyb + baseOff),
-                           status[p & 1], err, grp[p & 1], gate, gateMask, hiP, sqw);
-        return;
-      }
-      auto kern = codec == kCodecSplit ? skSplit : codec == kCodecPlanes ? skPlanes : sk;
+      // curOff != 0: the keys-only plane codecs with reserved runs
+      auto kern = codec == kCodecSplit ? (curOff ? skSplitR : skSplit)
+                  : codec == kCodecPlanes ? (curOff ? skPlanesR : skPlanes)
+                                          : sk;
       // kCodecPlanes: image-space input (identity map), digit at bits 16-23 of k'
       hipLaunchKernelGGL(kern, dim3((uint32_t)segPerCU * cu_count()), dim3(G::THREADS), lds, stream, kin, kout, vin,
                          vout, codec == kCodecPlanes ? kid : km, codec == kCodecPlanes ? 16 : startBits + 8 * p,
@@ -695,36 +682,17 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                          status[p & 1], err, grp[p & 1], gate, gateMask, hiP,
                          g_stamps ? g_stamps + (uint64_t)(p - nLow) * (plan.nTiles + kSegTilePad) * kStampSlots
                                   : nullptr,
-                         sqw, static_cast<const U*>(nullptr), static_cast<U*>(nullptr), km, 0);
+                         sqw, curOff ? reinterpret_cast<uint32_t*>(hyb + curOff) : nullptr,
+                         reinterpret_cast<const uint32_t*>(hyb + kRegTileOff), base + nLow * kBins);
     };
     const uint64_t sw = plan.wideStatus ? 8 : 4;
     const int setB = (nLow + 1) & 1;
-    // one launch per top pass for both plan modes (the plane codecs in mode
-    // 0, whole keys in mode 1)
-    auto launch_seg_merged = [&](int p, bool second) {
-      ProfScope prof(stream, 1, THRS_PK_PASS_SEG, moveBytes);
-      const U* kin = second ? reinterpret_cast<const U*>(loP) : K;
-      U* kout = second ? reinterpret_cast<U*>(lo2P) : reinterpret_cast<U*>(loP);
-      const U* kin2 = second ? keyOut : K;
-      U* kout2 = second ? K : keyOut;
-      hipLaunchKernelGGL(second ? skPlanesM : skSplitM, dim3((uint32_t)segPerCU * cu_count()), dim3(G::THREADS), lds,
-                         stream, kin, kout, second ? valOut : V, second ? V : valOut, second ? kid : km,
-                         second ? 16 : startBits + 8 * p,
-                         reinterpret_cast<uint32_t*>(hyb + (second ? kSegInfoOff : kSegInfoAOff)),
-                         reinterpret_cast<const uint32_t*>(hyb + (second ? kSegBaseOff : kSegBaseAOff)), status[p & 1],
-                         err, grp[p & 1], mode, kGateMode0, hiP,
-                         g_stamps ? g_stamps + (uint64_t)(p - nLow) * (plan.nTiles + kSegTilePad) * kStampSlots
-                                  : nullptr,
-                         sqw, kin2, kout2, km, startBits + 8 * p);
-    };
     if (segA) {
       // Both table sets are clean (zeroed up front); the segmented passes'
       // extra tile ids (rows past nTiles) are touched by nothing else.
-      if (planes && kMerge) {
-        launch_seg_merged(nLow, false);
-      } else if (planes) {
+      if (planes) {
         launch_seg(nLow, K, reinterpret_cast<U*>(loP), V, valOut, kSegInfoAOff, kSegBaseAOff, mode, kGateMode0,
-                   kCodecSplit);
+                   kCodecSplit, reserve ? kCursorAOff : 0);
         launch_seg(nLow, K, keyOut, V, valOut, kSegInfoAOff, kSegBaseAOff, mode, kGateMode1 | kGateMode3);
       } else {
         launch_seg(nLow, K, keyOut, V, valOut, kSegInfoAOff, kSegBaseAOff, mode, kGateMode0 | kGateMode1 | kGateMode3);
@@ -742,11 +710,9 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                          stream) != hipSuccess)
         return THRS_ERROR_HIP;
     }
-    if (planes && kMerge) {
-      launch_seg_merged(nLow + 1, true);
-    } else if (planes) {  // mode 0: planes -> lo2; mode 1 (big chunks) / 3 (f32 -0): keys
+    if (planes) {  // mode 0: planes -> lo2; mode 1 (big chunks) / 3 (f32 -0): keys
       launch_seg(nLow + 1, reinterpret_cast<U*>(loP), reinterpret_cast<U*>(lo2P), valOut, V, kSegInfoOff, kSegBaseOff,
-                 mode, kGateMode0, kCodecPlanes);
+                 mode, kGateMode0, kCodecPlanes, P.reserveB ? kCursorBOff : 0);
       launch_seg(nLow + 1, keyOut, K, valOut, V, kSegInfoOff, kSegBaseOff, mode, kGateMode1 | kGateMode3);
     } else if (segTop)
       launch_seg(nLow + 1, keyOut, K, valOut, V, kSegInfoOff, kSegBaseOff, mode, kGateMode0 | kGateMode1 | kGateMode3);

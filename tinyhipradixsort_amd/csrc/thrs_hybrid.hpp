@@ -182,10 +182,7 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
   __syncthreads();
   with_map<KT>(kmh, sq, [&](auto km) __attribute__((always_inline)) {
   // (a squeezed first histogram: does every key carry its half's dropped bit?)
-#ifndef THRS_HJ_NOCHECK
-#define THRS_HJ_NOCHECK 0  // EXPERIMENT only (the check's cost): a wrong guess then goes unnoticed
-#endif
-  constexpr bool kCheck = !SECOND && !std::is_same<decltype(km), KeyMap<U>>::value && !THRS_HJ_NOCHECK;
+  constexpr bool kCheck = !SECOND && !std::is_same<decltype(km), KeyMap<U>>::value;
   U viol = 0;
   const uint64_t len = hj_len(n, gridDim.x);
   const uint64_t lo = min((uint64_t)n, (uint64_t)blockIdx.x * len), hi = min((uint64_t)n, lo + len);
@@ -588,18 +585,40 @@ __device__ __forceinline__ void plan_squeeze(uint32_t* __restrict__ meta, int ke
 // The per-bucket fallback's plan (thrs_fallback.hpp), by the plan's last
 // workgroup (256 threads): prefixes of the big chunks' sizes (bigPos: their
 // positions in the concatenation of the big chunks) and tile counts (bigTile).
-__device__ __forceinline__ void plan_big_prefix(const uint32_t* __restrict__ joint, const uint32_t* __restrict__ meta,
-                                                const uint32_t* __restrict__ bigB, uint32_t* __restrict__ bigPos,
-                                                uint32_t* __restrict__ bigTile, uint32_t tileKeys, uint32_t (*s_w)[4]) {
+// Every listed entry is checked first: a bucket id past the histogram, or a
+// bucket that is not above the capacity, can only come from a plan-ordering
+// bug; it must never address past a table (the fallback indexes chunkOff by
+// these ids), so the fallback is switched off (no big chunk listed) and the
+// sort reports THRS_ERROR_DEVICE_CHECK through its error word.
+// (inject: fault-injection builds only -- a stale first entry, see
+// thrs_debug_inject)
+__device__ __forceinline__ void plan_big_prefix(const uint32_t* __restrict__ joint, uint32_t* __restrict__ meta,
+                                                uint32_t* __restrict__ bigB, uint32_t* __restrict__ bigPos,
+                                                uint32_t* __restrict__ bigTile, uint32_t tileKeys, uint32_t cap,
+                                                uint32_t (*s_w)[4], uint32_t* __restrict__ errFlag, int inject) {
   const uint32_t M = load_agent(&meta[kMetaBigCount]);
   if (M == 0) return;
   const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+  if (inject && t == 0) bigB[0] = 0xFFFFFFF0u;
+  __syncthreads();
   const uint32_t per = (M + kPlanRowThreads - 1) / kPlanRowThreads;
   const uint32_t i0 = min(M, t * per), i1 = min(M, i0 + per);
+  bool bad = false;
+  for (uint32_t i = i0; i < i1; ++i) {
+    const uint32_t b = bigB[i];
+    bad = bad || b >= kBuckets || joint[b] <= cap;
+  }
+  if (__syncthreads_or(bad)) {
+    if (t == 0) {
+      atomicOr(errFlag, kErrRunClamped);
+      meta[kMetaBigCount] = 0;
+      meta[kMetaFallback] = 0;
+    }
+    return;
+  }
   auto tiles_of = [&](uint32_t sz) { return (sz + tileKeys - 1) / tileKeys; };
   uint32_t ks = 0, ts = 0;
-  // (bucket ids clamped: a stale entry must never address past the histogram)
-  auto size_of = [&](uint32_t i) { return joint[min(bigB[i], kBuckets - 1)]; };
+  auto size_of = [&](uint32_t i) { return joint[bigB[i]]; };
   for (uint32_t i = i0; i < i1; ++i) {
     const uint32_t sz = size_of(i);
     ks += sz;
@@ -642,7 +661,8 @@ __global__ __launch_bounds__(kPlanRowThreads) void thrs_plan_rows(
     uint32_t* __restrict__ segInfo, uint32_t* __restrict__ segBase, uint32_t tileKeys, uint32_t histGrid,
     uint32_t* __restrict__ segInfoA, uint32_t* __restrict__ segBaseA, uint32_t* __restrict__ bigB, int sqMode,
     int keyBits, uint32_t* __restrict__ bigPos, uint32_t* __restrict__ bigTile, uint4* __restrict__ bigHist,
-    int nLow, const SqueezeWords* __restrict__ sample, int planes) {
+    int nLow, const SqueezeWords* __restrict__ sample, int planes, uint32_t* __restrict__ curA,
+    uint32_t* __restrict__ curB, uint32_t* __restrict__ regTiles, uint32_t* __restrict__ errFlag, int inject) {
   if (sqMode == 2 && meta[kMetaRehist] == 0) return;
   __shared__ uint32_t s_w[2][4], s_base, s_b2[kBins], s_sq[3], s_last;
   const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6, r = blockIdx.x;
@@ -671,6 +691,9 @@ __global__ __launch_bounds__(kPlanRowThreads) void thrs_plan_rows(
   chunkOff[kBins * r + t] = base + pre;
   chunkB0[kBins * r + t] = kBins * r + t;
   if ((t & 31u) == 0) segBase[(t >> 5) * kBins + r] = base + pre;  // segment s = columns [32s, 32s+32)
+  // reserved runs (thrs_pass_seg RES): the top-digit pass's cursor of bucket
+  // (r, t) starts at the bucket (a tile's 256 cursors lie on 256 lines)
+  if (curB) curB[(kBins * r + t) * kCursorStrideB] = base + pre;
   if (t == 0) baseTop[kBins + r] = base;
   if (x > cap) {  // a bucket above the chunk capacity: a big chunk; all n keys in one bucket: mode 2
     atomicOr(&meta[kMetaFallback], 1u);
@@ -714,7 +737,7 @@ __global__ __launch_bounds__(kPlanRowThreads) void thrs_plan_rows(
     if (sqMode == 1 && t == 0) plan_squeeze(meta, keyBits, sample);
     __syncthreads();
     if (!(sqMode == 1 && load_agent(&meta[kMetaRehist]) != 0u)) {
-      plan_big_prefix(joint, meta, bigB, bigPos, bigTile, tileKeys, s_w);
+      plan_big_prefix(joint, meta, bigB, bigPos, bigTile, tileKeys, cap, s_w, errFlag, inject);
       // f32 with a -0 key: whole keys through the top-digit passes (mode 3)
       // (more zeros than the zero log holds: thrs_local16 could not restore
       // the -0 signs from the planes)
@@ -737,9 +760,18 @@ __global__ __launch_bounds__(kPlanRowThreads) void thrs_plan_rows(
 #pragma unroll
   for (int sg = 0; sg < kSegs; ++sg) {
     segBaseA[sg * kBins + t] = sa;
+    if (curA) curA[(sg * kBins + t) * kCursorStrideA] = sa;
     sa += segHistA[sg * kBins + t];
   }
   __syncthreads();
+  if (regTiles) {  // reserved top-digit pass: every second-digit region tiled on its own
+    const uint32_t size = (t + 1 < kBins ? s_b2[t + 1] : n) - s_b2[t];
+    const uint32_t nt = (uint32_t)(((uint64_t)size + tileKeys - 1) / tileKeys);
+    uint32_t total = 0;
+    const uint32_t first = scan256(nt, 1, &total);
+    regTiles[t] = first;
+    if (t == 0) regTiles[kBins] = total;
+  }
   // segment positions, first tile ids (multiples of kGroup), tickets: thread 0
   // for the top-digit pass (second-digit ranges), thread 64 for the
   // second-digit pass (position ranges) -- as thrs_plan
