@@ -69,7 +69,6 @@ enum { THRS_CLAIMS_AUTO = 0, THRS_CLAIMS_XCD_BLOCKS = 1, THRS_CLAIMS_TICKET = 2 
 enum { THRS_RANK_AUTO = 0, THRS_RANK_ATOMIC = 1, THRS_RANK_BALLOT = 2 };
 enum { THRS_PLANES_AUTO = 0, THRS_PLANES_ON = 1, THRS_PLANES_OFF = 2 };
 enum { THRS_SQUEEZE_AUTO = 0, THRS_SQUEEZE_OFF = 1 };
-enum { THRS_OFFSETS_AUTO = 0, THRS_OFFSETS_LOOKBACK = 1, THRS_OFFSETS_RESERVE = 2, THRS_OFFSETS_RESERVE_FIRST = 3 };
 typedef struct thrs_options {
   int32_t path;          /* THRS_PATH_*: LSD = one device pass per digit; BUCKET = the
                             3-HBM-pass path wherever the key/value types and window
@@ -112,15 +111,6 @@ typedef struct thrs_options {
                             reference's float generator clears one, unittest.cpp:103,
                             108); AUTO = when the buckets would overflow, OFF = never.
                             Same bytes either way.                                   */
-  int32_t offsets;       /* THRS_OFFSETS_*: how a keys-only top-digit pass of the
-                            bucket path places a tile's digit runs: LOOKBACK = the
-                            decoupled look-back chain (stable); RESERVE = one
-                            atomic reservation per digit on its segment's cursor
-                            (no chain; equal keys of a keys-only sort are
-                            identical, so the output bytes are the same);
-                            RESERVE_FIRST = only the first of the two passes.
-                            AUTO = LOOKBACK (measured faster).                 */
-  int32_t pad0;          /* must be 0 */
   uint64_t rangeLo;
   uint64_t rangeHi;
 } thrs_options;

@@ -30,7 +30,7 @@ from tinyhipradixsort_amd import testutil as TU  # noqa: E402
 from sweep import load  # noqa: E402
 
 NAMES = ["claim+issue", "load+count", "scan", "rank+stage", "lookback", "writeout"]
-SEG_PAD = 8 * 17 + 256  # kSegTilePad
+SEG_PAD = 8 * 17  # kSegTilePad
 
 
 def q(x):

@@ -76,15 +76,14 @@ def test_temporary_buffer_layout(kt, vt, n):
     assert d.getOutputValueBuffer(1000) == 1000 + d.pSumBuffer + d.keyOutBuffer
     # scratch (look-back status words) stays a modest fraction of the payload
     # (the reference's pSum region is 4*256*ceil(n/2048) = n/2 bytes, hpp:839),
-    # plus a fixed ~3 MiB: the 3-pass path's bucket histogram and chunk table,
-    # the segmented pass's extra look-back rows and the two passes' reservation
-    # cursors (8 x 256 lines of 128 B + 65536 x 16 B); u32 / f32 keys: + the
+    # plus a fixed ~1.1 MiB: the 3-pass path's bucket histogram and chunk table
+    # and the segmented pass's extra look-back rows; u32 / f32 keys: + the
     # bucket path's u8 plane (n bytes: its two u16 planes fill keyOut),
     # reserved only where the default takes that path (n in [150M, 2^31 + 2^25])
     plane = -(-n // 256) * 256 if kt in (T.KeyType.U32, T.KeyType.F32) and 150000000 <= n <= (1 << 31) + (1 << 25) \
         else 0
     if n >= (1 << 20):
-        assert d.pSumBuffer < 0.3 * d.keyOutBuffer + plane + (7 << 20) // 2
+        assert d.pSumBuffer < 0.3 * d.keyOutBuffer + plane + (3 << 20) // 2
 
 
 def test_argument_validation_needs_no_device():

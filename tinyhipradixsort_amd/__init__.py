@@ -130,8 +130,8 @@ class _CConfig(ctypes.Structure):
 class _COptions(ctypes.Structure):
     _fields_ = [("path", ctypes.c_int32), ("localGeometry", ctypes.c_int32), ("segmented", ctypes.c_int32),
                 ("tileClaims", ctypes.c_int32), ("rank", ctypes.c_int32), ("planes", ctypes.c_int32),
-                ("keyRange", ctypes.c_int32), ("squeeze", ctypes.c_int32), ("offsets", ctypes.c_int32),
-                ("pad0", ctypes.c_int32), ("rangeLo", ctypes.c_uint64), ("rangeHi", ctypes.c_uint64)]
+                ("keyRange", ctypes.c_int32), ("squeeze", ctypes.c_int32), ("rangeLo", ctypes.c_uint64),
+                ("rangeHi", ctypes.c_uint64)]
 
 
 @dataclass
@@ -146,15 +146,13 @@ class Options:
     rank: str = "auto"            # auto | atomic | ballot
     planes: str = "auto"          # auto | on | off
     squeeze: str = "auto"         # auto | off (float keys: data-chosen bucket bits)
-    offsets: str = "auto"         # auto | lookback | reserve | reserve_first (keys-only top-digit passes)
     # key range promise (thrs_options.keyRange): every key's image
     # getKeyBits(k) ^ (descending ? ~0 : 0) lies in [rangeLo, rangeHi]; None = no promise
     keyRange: "tuple[int, int] | None" = None
 
     _ENUMS = {"path": ("auto", "lsd", "bucket"), "localGeometry": ("auto", "big", "small", "big32", "count16", "rank16", "wide16"),
               "segmented": ("auto", "top_only", "none"), "tileClaims": ("auto", "xcd_blocks", "ticket"),
-              "rank": ("auto", "atomic", "ballot"), "planes": ("auto", "on", "off"), "squeeze": ("auto", "off"),
-              "offsets": ("auto", "lookback", "reserve", "reserve_first")}
+              "rank": ("auto", "atomic", "ballot"), "planes": ("auto", "on", "off"), "squeeze": ("auto", "off")}
 
     def _c(self) -> "_COptions":
         o = _COptions()

@@ -166,8 +166,7 @@ bool valid_options(const thrs_options& o) {
          o.localGeometry <= THRS_LOCAL_WIDE16 && o.segmented >= THRS_SEG_AUTO && o.segmented <= THRS_SEG_NONE &&
          o.tileClaims >= THRS_CLAIMS_AUTO && o.tileClaims <= THRS_CLAIMS_TICKET && o.rank >= THRS_RANK_AUTO &&
          o.rank <= THRS_RANK_BALLOT && o.planes >= THRS_PLANES_AUTO && o.planes <= THRS_PLANES_OFF &&
-         (o.squeeze == THRS_SQUEEZE_AUTO || o.squeeze == THRS_SQUEEZE_OFF) && o.offsets >= THRS_OFFSETS_AUTO &&
-         o.offsets <= THRS_OFFSETS_RESERVE_FIRST && o.pad0 == 0 &&
+         (o.squeeze == THRS_SQUEEZE_AUTO || o.squeeze == THRS_SQUEEZE_OFF) &&
          (o.keyRange == 0 || (o.keyRange == 1 && o.rangeLo <= o.rangeHi));
 }
 

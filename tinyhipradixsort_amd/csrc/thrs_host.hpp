@@ -118,19 +118,13 @@ constexpr uint64_t kBigBOff = kSegBaseAOff + kSegs * 256 * 4;
 constexpr uint64_t kBigPosOff = kBigBOff + round_up_c((kBuckets + 1) * 4, 256);
 constexpr uint64_t kBigTileOff = kBigPosOff + round_up_c((kBuckets + 1) * 4, 256);
 constexpr uint64_t kZeroLogOff = kBigTileOff + round_up_c((kBuckets + 1) * 4, 256);  // f32: +-0 keys (thrs_hist_joint)
-// reserved runs (thrs_options.offsets RESERVE): per top-digit pass, one
-// cursor line per (segment, digit), set to the segment bases by thrs_plan_rows
-constexpr uint64_t kCursorAOff = kZeroLogOff + round_up_c(kZeroLogCap * 4, 256);  // second-digit pass: [8][256]
-constexpr uint64_t kCursorBOff = kCursorAOff + (uint64_t)kSegs * 256 * kCursorStrideA * 4;  // top-digit: [256][256]
-constexpr uint64_t kRegTileOff = kCursorBOff + (uint64_t)256 * 256 * kCursorStrideB * 4;   // u32 [257]
-constexpr uint64_t kHybridBytes = kRegTileOff + round_up_c(257 * 4, 256);
+constexpr uint64_t kHybridBytes = kZeroLogOff + round_up_c(kZeroLogCap * 4, 256);
 // the smallest local-sort capacity (LocSmall): a big chunk holds more keys
 constexpr uint64_t kMinLocalCap = LocSmall::CAP;
 // tile ids of the segmented pass: each of the 8 segments adds at most two
 // partial tiles (its first and last: seg_tiles) and rounds its id range up
 // to a multiple of kGroup
-// (+ 256: the reserved top-digit pass tiles every second-digit region on its own)
-constexpr uint64_t kSegTilePad = kSegs * (kGroup + 1) + 256;
+constexpr uint64_t kSegTilePad = kSegs * (kGroup + 1);
 
 inline Plan make_plan(int keyType, int valueBytesOrZero, uint32_t n) {
   Plan p{};
@@ -225,8 +219,7 @@ hipError_t allow_lds(F kernel, size_t bytes) {
 // The path one sort takes (host decision, no device work): run_sort and
 // thrs_path_info (thrs_capi.hip) share it.
 struct PathSel {
-  bool bucket, fullWindow, smallLocal, local16, wide16, small16, count16, local32, segTop, segA, planes, reserve, ranged,
-      useXb, reserveB;
+  bool bucket, fullWindow, smallLocal, local16, wide16, small16, count16, local32, segTop, segA, planes, ranged, useXb;
   int nLow;
   uint32_t cap;
 };
@@ -343,12 +336,6 @@ PathSel select_path(uint32_t n, int startBits, int nPass, const thrs_options& op
   P.planes = planes;
   P.ranged = ranged;
   P.useXb = useXb;
-  // the image-plane passes (keys only) place their runs by reservation
-  // instead of the look-back chain when asked (measured no faster: the
-  // reservation's device-scope atomics take ~6 us to return under the pass's
-  // own HBM load, longer than the walk they replace; docs/EXPERIMENTS.md)
-  P.reserve = planes && (opt.offsets == THRS_OFFSETS_RESERVE || opt.offsets == THRS_OFFSETS_RESERVE_FIRST);
-  P.reserveB = P.reserve && opt.offsets != THRS_OFFSETS_RESERVE_FIRST;
   P.nLow = nLow;
   P.cap = cap;
   return P;
@@ -394,7 +381,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   const PathSel P = select_path<KT, VB>(n, startBits, nPass, opt, plan, counts != nullptr);
   const bool bucket = P.bucket, smallLocal = P.smallLocal, local16 = P.local16, wide16 = P.wide16;
   const bool small16 = P.small16, count16 = P.count16, local32 = P.local32, segTop = P.segTop, segA = P.segA;
-  const bool planes = P.planes, ranged = P.ranged, useXb = P.useXb, reserve = P.reserve;
+  const bool planes = P.planes, ranged = P.ranged, useXb = P.useXb;
   const int nLow = P.nLow;
   const uint32_t cap = P.cap;
   // the device-chosen squeeze (float keys over the whole key, single-bucket
@@ -441,12 +428,6 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                             : thrs_pass_seg<KT, VB, ST, false, kPlanes4 ? kCodecSplit : kCodecKeys>;
   auto skPlanes = atomicRank ? thrs_pass_seg<kPlaneKT, VB, ST, true, kPlanes4 ? kCodecPlanes : kCodecKeys>
                              : thrs_pass_seg<kPlaneKT, VB, ST, false, kPlanes4 ? kCodecPlanes : kCodecKeys>;
-  // ... with reserved runs (keys only: with values these are the kernels
-  // above, never launched reserved)
-  auto skSplitR = atomicRank ? thrs_pass_seg<KT, VB, ST, true, kPlanes4 ? kCodecSplit : kCodecKeys, VB == 0>
-                             : thrs_pass_seg<KT, VB, ST, false, kPlanes4 ? kCodecSplit : kCodecKeys, VB == 0>;
-  auto skPlanesR = atomicRank ? thrs_pass_seg<kPlaneKT, VB, ST, true, kPlanes4 ? kCodecPlanes : kCodecKeys, VB == 0>
-                              : thrs_pass_seg<kPlaneKT, VB, ST, false, kPlanes4 ? kCodecPlanes : kCodecKeys, VB == 0>;
   const uint32_t segTileKeys = (uint32_t)seg_tile_keys(KB, VB);
   const int histPasses = nPass;
   const size_t histLds = (size_t)histPasses * kBins * hist_copies<(int)sizeof(U)>() * 4;
@@ -457,8 +438,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     if (allow_lds(thrs_hist_joint<KT>, kJointLds) != hipSuccess || allow_lds(sk, lds) != hipSuccess ||
         (squeeze && allow_lds(thrs_hist_joint<KT, true>, kJointLds) != hipSuccess))
       return THRS_ERROR_HIP;
-    if (planes && (allow_lds(skSplit, lds) != hipSuccess || allow_lds(skPlanes, lds) != hipSuccess ||
-                   allow_lds(skSplitR, lds) != hipSuccess || allow_lds(skPlanesR, lds) != hipSuccess))
+    if (planes && (allow_lds(skSplit, lds) != hipSuccess || allow_lds(skPlanes, lds) != hipSuccess))
       return THRS_ERROR_HIP;
     if constexpr (kKV) {
       if (allow_lds(atomicRank ? thrs_local_kv<KT, VB, true> : thrs_local_kv<KT, VB, false>, LocKV::LDS) != hipSuccess)
@@ -576,9 +556,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                            reinterpret_cast<uint32_t*>(hyb + kBigPosOff), reinterpret_cast<uint32_t*>(hyb + kBigTileOff),
                            reinterpret_cast<uint4*>(scratch + plan.bigHistOff), nLow,
                            sqMode == 1 ? static_cast<const SqueezeWords*>(sample) : nullptr, planes ? 1 : 0,
-                           reserve ? reinterpret_cast<uint32_t*>(hyb + kCursorAOff) : nullptr,
-                           reserve ? reinterpret_cast<uint32_t*>(hyb + kCursorBOff) : nullptr,
-                           reserve ? reinterpret_cast<uint32_t*>(hyb + kRegTileOff) : nullptr, err, g_inject);
+                           err, g_inject);
       };
       if (!local32 && squeeze) {
         plan_rows(1, 0, kSegHistAOff, kRowHistOff);
@@ -669,12 +647,9 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     // every key: both top digits constant) neither -- both are identities,
     // and skipping both keeps the keys in K.
     auto launch_seg = [&](int p, U* kin, U* kout, VW* vin, VW* vout, uint64_t infoOff, uint64_t baseOff,
-                          const uint32_t* gate, uint32_t gateMask, int codec = kCodecKeys, uint64_t curOff = 0) {
+                          const uint32_t* gate, uint32_t gateMask, int codec = kCodecKeys) {
       ProfScope prof(stream, 1, THRS_PK_PASS_SEG, moveBytes);
-      // curOff != 0: the keys-only plane codecs with reserved runs
-      auto kern = codec == kCodecSplit ? (curOff ? skSplitR : skSplit)
-                  : codec == kCodecPlanes ? (curOff ? skPlanesR : skPlanes)
-                                          : sk;
+      auto kern = codec == kCodecSplit ? skSplit : codec == kCodecPlanes ? skPlanes : sk;
       // kCodecPlanes: image-space input (identity map), digit at bits 16-23 of k'
       hipLaunchKernelGGL(kern, dim3((uint32_t)segPerCU * cu_count()), dim3(G::THREADS), lds, stream, kin, kout, vin,
                          vout, codec == kCodecPlanes ? kid : km, codec == kCodecPlanes ? 16 : startBits + 8 * p,
@@ -682,8 +657,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                          status[p & 1], err, grp[p & 1], gate, gateMask, hiP,
                          g_stamps ? g_stamps + (uint64_t)(p - nLow) * (plan.nTiles + kSegTilePad) * kStampSlots
                                   : nullptr,
-                         sqw, curOff ? reinterpret_cast<uint32_t*>(hyb + curOff) : nullptr,
-                         reinterpret_cast<const uint32_t*>(hyb + kRegTileOff), base + nLow * kBins);
+                         sqw);
     };
     const uint64_t sw = plan.wideStatus ? 8 : 4;
     const int setB = (nLow + 1) & 1;
@@ -692,7 +666,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
       // extra tile ids (rows past nTiles) are touched by nothing else.
       if (planes) {
         launch_seg(nLow, K, reinterpret_cast<U*>(loP), V, valOut, kSegInfoAOff, kSegBaseAOff, mode, kGateMode0,
-                   kCodecSplit, reserve ? kCursorAOff : 0);
+                   kCodecSplit);
         launch_seg(nLow, K, keyOut, V, valOut, kSegInfoAOff, kSegBaseAOff, mode, kGateMode1 | kGateMode3);
       } else {
         launch_seg(nLow, K, keyOut, V, valOut, kSegInfoAOff, kSegBaseAOff, mode, kGateMode0 | kGateMode1 | kGateMode3);
@@ -712,7 +686,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     }
     if (planes) {  // mode 0: planes -> lo2; mode 1 (big chunks) / 3 (f32 -0): keys
       launch_seg(nLow + 1, reinterpret_cast<U*>(loP), reinterpret_cast<U*>(lo2P), valOut, V, kSegInfoOff, kSegBaseOff,
-                 mode, kGateMode0, kCodecPlanes, P.reserveB ? kCursorBOff : 0);
+                 mode, kGateMode0, kCodecPlanes);
       launch_seg(nLow + 1, keyOut, K, valOut, V, kSegInfoOff, kSegBaseOff, mode, kGateMode1 | kGateMode3);
     } else if (segTop)
       launch_seg(nLow + 1, keyOut, K, valOut, V, kSegInfoOff, kSegBaseOff, mode, kGateMode0 | kGateMode1 | kGateMode3);

@@ -661,8 +661,7 @@ __global__ __launch_bounds__(kPlanRowThreads) void thrs_plan_rows(
     uint32_t* __restrict__ segInfo, uint32_t* __restrict__ segBase, uint32_t tileKeys, uint32_t histGrid,
     uint32_t* __restrict__ segInfoA, uint32_t* __restrict__ segBaseA, uint32_t* __restrict__ bigB, int sqMode,
     int keyBits, uint32_t* __restrict__ bigPos, uint32_t* __restrict__ bigTile, uint4* __restrict__ bigHist,
-    int nLow, const SqueezeWords* __restrict__ sample, int planes, uint32_t* __restrict__ curA,
-    uint32_t* __restrict__ curB, uint32_t* __restrict__ regTiles, uint32_t* __restrict__ errFlag, int inject) {
+    int nLow, const SqueezeWords* __restrict__ sample, int planes, uint32_t* __restrict__ errFlag, int inject) {
   if (sqMode == 2 && meta[kMetaRehist] == 0) return;
   __shared__ uint32_t s_w[2][4], s_base, s_b2[kBins], s_sq[3], s_last;
   const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6, r = blockIdx.x;
@@ -691,9 +690,6 @@ __global__ __launch_bounds__(kPlanRowThreads) void thrs_plan_rows(
   chunkOff[kBins * r + t] = base + pre;
   chunkB0[kBins * r + t] = kBins * r + t;
   if ((t & 31u) == 0) segBase[(t >> 5) * kBins + r] = base + pre;  // segment s = columns [32s, 32s+32)
-  // reserved runs (thrs_pass_seg RES): the top-digit pass's cursor of bucket
-  // (r, t) starts at the bucket (a tile's 256 cursors lie on 256 lines)
-  if (curB) curB[(kBins * r + t) * kCursorStrideB] = base + pre;
   if (t == 0) baseTop[kBins + r] = base;
   if (x > cap) {  // a bucket above the chunk capacity: a big chunk; all n keys in one bucket: mode 2
     atomicOr(&meta[kMetaFallback], 1u);
@@ -760,18 +756,9 @@ __global__ __launch_bounds__(kPlanRowThreads) void thrs_plan_rows(
 #pragma unroll
   for (int sg = 0; sg < kSegs; ++sg) {
     segBaseA[sg * kBins + t] = sa;
-    if (curA) curA[(sg * kBins + t) * kCursorStrideA] = sa;
     sa += segHistA[sg * kBins + t];
   }
   __syncthreads();
-  if (regTiles) {  // reserved top-digit pass: every second-digit region tiled on its own
-    const uint32_t size = (t + 1 < kBins ? s_b2[t + 1] : n) - s_b2[t];
-    const uint32_t nt = (uint32_t)(((uint64_t)size + tileKeys - 1) / tileKeys);
-    uint32_t total = 0;
-    const uint32_t first = scan256(nt, 1, &total);
-    regTiles[t] = first;
-    if (t == 0) regTiles[kBins] = total;
-  }
   // segment positions, first tile ids (multiples of kGroup), tickets: thread 0
   // for the top-digit pass (second-digit ranges), thread 64 for the
   // second-digit pass (position ranges) -- as thrs_plan

@@ -582,19 +582,14 @@ constexpr int kGroupWindow = THRS_GROUP_WINDOW;
 #endif
 constexpr int kTileWindow = THRS_TILE_WINDOW;  // own-group tile rows per round trip
 constexpr uint32_t kArrival = 1u << 20;
-// reserved runs (pass_tile RES), in words between neighbouring cursors: the
-// second-digit pass's per-(segment, digit) cursors each on a 128-byte line of
-// their own (4096 reservations each per pass at 2^30 keys), the top-digit
-// pass's per-bucket cursors 16 bytes apart (~128 each)
-constexpr uint32_t kCursorStrideA = 32, kCursorStrideB = 4;
 // error word bits (the sort's temp buffer): a look-back / claim spin gave up;
 // a run reserved past the output end was clamped
 constexpr uint32_t kErrSpin = 1u, kErrRunClamped = 2u;
 template <typename ST> struct GroupTables {
   uint32_t* ga;      // [nGroups][256] count | arrivals << 20   (this pass)
   ST* gp;            // [nGroups][256] Status<ST>::pre(inclusive prefix)
-  uint32_t* gaNext;  // next pass's tables, cleared by each group's last tile
-  ST* gpNext;
+  uint32_t* gaNext = nullptr;  // next pass's tables, cleared by each group's last tile
+  ST* gpNext = nullptr;
   uint32_t nTiles;    // end of this tile's chain (tile ids)
   uint32_t gmin = 0;  // first group of this tile's chain (segmented passes)
 };
@@ -958,7 +953,7 @@ struct NoMid {
 // GROUPED = false: the flat per-tile look-back (the per-bucket fallback,
 // whose chains may be shorter than a group; thrs_fallback.hpp).
 template <int KT, int VB, typename ST, bool ATOMIC_RANK, typename Mid, int CODEC = kCodecKeys, bool GROUPED = true,
-          bool RES = false, typename KM>
+          typename KM>
 __device__ __forceinline__ void pass_tile(
     const typename KeyTraits<KT>::U* __restrict__ keysIn, typename KeyTraits<KT>::U* __restrict__ keysOut,
     const typename ValueWord<VB>::T* __restrict__ valsIn, typename ValueWord<VB>::T* __restrict__ valsOut,
@@ -967,12 +962,11 @@ __device__ __forceinline__ void pass_tile(
     uint32_t chainStart, const GroupTables<ST>& grp, unsigned char* smem, uint64_t* __restrict__ stamps,
     typename KeyTraits<KT>::U (&k)[PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::KPT],
     typename ValueWord<VB>::T (&v)[VB ? PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::KPT : 1], Mid mid,
-    uint8_t* __restrict__ hiOut = nullptr, uint32_t* __restrict__ cursor = nullptr, uint32_t curStride = 0) {
+    uint8_t* __restrict__ hiOut = nullptr) {
   using U = typename KeyTraits<KT>::U;
   using VW = typename ValueWord<VB>::T;
   using G = PassGeom<sizeof(U), VB>;
   static_assert(CODEC == kCodecKeys || (sizeof(U) == 4 && VB == 0), "codecs: u32 keys only");
-  static_assert(!RES || VB == 0, "reserved runs reorder equal keys: keys-only passes");
   constexpr int WAVES = G::WAVES, KPT = G::KPT, ROUNDS = G::ROUNDS, THREADS = G::THREADS;
   constexpr uint32_t T = G::TILE, STAGE = G::STAGE, CHUNK = 64 * KPT;
   constexpr int STAGE_SHIFT = __builtin_ctz(STAGE);
@@ -1090,16 +1084,7 @@ __device__ __forceinline__ void pass_tile(
   // counts stores too on gfx9-family parts, so if the walkers (waves 0-3)
   // issued these write-through stores, their first wait on a look-back load
   // would also wait for the stores' acknowledgement -- several us under load.
-  // RES (keys-only passes, thrs_pass_seg with cursors): no status row and no
-  // look-back -- each digit's run is RESERVED on its segment's cursor (one
-  // agent-scope add per digit, issued here and consumed after the rank, so
-  // its round trip runs under the scan and the rank)
-  uint32_t resv = 0;
-  if constexpr (RES) {
-    if (tid < 256) resv = __hip_atomic_fetch_add(cursor + d * curStride, realTot, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-  }
-  if (!RES && PUB_LO <= tid && tid < PUB_LO + 256) {
+  if (PUB_LO <= tid && tid < PUB_LO + 256) {
     const uint32_t dp = tid - PUB_LO;
     uint32_t t2 = 0;
 #pragma unroll
@@ -1213,13 +1198,7 @@ __device__ __forceinline__ void pass_tile(
 
   // ---- D: decoupled look-back for digit d, kLookWindow rows per round trip;
   // a not-yet-published word stops the window and is re-polled.
-  if constexpr (RES) {
-    if (tid < 256) {
-      // (a run past the output end -- only a wrong plan could put it there --
-      // is clamped and reported)
-      s_gofs[d] = clamp_run(resv, 0u, realTot, outEnd, errFlag) - localStart;
-    }
-  } else if constexpr (kGroup > 0 && GROUPED) {
+  if constexpr (kGroup > 0 && GROUPED) {
     if (tid < 256) gw.finish(realTot, myBase, outEnd, localStart, s_gofs, s_misc, errFlag, stamps);
 #ifdef THRS_STAMPS
     if (stamps && lane == 0 && w < 4) {  // slots 12..15: waves 0..3 arrive at the post-walk barrier
@@ -1574,148 +1553,83 @@ __host__ __device__ __forceinline__ uint64_t seg_tile_base(uint32_t pos, uint32_
 __host__ __device__ __forceinline__ uint32_t seg_tiles(uint32_t pos, uint32_t end, uint32_t T) {
   return end > pos ? (uint32_t)(((uint64_t)end - seg_tile_base(pos, T) + T - 1) / T) : 0u;
 }
-// RES (keys only, thrs_options.offsets): no look-back chain -- every tile
-// reserves its digit runs on cursors (pass_tile).  Equal keys of a keys-only
-// sort are identical, so the order of runs inside a region does not matter,
-// but the REGION a key lands in must carry every bit that is not stored:
-//   split codec (second digit): one cursor per (segment, digit) -- the
-//     output keeps the top byte (u8 plane) and the low 16 bits, and its
-//     position gives the second digit;
-//   planes codec (top digit, kReg): its input holds no second digit (only the
-//     position in the second-digit region does), so its tiles never cross a
-//     region: region a = [regPos[a], regPos[a+1]) is tiled on its own (tile
-//     ids regTiles[a] .. regTiles[a+1]), and a tile reserves on the cursors of
-//     the BUCKETS (top digit, a) -- each bucket's keys land in the bucket.
-// cursors: split [8][256] x kCursorStrideA words, planes [256 top][256 a] x
-// kCursorStrideB words (a tile's 256 cursors on 256 lines), set by
-// thrs_plan_rows.
-template <int KT, int VB, typename ST, bool ATOMIC_RANK, int CODEC, bool RES = false>
+template <int KT, int VB, typename ST, bool ATOMIC_RANK, int CODEC>
 __device__ __forceinline__ void thrs_pass_seg_body(
     const typename KeyTraits<KT>::U* __restrict__ keysIn, typename KeyTraits<KT>::U* __restrict__ keysOut,
     const typename ValueWord<VB>::T* __restrict__ valsIn, typename ValueWord<VB>::T* __restrict__ valsOut,
     KeyMap<typename KeyTraits<KT>::U> km, int shift, uint32_t* __restrict__ segInfo,
     const uint32_t* __restrict__ segBase, ST* __restrict__ status, uint32_t* __restrict__ errFlag,
     GroupTables<ST> grp, uint8_t* __restrict__ hiPlane, uint64_t* __restrict__ stamps,
-    const SqueezeWords* __restrict__ sq, uint32_t* __restrict__ cursors, const uint32_t* __restrict__ regTiles,
-    const uint32_t* __restrict__ regPos) {
+    const SqueezeWords* __restrict__ sq) {
   using U = typename KeyTraits<KT>::U;
   using VW = typename ValueWord<VB>::T;
   using G = PassGeom<sizeof(U), VB>;
   constexpr uint32_t T = G::TILE;
-  constexpr bool kReg = RES && CODEC == kCodecPlanes;
-  constexpr uint32_t kRegs = kReg ? kBins + 1 : 1;
-  constexpr uint32_t kRegsPerSeg = kBins / kSegs;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint32_t* s_cnt = reinterpret_cast<uint32_t*>(smem + G::STAGE * (sizeof(U) + VB));
   uint32_t* s_misc = s_cnt + (G::WAVES + 1) * kBins;
   __shared__ uint32_t segPos[kSegs + 1], segTiles[kSegs + 1];  // read once per workgroup
-  __shared__ uint32_t s_rt[kRegs], s_rp[kRegs];                // kReg: region tile ids, positions
   uint32_t* tickets = segInfo + 64;                            // a cache line of their own
   const uint32_t tid = threadIdx.x;
   if (tid < 2 * (kSegs + 1)) (tid <= (uint32_t)kSegs ? segPos[tid] : segTiles[tid - kSegs - 1]) = segInfo[tid];
-  if constexpr (kReg) {
-    for (uint32_t i = tid; i < kRegs; i += G::THREADS) {
-      s_rt[i] = regTiles[i];
-      s_rp[i] = i < kBins ? regPos[i] : segInfo[kSegs];
-    }
-  }
   __syncthreads();
   const uint32_t home = xcc_id() & (kSegs - 1);
-  auto seg_ntiles = [&](uint32_t s) -> uint32_t {
-    if constexpr (kReg) return s_rt[kRegsPerSeg * (s + 1)] - s_rt[kRegsPerSeg * s];
-    else return seg_tiles(segPos[s], segPos[s + 1], T);
-  };
   with_map<KT>(km, sq, [&](auto kmx) __attribute__((always_inline)) {
   uint32_t done = 0;  // thread 0: segments found exhausted
   U k[G::KPT];
   VW v[VB ? G::KPT : 1];
   for (;;) {
-    if (tid < 64) {
+    if (tid == 0) {
       uint32_t seg = kSegs, t = 0;
-      if (tid == 0) {
-        for (int q = 0; q < kSegs; ++q) {
-          const uint32_t s = (home + q) & (kSegs - 1);
-          if (done & (1u << s)) continue;
-          const uint32_t nT = seg_ntiles(s);
-          const uint32_t x = nT ? atomicAdd(&tickets[s], 1u) : nT;
-          if (x < nT) {
-            seg = s;
-            t = x;
-            break;
-          }
-          done |= 1u << s;
+      for (int q = 0; q < kSegs; ++q) {
+        const uint32_t s = (home + q) & (kSegs - 1);
+        if (done & (1u << s)) continue;
+        const uint32_t nT = seg_tiles(segPos[s], segPos[s + 1], T);
+        const uint32_t x = nT ? atomicAdd(&tickets[s], 1u) : nT;
+        if (x < nT) {
+          seg = s;
+          t = x;
+          break;
         }
+        done |= 1u << s;
       }
-      seg = (uint32_t)__builtin_amdgcn_readfirstlane((int)seg);
-      t = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
-      uint32_t a = 0;
-      if constexpr (kReg) {
-        // the tile's region: the last of the segment's 32 regions whose first
-        // tile id is <= this one (one ballot; empty regions share their id)
-        if (seg < (uint32_t)kSegs) {
-          const uint32_t r0 = kRegsPerSeg * seg, gt = s_rt[r0] + t;
-          const uint64_t m = __ballot(tid < kRegsPerSeg && s_rt[r0 + tid] <= gt);
-          a = r0 + 63u - (uint32_t)__builtin_clzll(m);
-        }
-      }
-      if (tid == 0) {
-        s_misc[8] = seg;
-        s_misc[9] = t;
-        s_misc[10] = a;
+      s_misc[8] = seg;
+      s_misc[9] = t;
 #ifdef THRS_STAMPS
-        if (stamps && seg < (uint32_t)kSegs) {  // slot 7: xcc | segment << 4 (| walk maxima, pass_tile)
-          uint64_t* s_stamp = reinterpret_cast<uint64_t*>(s_misc + 16);
-          for (int i = 0; i < kStampSlots; ++i) s_stamp[i] = 0;
-          s_stamp[0] = __builtin_amdgcn_s_memrealtime();
-          s_stamp[7] = xcc_id() | (seg << 4);
-          s_misc[1] = s_misc[2] = s_misc[3] = 0;
-        }
-#endif
+      if (stamps && seg < (uint32_t)kSegs) {  // slot 7: xcc | segment << 4 (| walk maxima, pass_tile)
+        uint64_t* s_stamp = reinterpret_cast<uint64_t*>(s_misc + 16);
+        for (int i = 0; i < kStampSlots; ++i) s_stamp[i] = 0;
+        s_stamp[0] = __builtin_amdgcn_s_memrealtime();
+        s_stamp[7] = xcc_id() | (seg << 4);
+        s_misc[1] = s_misc[2] = s_misc[3] = 0;
       }
+#endif
     }
     for (uint32_t i = tid; i < (uint32_t)(G::WAVES * kBins); i += G::THREADS) s_cnt[i] = 0;
     lds_barrier();
     const uint32_t seg = s_misc[8], t = s_misc[9];
     if (seg >= (uint32_t)kSegs) break;
     const uint32_t segStart = segPos[seg], segEnd = segPos[seg + 1];
-    uint64_t keyStart;
-    uint32_t valid, tileId;
-    uint32_t* cur = nullptr;
-    uint32_t curStride = 0;
-    if constexpr (kReg) {
-      const uint32_t a = s_misc[10];
-      tileId = s_rt[kRegsPerSeg * seg] + t;
-      keyStart = (uint64_t)s_rp[a] + (uint64_t)(tileId - s_rt[a]) * T;
-      valid = (uint32_t)min((uint64_t)T, (uint64_t)s_rp[a + 1] - keyStart);
-      cur = cursors + (uint64_t)a * kCursorStrideB;  // bucket (d, a) at (256 d + a) x stride
-      curStride = kBins * kCursorStrideB;
-    } else {
-      const uint64_t t0 = seg_tile_base(segStart, T) + (uint64_t)t * T;
-      keyStart = max((uint64_t)segStart, t0);
-      valid = (uint32_t)(min((uint64_t)segEnd, t0 + T) - keyStart);
-      tileId = segTiles[seg] + t;
-      if constexpr (RES) {
-        cur = cursors + (uint64_t)seg * kBins * kCursorStrideA;
-        curStride = kCursorStrideA;
-      }
-    }
+    const uint64_t t0 = seg_tile_base(segStart, T) + (uint64_t)t * T;
+    const uint64_t keyStart = max((uint64_t)segStart, t0);
+    const uint32_t valid = (uint32_t)(min((uint64_t)segEnd, t0 + T) - keyStart);
     const uint32_t chain = segTiles[seg];
     GroupTables<ST> g = grp;
     g.nTiles = chain + seg_tiles(segStart, segEnd, T);  // end of this segment's tile ids
     g.gmin = chain / kGroup;
     g.gaNext = nullptr;
     g.gpNext = nullptr;
-    const uint32_t myBase = RES ? 0u : segBase[seg * kBins + (tid & 255u)];
+    const uint32_t myBase = segBase[seg * kBins + (tid & 255u)];
     load_tile<KT, VB, CODEC>(keysIn, valsIn, keyStart, valid, k, v, hiPlane);
-    pass_tile<KT, VB, ST, ATOMIC_RANK, NoMid, CODEC, true, RES>(
-        keysIn, keysOut, valsIn, valsOut, keyStart, valid, kmx, shift, myBase, segPos[kSegs], status, nullptr, errFlag,
-        tileId, chain, g, smem, stamps, k, v, NoMid{}, hiPlane, cur, curStride);
+    pass_tile<KT, VB, ST, ATOMIC_RANK, NoMid, CODEC>(keysIn, keysOut, valsIn, valsOut, keyStart, valid, kmx,
+                                                     shift, myBase, segPos[kSegs], status, nullptr, errFlag, chain + t, chain, g, smem,
+                                                     stamps, k, v, NoMid{}, hiPlane);
     lds_barrier();  // stage, s_gofs and s_misc are reused by the next tile
   }
   });
 }
 
-template <int KT, int VB, typename ST, bool ATOMIC_RANK, int CODEC = kCodecKeys, bool RES = false>
+template <int KT, int VB, typename ST, bool ATOMIC_RANK, int CODEC = kCodecKeys>
 __global__ __launch_bounds__((PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::THREADS))
 __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::WPE))) void thrs_pass_seg(
     const typename KeyTraits<KT>::U* __restrict__ keysIn, typename KeyTraits<KT>::U* __restrict__ keysOut,
@@ -1723,12 +1637,10 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
     KeyMap<typename KeyTraits<KT>::U> km, int shift, uint32_t* __restrict__ segInfo,
     const uint32_t* __restrict__ segBase, ST* __restrict__ status, uint32_t* __restrict__ errFlag,
     GroupTables<ST> grp, const uint32_t* __restrict__ gate, uint32_t gateMask, uint8_t* __restrict__ hiPlane,
-    uint64_t* __restrict__ stamps, const SqueezeWords* __restrict__ sq, uint32_t* __restrict__ cursors,
-    const uint32_t* __restrict__ regTiles, const uint32_t* __restrict__ regPos) {
+    uint64_t* __restrict__ stamps, const SqueezeWords* __restrict__ sq) {
   if (gate && !((gateMask >> *gate) & 1u)) return;
-  thrs_pass_seg_body<KT, VB, ST, ATOMIC_RANK, CODEC, RES>(keysIn, keysOut, valsIn, valsOut, km, shift, segInfo,
-                                                           segBase, status, errFlag, grp, hiPlane, stamps, sq, cursors,
-                                                           regTiles, regPos);
+  thrs_pass_seg_body<KT, VB, ST, ATOMIC_RANK, CODEC>(keysIn, keysOut, valsIn, valsOut, km, shift, segInfo, segBase,
+                                                      status, errFlag, grp, hiPlane, stamps, sq);
 }
 
 // Zeroing of up to three 16-byte-aligned ranges in one launch (the scratch

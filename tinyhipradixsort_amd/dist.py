@@ -389,9 +389,14 @@ class DistributedRadixSort:
         plan = ExchangePlan(cut_points(all_counts, targets), self.rank)
         self.last_plan = plan
         clock.mark("split")
-        rk = torch.empty(plan.n_out * kb, dtype=torch.uint8, device=dev)
-        rv = torch.empty(plan.n_out * vb, dtype=torch.uint8, device=dev) if vb else None
-        self._exchange(rk, rv, pk, pv, plan)
+        if self.world == 1:
+            # every key stays on this rank: the exchange would copy pk into a
+            # buffer of its own size -- finish pk in place
+            rk, rv = pk[:plan.n_out * kb], (pv[:plan.n_out * vb] if vb else None)
+        else:
+            rk = torch.empty(plan.n_out * kb, dtype=torch.uint8, device=dev)
+            rv = torch.empty(plan.n_out * vb, dtype=torch.uint8, device=dev) if vb else None
+            self._exchange(rk, rv, pk, pv, plan)
         del pk, pv
         clock.mark("exchange")
         full = start_bits == 0 and end_bits >= kb * 8
