@@ -657,7 +657,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                          status[p & 1], err, grp[p & 1], gate, gateMask, hiP,
                          g_stamps ? g_stamps + (uint64_t)(p - nLow) * (plan.nTiles + kSegTilePad) * kStampSlots
                                   : nullptr,
-                         sqw);
+                         sqw, codec == kCodecPlanes ? base + nLow * kBins : nullptr);
     };
     const uint64_t sw = plan.wideStatus ? 8 : 4;
     const int setB = (nLow + 1) & 1;

@@ -770,12 +770,13 @@ __global__ __launch_bounds__(kPlanRowThreads) void thrs_plan_rows(
       return top ? s_b2[32 * sg] : hj_seg_pos(n, histGrid, (uint32_t)sg);
     };
     uint32_t tiles = 0;
+    info[kSegAlignWord] = top ? 1u : 0u;  // the top-digit pass's tiles are aligned (thrs_pass_seg_body)
     for (int sg = 0; sg <= kSegs; ++sg) {
       const uint32_t pos = pos_of(sg);
       info[sg] = pos;
       info[kSegs + 1 + sg] = tiles;
       if (sg < kSegs) {
-        const uint32_t nT = seg_tiles(pos, pos_of(sg + 1), tileKeys);
+        const uint32_t nT = seg_tiles(pos, pos_of(sg + 1), tileKeys, top);
         tiles += (nT + kGroup - 1) / kGroup * kGroup;
         info[64 + sg] = 0;  // ticket (own cache line)
       }
@@ -944,12 +945,13 @@ __global__ __launch_bounds__(kPlanThreads) void thrs_plan(const uint32_t* __rest
       return top ? s_b2[32 * sg] : hj_seg_pos(n, histGrid, (uint32_t)sg);
     };
     uint32_t tiles = 0;
+    info[kSegAlignWord] = top ? 1u : 0u;  // the top-digit pass's tiles are aligned (thrs_pass_seg_body)
     for (int sg = 0; sg <= kSegs; ++sg) {
       const uint32_t pos = pos_of(sg);
       info[sg] = pos;
       info[kSegs + 1 + sg] = tiles;
       if (sg < kSegs) {
-        const uint32_t nT = seg_tiles(pos, pos_of(sg + 1), tileKeys);
+        const uint32_t nT = seg_tiles(pos, pos_of(sg + 1), tileKeys, top);
         tiles += (nT + kGroup - 1) / kGroup * kGroup;
         info[64 + sg] = 0;  // ticket (own cache line)
       }

@@ -858,7 +858,7 @@ __device__ __forceinline__ void load_tile(const typename KeyTraits<KT>::U* __res
                                           uint32_t valid,
                                           typename KeyTraits<KT>::U (&k)[PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::KPT],
                                           typename ValueWord<VB>::T (&v)[VB ? PassGeom<sizeof(typename KeyTraits<KT>::U), VB>::KPT : 1],
-                                          const uint8_t* __restrict__ hiIn = nullptr) {
+                                          const uint8_t* __restrict__ hiIn = nullptr, bool vec = false) {
   using U = typename KeyTraits<KT>::U;
   using VW = typename ValueWord<VB>::T;
   using G = PassGeom<sizeof(U), VB>;
@@ -871,6 +871,36 @@ __device__ __forceinline__ void load_tile(const typename KeyTraits<KT>::U* __res
   if constexpr (CODEC == kCodecPlanes) {
     static_assert(sizeof(U) == 4 && VB == 0, "planes: u32 keys without values");
     const uint16_t* lo = reinterpret_cast<const uint16_t*>(keysIn);
+    if constexpr (KPT % 4 == 0) {
+      // vec (a whole tile, keyStart a multiple of 4, inside ONE second-digit
+      // region -- thrs_pass_seg_body): four consecutive keys per lane and
+      // load, item 4q + c of lane l = key 256q + 4l + c of the wave's run: an
+      // 8-byte load of the u16 plane and a dword of the u8 plane, no lane
+      // permutes (a third of the loads, none of the ds_bpermutes).  The rank
+      // then walks the keys out of their input order, which changes nothing
+      // a keys-only sort can see: every key of the tile lands in the same
+      // bucket run, and the order inside a bucket is the local sort's
+      // (docs/EXPERIMENTS.md row 107).
+      if (vec) {
+        const uint2* lq = reinterpret_cast<const uint2*>(lo + chunkBase) + lane;
+        const uint32_t* hq = reinterpret_cast<const uint32_t*>(hiIn + chunkBase) + lane;
+        uint2 l2[KPT / 4];
+        uint32_t h4[KPT / 4];
+#pragma unroll
+        for (int q = 0; q < KPT / 4; ++q) {
+          l2[q] = lq[q * 64];
+          h4[q] = hq[q * 64];
+        }
+#pragma unroll
+        for (int q = 0; q < KPT / 4; ++q) {
+          k[4 * q] = (U)(((h4[q] & 0xFFu) << 16) | (l2[q].x & 0xFFFFu));
+          k[4 * q + 1] = (U)((((h4[q] >> 8) & 0xFFu) << 16) | (l2[q].x >> 16));
+          k[4 * q + 2] = (U)((((h4[q] >> 16) & 0xFFu) << 16) | (l2[q].y & 0xFFFFu));
+          k[4 * q + 3] = (U)(((h4[q] >> 24) << 16) | (l2[q].y >> 16));
+        }
+        return;
+      }
+    }
 #ifndef THRS_HI_DWORD
 #define THRS_HI_DWORD 1
 #endif
@@ -1538,20 +1568,18 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
 // plane written by kCodecSplit / read by kCodecPlanes; keysIn / keysOut are
 // then u16 planes).
 constexpr int kSegs = 8;
-// Tiles of a segment [pos, end) are aligned to the whole key array: tile t
+// Aligned segments (segInfo[kSegAlignWord] = 1: the top-digit pass, whose
+// segments start at data-dependent positions): tile t of a segment [pos, end)
 // covers [max(pos, a + tT), min(end, a + (t+1)T)), a = pos rounded down to a
-// multiple of T, so every interior tile's loads start on a 128-B line (the
-// second top-digit pass's segments start at data-dependent positions: with
-// tiles counted from pos every wave load of u16 keys would straddle two
-// lines); the first tile (and the last) may be partial.
-#ifndef THRS_SEG_ALIGN
-#define THRS_SEG_ALIGN 0  // measured slower (docs/EXPERIMENTS.md row 85): off
-#endif
-__host__ __device__ __forceinline__ uint64_t seg_tile_base(uint32_t pos, uint32_t T) {
-  return THRS_SEG_ALIGN ? (uint64_t)pos / T * T : (uint64_t)pos;
+// multiple of T, so every interior tile starts at a multiple of T -- the
+// planes codec's vector loads need a multiple of 4; the first tile (and the
+// last) may be partial.  Otherwise tiles are counted from pos.
+constexpr int kSegAlignWord = 32;
+__host__ __device__ __forceinline__ uint64_t seg_tile_base(uint32_t pos, uint32_t T, bool align) {
+  return align ? (uint64_t)pos / T * T : (uint64_t)pos;
 }
-__host__ __device__ __forceinline__ uint32_t seg_tiles(uint32_t pos, uint32_t end, uint32_t T) {
-  return end > pos ? (uint32_t)(((uint64_t)end - seg_tile_base(pos, T) + T - 1) / T) : 0u;
+__host__ __device__ __forceinline__ uint32_t seg_tiles(uint32_t pos, uint32_t end, uint32_t T, bool align) {
+  return end > pos ? (uint32_t)(((uint64_t)end - seg_tile_base(pos, T, align) + T - 1) / T) : 0u;
 }
 template <int KT, int VB, typename ST, bool ATOMIC_RANK, int CODEC>
 __device__ __forceinline__ void thrs_pass_seg_body(
@@ -1560,19 +1588,29 @@ __device__ __forceinline__ void thrs_pass_seg_body(
     KeyMap<typename KeyTraits<KT>::U> km, int shift, uint32_t* __restrict__ segInfo,
     const uint32_t* __restrict__ segBase, ST* __restrict__ status, uint32_t* __restrict__ errFlag,
     GroupTables<ST> grp, uint8_t* __restrict__ hiPlane, uint64_t* __restrict__ stamps,
-    const SqueezeWords* __restrict__ sq) {
+    const SqueezeWords* __restrict__ sq, const uint32_t* __restrict__ secondBase) {
   using U = typename KeyTraits<KT>::U;
   using VW = typename ValueWord<VB>::T;
   using G = PassGeom<sizeof(U), VB>;
   constexpr uint32_t T = G::TILE;
+  // the planes codec (the top-digit pass over second-digit regions): whole,
+  // aligned tiles inside one region take the vector loads (load_tile)
+  constexpr bool kVec = CODEC == kCodecPlanes && G::KPT % 4 == 0;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint32_t* s_cnt = reinterpret_cast<uint32_t*>(smem + G::STAGE * (sizeof(U) + VB));
   uint32_t* s_misc = s_cnt + (G::WAVES + 1) * kBins;
-  __shared__ uint32_t segPos[kSegs + 1], segTiles[kSegs + 1];  // read once per workgroup
-  uint32_t* tickets = segInfo + 64;                            // a cache line of their own
+  __shared__ uint32_t segPos[kSegs + 1], segTiles[kSegs + 1], s_align;  // read once per workgroup
+  __shared__ uint32_t s_b2[kVec ? kBins : 1];                            // second-digit region starts
+  uint32_t* tickets = segInfo + 64;                                      // a cache line of their own
   const uint32_t tid = threadIdx.x;
   if (tid < 2 * (kSegs + 1)) (tid <= (uint32_t)kSegs ? segPos[tid] : segTiles[tid - kSegs - 1]) = segInfo[tid];
+  if (tid == 0) s_align = segInfo[kSegAlignWord];
+  if constexpr (kVec) {
+    if (secondBase)
+      for (uint32_t i = tid; i < kBins; i += G::THREADS) s_b2[i] = secondBase[i];
+  }
   __syncthreads();
+  const bool salign = s_align != 0;
   const uint32_t home = xcc_id() & (kSegs - 1);
   with_map<KT>(km, sq, [&](auto kmx) __attribute__((always_inline)) {
   uint32_t done = 0;  // thread 0: segments found exhausted
@@ -1584,7 +1622,7 @@ __device__ __forceinline__ void thrs_pass_seg_body(
       for (int q = 0; q < kSegs; ++q) {
         const uint32_t s = (home + q) & (kSegs - 1);
         if (done & (1u << s)) continue;
-        const uint32_t nT = seg_tiles(segPos[s], segPos[s + 1], T);
+        const uint32_t nT = seg_tiles(segPos[s], segPos[s + 1], T, salign);
         const uint32_t x = nT ? atomicAdd(&tickets[s], 1u) : nT;
         if (x < nT) {
           seg = s;
@@ -1610,17 +1648,28 @@ __device__ __forceinline__ void thrs_pass_seg_body(
     const uint32_t seg = s_misc[8], t = s_misc[9];
     if (seg >= (uint32_t)kSegs) break;
     const uint32_t segStart = segPos[seg], segEnd = segPos[seg + 1];
-    const uint64_t t0 = seg_tile_base(segStart, T) + (uint64_t)t * T;
+    const uint64_t t0 = seg_tile_base(segStart, T, salign) + (uint64_t)t * T;
     const uint64_t keyStart = max((uint64_t)segStart, t0);
     const uint32_t valid = (uint32_t)(min((uint64_t)segEnd, t0 + T) - keyStart);
+    bool vec = false;
+    if constexpr (kVec) {
+      // no second-digit region boundary inside the tile (its keys all go to
+      // the buckets of one second digit): the segment's 31 inner boundaries,
+      // one per lane, checked by every wave
+      if (secondBase && valid == T && (keyStart & 3u) == 0) {
+        const uint32_t lane = tid & 63u;
+        const uint32_t b = lane < kBins / kSegs - 1 ? s_b2[(kBins / kSegs) * seg + 1 + lane] : 0u;
+        vec = __ballot(lane < kBins / kSegs - 1 && b > keyStart && (uint64_t)b < keyStart + T) == 0;
+      }
+    }
     const uint32_t chain = segTiles[seg];
     GroupTables<ST> g = grp;
-    g.nTiles = chain + seg_tiles(segStart, segEnd, T);  // end of this segment's tile ids
+    g.nTiles = chain + seg_tiles(segStart, segEnd, T, salign);  // end of this segment's tile ids
     g.gmin = chain / kGroup;
     g.gaNext = nullptr;
     g.gpNext = nullptr;
     const uint32_t myBase = segBase[seg * kBins + (tid & 255u)];
-    load_tile<KT, VB, CODEC>(keysIn, valsIn, keyStart, valid, k, v, hiPlane);
+    load_tile<KT, VB, CODEC>(keysIn, valsIn, keyStart, valid, k, v, hiPlane, vec);
     pass_tile<KT, VB, ST, ATOMIC_RANK, NoMid, CODEC>(keysIn, keysOut, valsIn, valsOut, keyStart, valid, kmx,
                                                      shift, myBase, segPos[kSegs], status, nullptr, errFlag, chain + t, chain, g, smem,
                                                      stamps, k, v, NoMid{}, hiPlane);
@@ -1637,10 +1686,10 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
     KeyMap<typename KeyTraits<KT>::U> km, int shift, uint32_t* __restrict__ segInfo,
     const uint32_t* __restrict__ segBase, ST* __restrict__ status, uint32_t* __restrict__ errFlag,
     GroupTables<ST> grp, const uint32_t* __restrict__ gate, uint32_t gateMask, uint8_t* __restrict__ hiPlane,
-    uint64_t* __restrict__ stamps, const SqueezeWords* __restrict__ sq) {
+    uint64_t* __restrict__ stamps, const SqueezeWords* __restrict__ sq, const uint32_t* __restrict__ secondBase) {
   if (gate && !((gateMask >> *gate) & 1u)) return;
   thrs_pass_seg_body<KT, VB, ST, ATOMIC_RANK, CODEC>(keysIn, keysOut, valsIn, valsOut, km, shift, segInfo, segBase,
-                                                      status, errFlag, grp, hiPlane, stamps, sq);
+                                                      status, errFlag, grp, hiPlane, stamps, sq, secondBase);
 }
 
 // Zeroing of up to three 16-byte-aligned ranges in one launch (the scratch
