@@ -708,7 +708,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
       if constexpr (kKV) {
         auto lk = atomicRank ? thrs_local_kv<KT, VB, true> : thrs_local_kv<KT, VB, false>;
         hipLaunchKernelGGL(lk, lgrid, dim3(LocKV::THREADS), LocKV::LDS, stream, K, V, km, chunkOff, chunkB0, meta,
-                           sqw);
+                           sqw, g_lstamps);
       } else if constexpr (kPairs4) {
         auto launch_pairs = [&](auto geom) {
           using LG = decltype(geom);

@@ -2186,7 +2186,8 @@ __device__ __noinline__ void kv8_six_rounds(unsigned char* smem, uint32_t size) 
 template <int KT, int VB, bool ATOMIC_RANK, typename KM>
 __device__ __forceinline__ void local_kv_chunk(typename KeyTraits<KT>::U* __restrict__ keys,
                                                typename ValueWord<VB>::T* __restrict__ vals, KM km, uint32_t c,
-                                               uint32_t start, uint32_t size, const uint32_t* __restrict__ chunkB0) {
+                                               uint32_t start, uint32_t size, const uint32_t* __restrict__ chunkB0,
+                                               uint64_t* stp) {
   using U = typename KeyTraits<KT>::U;
   constexpr int KB = (int)sizeof(U);
   using Item = typename std::conditional<KB == 4, uint32_t, uint64_t>::type;
@@ -2279,20 +2280,28 @@ __device__ __forceinline__ void local_kv_chunk(typename KeyTraits<KT>::U* __rest
         it[j] = (j * 64 < lim) ? ((uint32_t)(im >> 32) << 16) | p : 0xFFFF0000u | p;
       }
     }
+    loc_stamp(stp, 1);
     round(it, st, 16);
     reload(it, st);
     round(it, st, 24);
+    loc_stamp(stp, 2);
     auto pre_of = [&](uint32_t slot) -> uint32_t { return st[slot] >> 16; };
     auto key_of = [&](uint32_t v) -> uint64_t { return ((uint64_t)low[v & 0xFFFFu] << 16) | (v & 0xFFFFu); };
     bool over = false;
-    for (uint32_t h = tid; h + 1 < size; h += LocKV::THREADS) {
-      const uint32_t pre = pre_of(h);
-      if ((h > 0 && pre_of(h - 1) == pre) || pre_of(h + 1) != pre) continue;  // not a run's first slot
-      uint32_t e = h + 2;
+    // The runs' first slots among this lane's slots (neighbours read FB
+    // slots at a time: independent loads, one wait) as a bit mask; then
+    // each lane walks its own runs (random keys: ~1.7 per lane, a few lanes
+    // with 5-6).  A run of up to four items -- all but ~1 run in 10^4 -- is
+    // sorted by a four-input network in registers (items past the run rank
+    // last), a longer one insertion-sorted.  (Per-slot predicated code for
+    // the runs cost ~7000 instructions per wave -- the fix-up was issue-bound
+    // at 13 us per chunk; docs/EXPERIMENTS.md row 111.)
+    auto sort_run = [&](uint32_t h, uint32_t pre) __attribute__((always_inline)) {
+      uint32_t e = h + 5;  // (h .. h + 4 are in the run)
       while (e < size && e - h <= (uint32_t)kTieScan && pre_of(e) == pre) ++e;
       if (e - h > (uint32_t)kTieScan) {
         over = true;
-        continue;
+        return;
       }
       for (uint32_t i = h + 1; i < e; ++i) {
         const uint32_t x = st[i];
@@ -2301,9 +2310,87 @@ __device__ __forceinline__ void local_kv_chunk(typename KeyTraits<KT>::U* __rest
         for (; j > h && key_of(st[j - 1]) > kx; --j) st[j] = st[j - 1];
         st[j] = x;
       }
+    };
+    auto cx = [](uint64_t& x, uint64_t& y) __attribute__((always_inline)) {
+      const uint64_t lo = x < y ? x : y, hi = x < y ? y : x;
+      x = lo;
+      y = hi;
+    };
+    uint32_t fm = 0;
+    constexpr int FB = 6;
+#pragma unroll
+    for (int j0 = 0; j0 < KPT; j0 += FB) {
+      uint32_t c[FB], pv[FB], n1[FB];
+#pragma unroll
+      for (int jj = 0; jj < FB; ++jj) {
+        if (j0 + jj < KPT) {  // (st[s + 1] <= st[CAP]: the low words, in the LDS)
+          const uint32_t s = myOff + 64 * (j0 + jj);
+          c[jj] = st[s];
+          pv[jj] = st[s == 0 ? 0u : s - 1];
+          n1[jj] = st[s + 1];
+        }
+      }
+#pragma unroll
+      for (int jj = 0; jj < FB; ++jj) {
+        if (j0 + jj < KPT) {
+          const uint32_t s = myOff + 64 * (j0 + jj), pre = c[jj] >> 16;
+          const bool f = s + 1 < size && (n1[jj] >> 16) == pre && (s == 0 || (pv[jj] >> 16) != pre);
+          fm |= (f ? 1u : 0u) << (j0 + jj);
+        }
+      }
+    }
+    auto fix_run = [&](uint32_t h) __attribute__((always_inline)) {
+      // (h + 1 < size <= CAP: h + 4 <= CAP + 2, in the LDS)
+      const uint32_t w0 = st[h], w1 = st[h + 1], w2 = st[h + 2], w3 = st[h + 3], w4 = st[h + 4];
+      const uint32_t pre = w0 >> 16;
+      const bool m2 = h + 2 < size && (w2 >> 16) == pre;
+      const bool m3 = m2 && h + 3 < size && (w3 >> 16) == pre;
+      if (m3 && h + 4 < size && (w4 >> 16) == pre) {
+        sort_run(h, pre);
+        return;
+      }
+      constexpr uint32_t PMAX = LocKV::CAP - 1;  // (a slot past the run may hold anything)
+      const uint32_t l0 = low[w0 & 0xFFFFu], l1 = low[w1 & 0xFFFFu];
+      const uint32_t l2 = low[min(w2 & 0xFFFFu, PMAX)], l3 = low[min(w3 & 0xFFFFu, PMAX)];
+      uint64_t k0 = ((uint64_t)l0 << 16) | (w0 & 0xFFFFu), k1 = ((uint64_t)l1 << 16) | (w1 & 0xFFFFu);
+      uint64_t k2 = m2 ? ((uint64_t)l2 << 16) | (w2 & 0xFFFFu) : ~(uint64_t)0;
+      uint64_t k3 = m3 ? ((uint64_t)l3 << 16) | (w3 & 0xFFFFu) : ~(uint64_t)0;
+      cx(k0, k1);
+      cx(k2, k3);
+      cx(k0, k2);
+      cx(k1, k3);
+      cx(k1, k2);
+      const uint32_t hi = w0 & 0xFFFF0000u;
+      st[h] = hi | (uint32_t)(k0 & 0xFFFFu);
+      st[h + 1] = hi | (uint32_t)(k1 & 0xFFFFu);
+      if (m2) st[h + 2] = hi | (uint32_t)(k2 & 0xFFFFu);
+      if (m3) st[h + 3] = hi | (uint32_t)(k3 & 0xFFFFu);
+    };
+    {
+      // the wave's runs listed in its (now free) counter words, then taken
+      // one per lane: ~2 passes instead of the busiest lane's ~6 runs
+      uint32_t* list = reinterpret_cast<uint32_t*>(smem + (size_t)LocKV::CAP * 8) + w * kBins;
+      const uint32_t cnt = (uint32_t)__builtin_popcount(fm);
+      const uint32_t incl = wave_incl_scan(cnt, lane);
+      const uint32_t R = min(__shfl(incl, 63), (uint32_t)kBins);
+      uint32_t k = incl - cnt;
+      uint32_t f = fm;
+      while (f && k < (uint32_t)kBins) {
+        const uint32_t j = (uint32_t)__builtin_ctz(f);
+        f &= f - 1;
+        list[k++] = myOff + 64u * j;
+        fm &= ~(1u << j);
+      }
+      for (uint32_t i = lane; i < R; i += 64) fix_run(list[i]);
+    }
+    while (fm) {  // (more runs than list words: the rest by their own lane)
+      const uint32_t h = myOff + 64u * (uint32_t)__builtin_ctz(fm);
+      fm &= fm - 1;
+      fix_run(h);
     }
     if (over) s_over = 1;  // (every writer stores 1)
     lds_barrier();
+    loc_stamp(stp, 3);
     if (s_over == 0) {
 #pragma unroll
       for (int j = 0; j < KPT; ++j) it[j] = st[myOff + j * 64];
@@ -2326,12 +2413,14 @@ __device__ __forceinline__ void local_kv_chunk(typename KeyTraits<KT>::U* __rest
       for (int j = 0; j < KPT; ++j) pos[j / 2] |= (uint32_t)(st64[myOff + j * 64] & 0xFFFFu) << (16 * (j & 1));
     }
   }
+  loc_stamp(stp, 4);
   U* kdst = keys + start + myOff;
   if constexpr (!PERMUTE_KEYS) {
 #pragma unroll
     for (int j = 0; j < KPT; ++j)
       if (j * 64 < lim) kdst[j * 64] = kinv_int(km, (U)(hiImg | (U)img[j]));  // integer keys: rebuilt
   }
+  loc_stamp(stp, 5);
   // carried positions: two 16-bit halves per register
   auto pos_of = [&](int j) -> uint32_t { return (pos[j / 2] >> (16 * (j & 1))) & 0xFFFFu; };
   // out[j] = in[pos_of(j)] through the stage, for T of 4 or 8 bytes
@@ -2383,6 +2472,17 @@ __device__ __forceinline__ void local_kv_chunk(typename KeyTraits<KT>::U* __rest
       if (j * 64 < lim) vdst[j * 64] = make_uint4((uint32_t)o[j], (uint32_t)(o[j] >> 32), (uint32_t)h, (uint32_t)(h >> 32));
     }
   }
+#ifdef THRS_STAMPS
+  if (stp) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    loc_stamp(stp, 6);
+    if (threadIdx.x == 0) {
+      uint32_t hw;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+      stp[7] = hw;
+    }
+  }
+#endif
 }
 
 template <int KT, int VB, bool ATOMIC_RANK>
@@ -2392,7 +2492,8 @@ __global__ __launch_bounds__(LocKV::THREADS) void thrs_local_kv(typename KeyTrai
                                                                 const uint32_t* __restrict__ chunkOff,
                                                                 const uint32_t* __restrict__ chunkB0,
                                                                 const uint32_t* __restrict__ meta,
-                                                                const SqueezeWords* __restrict__ sq) {
+                                                                const SqueezeWords* __restrict__ sq,
+                                                                uint64_t* __restrict__ stamps) {
   using U = typename KeyTraits<KT>::U;
   constexpr int KB = (int)sizeof(U);
   static_assert(KB == 8 || VB >= 8, "4-byte keys with 0 / 4-byte values: thrs_local16 / thrs_local / thrs_local_pairs");
@@ -2400,13 +2501,15 @@ __global__ __launch_bounds__(LocKV::THREADS) void thrs_local_kv(typename KeyTrai
   if (c >= meta[kMetaChunks]) return;
   const uint32_t start = chunkOff[c], size = chunkOff[c + 1] - start;
   if (size == 0 || size > LocKV::CAP) return;  // big chunk: the per-bucket fallback sorts it
+  uint64_t* st = stamps ? stamps + (uint64_t)c * kLocStampSlots : nullptr;
+  loc_stamp(st, 0);
   if constexpr (kSqueezable<KT>) {
     if (sq && sq->on) {
-      local_kv_chunk<KT, VB, ATOMIC_RANK>(keys, vals, with_squeeze(kmh, sq), c, start, size, chunkB0);
+      local_kv_chunk<KT, VB, ATOMIC_RANK>(keys, vals, with_squeeze(kmh, sq), c, start, size, chunkB0, st);
       return;
     }
   }
-  local_kv_chunk<KT, VB, ATOMIC_RANK>(keys, vals, kmh, c, start, size, chunkB0);
+  local_kv_chunk<KT, VB, ATOMIC_RANK>(keys, vals, kmh, c, start, size, chunkB0, st);
 }
 
 }  // namespace
