@@ -63,7 +63,7 @@ typedef struct thrs_config {
  * never fit the local sort).  Nothing is read from the environment. */
 enum { THRS_PATH_AUTO = 0, THRS_PATH_LSD = 1, THRS_PATH_BUCKET = 2 };
 enum { THRS_LOCAL_AUTO = 0, THRS_LOCAL_BIG = 1, THRS_LOCAL_SMALL = 2, THRS_LOCAL_BIG32 = 3, THRS_LOCAL_COUNT16 = 4,
-       THRS_LOCAL_RANK16 = 5, THRS_LOCAL_WIDE16 = 6 };
+       THRS_LOCAL_RANK16 = 5, THRS_LOCAL_WIDE16 = 6, THRS_LOCAL_TINY16 = 7 };
 enum { THRS_SEG_AUTO = 0, THRS_SEG_TOP_ONLY = 1, THRS_SEG_NONE = 2 };
 enum { THRS_CLAIMS_AUTO = 0, THRS_CLAIMS_XCD_BLOCKS = 1, THRS_CLAIMS_TICKET = 2 };
 enum { THRS_RANK_AUTO = 0, THRS_RANK_ATOMIC = 1, THRS_RANK_BALLOT = 2 };
@@ -78,7 +78,8 @@ typedef struct thrs_options {
                             key sort 16-bit items, BIG32 = 32-bit items; u32 keys-only:
                             COUNT16 = counting sort of the 16-bit items, RANK16 = two
                             LSD rounds on them; WIDE16 = 34816-key chunks (AUTO above
-                            2^30 + 2^26, to 2^31 + 2^25).  Sorts with 8/16-byte values
+                            2^30 + 2^26, to 2^31 + 2^25); TINY16 = 4096-key chunks
+                            (AUTO for u32 up to 3 x 2^26).  Sorts with 8/16-byte values
                             or 8-byte keys use 17408-key chunks whatever is asked.    */
   int32_t segmented;     /* THRS_SEG_*: XCD-segmented top-digit passes (AUTO: both)   */
   int32_t tileClaims;    /* THRS_CLAIMS_*: XCD-block tile claims in the digit passes

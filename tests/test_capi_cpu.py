@@ -79,11 +79,14 @@ def test_temporary_buffer_layout(kt, vt, n):
     # plus a fixed ~1.1 MiB: the 3-pass path's bucket histogram and chunk table
     # and the segmented pass's extra look-back rows; u32 / f32 keys: + the
     # bucket path's u8 plane (n bytes: its two u16 planes fill keyOut),
-    # reserved only where the default takes that path (n in [150M, 2^31 + 2^25])
-    plane = -(-n // 256) * 256 if kt in (T.KeyType.U32, T.KeyType.F32) and 150000000 <= n <= (1 << 31) + (1 << 25) \
-        else 0
+    # reserved only where the default takes that path (n in [90M (u32) / 150M
+    # (f32), 2^31 + 2^25]),
+    # and room for a big chunk per 4097 keys (the 4096-key local geometry:
+    # 3 KiB of fallback tables each, ~0.75 B per key below 2^28 keys)
+    lo = 90000000 if kt == T.KeyType.U32 else 150000000
+    plane = -(-n // 256) * 256 if kt in (T.KeyType.U32, T.KeyType.F32) and lo <= n <= (1 << 31) + (1 << 25) else 0
     if n >= (1 << 20):
-        assert d.pSumBuffer < 0.3 * d.keyOutBuffer + plane + (3 << 20) // 2
+        assert d.pSumBuffer < (0.4 if kb == 4 else 0.3) * d.keyOutBuffer + plane + (3 << 20) // 2
 
 
 def test_argument_validation_needs_no_device():
@@ -146,9 +149,16 @@ def test_path_info_matches_the_configs():
     assert (c4["path"], c4["local"], c4["planes"], c4["local_cap"]) == ("bucket", "thrs_local16", True, 9216)
     assert c4["min_bytes"] == (4 + 7 + 5 + 6) * (1 << 28)
     # the lower bounds of the default's bucket window (docs/EXPERIMENTS.md row 87)
-    assert info(U32, T.ValueType.U32, 149999999, False)["path"] == "lsd"
-    assert info(U32, T.ValueType.U32, 150000000, False)["path"] == "bucket"
-    assert info(U32, T.ValueType.U32, 150000000, False)["planes"]
+    assert info(U32, T.ValueType.U32, 89999999, False)["path"] == "lsd"
+    assert info(U32, T.ValueType.U32, 90000000, False)["path"] == "bucket"
+    assert info(U32, T.ValueType.U32, 90000000, False)["planes"]
+    assert info(F32, T.ValueType.U32, 149999999, False)["path"] == "lsd"
+    assert info(F32, T.ValueType.U32, 150000000, False)["path"] == "bucket"
+    # u32 keys-only up to 3 x 2^26: 4096-key chunks (docs/EXPERIMENTS.md row 112)
+    assert info(U32, T.ValueType.U32, 160000000, False)["local_cap"] == 4096
+    assert info(U32, T.ValueType.U32, 3 << 26, False)["local_cap"] == 4096
+    assert info(U32, T.ValueType.U32, (3 << 26) + 1, False)["local_cap"] == 9216
+    assert info(F32, T.ValueType.U32, 160000000, False)["local_cap"] == 9216
     assert info(U32, T.ValueType.U32, 99999999, True)["path"] == "lsd"
     assert info(U32, T.ValueType.U32, 100000000, True)["path"] == "bucket"
     assert info(U64, T.ValueType.U32, (1 << 28) - 1, False)["path"] == "lsd"

@@ -178,7 +178,8 @@ def test_cpp_port_with_path_forced(gpu, path):
 
 @pytest.mark.parametrize("geom,seg", [("big", "1"), ("small", "1"), ("big", "0"), ("big", "top"), ("big32", "1"),
                                       ("big", "1-noplanes"), ("count16", "1"), ("count16", "1-noplanes"),
-                                      ("count16", "0"), ("wide16", "1"), ("wide16", "1-noplanes")])
+                                      ("count16", "0"), ("wide16", "1"), ("wide16", "1-noplanes"), ("tiny16", "1"),
+                                      ("tiny16", "1-noplanes")])
 @pytest.mark.parametrize("kt", [O.U32, O.F32])
 @pytest.mark.parametrize("desc", [False, True])
 def test_hybrid_paths_vs_oracle(gpu, kt, desc, geom, seg):
@@ -526,7 +527,7 @@ def test_local_kv_tie_runs(gpu, kt, vb, desc):
 
 
 @pytest.mark.parametrize("desc", [False, True])
-@pytest.mark.parametrize("geom", ["auto", "small", "wide16"])
+@pytest.mark.parametrize("geom", ["auto", "small", "wide16", "tiny16"])
 def test_f32_keys_only_zero_chunk(gpu, desc, geom):
     """f32 keys-only on the bucket path sort 16-bit items (thrs_local16): +0
     and -0 share one image, so the chunk holding it takes the zeros' bit

@@ -140,7 +140,7 @@ class Options:
     reference counterpart.  Every choice gives the same bit-exact result; the
     defaults are the library's own choice.  Values are the names below."""
     path: str = "auto"            # auto | lsd | bucket
-    localGeometry: str = "auto"   # auto | big | small | big32 | count16 | rank16 | wide16
+    localGeometry: str = "auto"   # auto | big | small | big32 | count16 | rank16 | wide16 | tiny16
     segmented: str = "auto"       # auto | top_only | none
     tileClaims: str = "auto"      # auto | xcd_blocks | ticket
     rank: str = "auto"            # auto | atomic | ballot
@@ -150,7 +150,7 @@ class Options:
     # getKeyBits(k) ^ (descending ? ~0 : 0) lies in [rangeLo, rangeHi]; None = no promise
     keyRange: "tuple[int, int] | None" = None
 
-    _ENUMS = {"path": ("auto", "lsd", "bucket"), "localGeometry": ("auto", "big", "small", "big32", "count16", "rank16", "wide16"),
+    _ENUMS = {"path": ("auto", "lsd", "bucket"), "localGeometry": ("auto", "big", "small", "big32", "count16", "rank16", "wide16", "tiny16"),
               "segmented": ("auto", "top_only", "none"), "tileClaims": ("auto", "xcd_blocks", "ticket"),
               "rank": ("auto", "atomic", "ballot"), "planes": ("auto", "on", "off"), "squeeze": ("auto", "off")}
 

@@ -37,7 +37,9 @@ using namespace thrs_dev;
 
 constexpr uint64_t kAlign = 256;
 // the bucket path's lower bounds (default path; docs/EXPERIMENTS.md row 87)
-constexpr uint64_t kBucketMinKeys4 = 150000000ull;   // 4-byte keys without values
+constexpr uint64_t kBucketMinKeys4 = 150000000ull;   // f32 keys without values
+constexpr uint64_t kBucketMinKeysU32 = 90000000ull;  // u32 keys without values (4096-key chunks: row 112)
+constexpr uint64_t kTiny16MaxKeys = 3ull << 26;      // u32 keys-only: 4096-key chunks (Loc16Tiny) up to here
 constexpr uint64_t kBucketMinPairs4 = 100000000ull;  // 4-byte keys with 4-byte values
 constexpr uint64_t kHistOff = 0;                       // u32 [8][256]
 constexpr uint64_t kBaseOff = 8 * 256 * 4;             // u32 [8][256]
@@ -133,9 +135,11 @@ inline Plan make_plan(int keyType, int valueBytesOrZero, uint32_t n) {
   p.tileKeys = tile_keys(p.kb, p.vb);
   p.nTiles = std::max<uint64_t>(1, ((uint64_t)n + p.tileKeys - 1) / p.tileKeys);
   p.wideStatus = (uint64_t)n >= (1ull << 31);
-  // the per-bucket fallback (thrs_fallback.hpp): big chunks hold > kMinLocalCap
-  // keys each, and there are at most 65536 buckets
-  p.bigMax = std::min<uint64_t>(kBuckets, (uint64_t)n / (kMinLocalCap + 1) + 1);
+  // the per-bucket fallback (thrs_fallback.hpp): big chunks hold more keys
+  // than the smallest local capacity each (4-byte keys-only: Loc16Tiny's),
+  // and there are at most 65536 buckets
+  const uint64_t minCap = (p.kb == 4 && p.vb == 0) ? (uint64_t)Loc16Tiny::CAP : kMinLocalCap;
+  p.bigMax = std::min<uint64_t>(kBuckets, (uint64_t)n / (minCap + 1) + 1);
   // status rows: a tile id per tile, + the segmented passes' extra ids (each
   // segment rounds up to a look-back group) or the fallback's (a partial tile
   // per big chunk; the fallback passes use the same two table sets)
@@ -158,10 +162,12 @@ inline Plan make_plan(int keyType, int valueBytesOrZero, uint32_t n) {
   // planes fill keyOut, which is all a sortKeys caller must allocate
   // (getTemporaryBufferBytesForSortKeys = pSumBuffer + keyOutBuffer).  Only
   // where the default takes the bucket path with planes (u32 / f32 keys-only,
-  // n in [kBucketMinKeys4, 2^31 + 2^25]); a forced bucket path elsewhere runs
+  // n in [kBucketMinKeysU32 (u32) / kBucketMinKeys4 (f32), 2^31 + 2^25]); a
+  // forced bucket path elsewhere runs
   // without them.
   p.hiPlaneOff = p.scratchBytes;
-  if ((keyType == THRS_KEY_U32 || keyType == THRS_KEY_F32) && valueBytesOrZero == 0 && (uint64_t)n >= kBucketMinKeys4 &&
+  if ((keyType == THRS_KEY_U32 || keyType == THRS_KEY_F32) && valueBytesOrZero == 0 &&
+      (uint64_t)n >= (keyType == THRS_KEY_U32 ? kBucketMinKeysU32 : kBucketMinKeys4) &&
       (uint64_t)n <= (1ull << 31) + (1ull << 25))
     p.scratchBytes += round_up(n, kAlign);
   return p;
@@ -219,7 +225,7 @@ hipError_t allow_lds(F kernel, size_t bytes) {
 // The path one sort takes (host decision, no device work): run_sort and
 // thrs_path_info (thrs_capi.hip) share it.
 struct PathSel {
-  bool bucket, fullWindow, smallLocal, local16, wide16, small16, count16, local32, segTop, segA, planes, ranged, useXb;
+  bool bucket, fullWindow, smallLocal, local16, wide16, tiny16, small16, count16, local32, segTop, segA, planes, ranged, useXb;
   int nLow;
   uint32_t cap;
 };
@@ -262,7 +268,7 @@ PathSel select_path(uint32_t n, int startBits, int nPass, const thrs_options& op
   // (the 2^27 bound of a ranged finish is measured for 4-byte keys without
   // values, the C2 finish; other key / value types keep their own bounds)
   const uint64_t minN = (rangedReq && kKeys4) ? (1ull << 27)
-                        : kKeys4  ? kBucketMinKeys4
+                        : kKeys4  ? (KT == 0 ? kBucketMinKeysU32 : kBucketMinKeys4)
                         : (KB == 4 && VB == 4) ? kBucketMinPairs4
                                                : (1ull << 28);
   const bool sizeOk = nn >= minN && nn <= (1ull << 30) + (kKV ? (1ull << 24) : (1ull << 26));
@@ -294,7 +300,11 @@ PathSel select_path(uint32_t n, int startBits, int nPass, const thrs_options& op
   // 9216-key chunks for n <= 2^29 (or asked: SMALL)
   const bool wide16 = local16 && (opt.localGeometry == THRS_LOCAL_WIDE16 ||
                                   (opt.localGeometry == THRS_LOCAL_AUTO && nEff > (double)((1ull << 30) + (1ull << 26))));
-  const bool small16 = local16 && !wide16 && smallLocal;
+  // ... in 4096-key chunks for u32 up to 3 x 2^26 keys (or asked: TINY16)
+  const bool tiny16 = local16 && !wide16 &&
+                      (opt.localGeometry == THRS_LOCAL_TINY16 ||
+                       (opt.localGeometry == THRS_LOCAL_AUTO && KT == 0 && nEff <= (double)kTiny16MaxKeys));
+  const bool small16 = local16 && !wide16 && !tiny16 && smallLocal;
   // ... u32 only: sorted by counting (thrs_local_count16) when asked (it
   // measured slower, docs/EXPERIMENTS.md row 56)
   const bool count16 = local16 && KT == 0 && !wide16 && !small16 && opt.localGeometry == THRS_LOCAL_COUNT16;
@@ -310,7 +320,10 @@ PathSel select_path(uint32_t n, int startBits, int nPass, const thrs_options& op
                       plan.scratchBytes - plan.hiPlaneOff >= (uint64_t)n;
   // the local sort's chunk capacity (a bigger bucket is a big chunk)
   const uint32_t cap = kKV ? LocKV::CAP
-                       : local16 ? (wide16 ? Loc16Wide::CAP : small16 ? Loc16Small::CAP : Loc16::CAP)
+                       : local16 ? (wide16    ? Loc16Wide::CAP
+                                    : tiny16  ? Loc16Tiny::CAP
+                                    : small16 ? Loc16Small::CAP
+                                              : Loc16::CAP)
                                  : (smallLocal ? LocSmall::CAP : LocBig::CAP);
   // The key range (thrs_options.keyRange, thrs_kernels.hpp KeyMap): for
   // full-window sorts, except the 32-bit local sort (it sorts the keys
@@ -328,6 +341,7 @@ PathSel select_path(uint32_t n, int startBits, int nPass, const thrs_options& op
   P.smallLocal = smallLocal;
   P.local16 = local16;
   P.wide16 = wide16;
+  P.tiny16 = tiny16;
   P.small16 = small16;
   P.count16 = count16;
   P.local32 = local32;
@@ -746,6 +760,8 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
           }
         } else if (wide16) {
           launch16(Loc16Wide{});
+        } else if (P.tiny16) {
+          launch16(Loc16Tiny{});
         } else if (small16) {
           launch16(Loc16Small{});
         } else if (local16) {

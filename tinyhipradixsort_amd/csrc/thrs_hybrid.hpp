@@ -1350,6 +1350,12 @@ template <int W, int K, int WPE_ = 6, int LB_ = K> struct Loc16G {
 using Loc16 = Loc16G<8, 36>;
 // n <= 2^29: 9216-key chunks (uniform buckets of <= 8K keys), 6 WGs per CU
 using Loc16Small = Loc16G<4, 36, 6, 36>;
+// u32 keys-only up to 3 x 2^26 keys (uniform buckets of <= 3072 keys): 4096-
+// key chunks, 8 WGs per CU.  A chunk's items spread over all four waves
+// (~10 per lane at 160M keys instead of 36 in wave 0 and ~2 in wave 1 of a
+// 9216-key chunk): the rounds' critical path is 2-3x shorter
+// (docs/EXPERIMENTS.md row 112)
+using Loc16Tiny = Loc16G<4, 16, 8, 16>;
 static_assert(Loc16::CAP == LocBig::CAP, "same chunk capacity as the 32-bit geometry (thrs_plan's cap)");
 // Wide chunks for u32 keys-only sorts above 2^30 + 2^26, whose uniform
 // buckets (n / 65536 keys) outgrow Loc16's 18432 slots: 34816 keys (8 waves x
@@ -2372,7 +2378,7 @@ __device__ __forceinline__ void local_kv_chunk(typename KeyTraits<KT>::U* __rest
       uint32_t* list = reinterpret_cast<uint32_t*>(smem + (size_t)LocKV::CAP * 8) + w * kBins;
       const uint32_t cnt = (uint32_t)__builtin_popcount(fm);
       const uint32_t incl = wave_incl_scan(cnt, lane);
-      const uint32_t R = min(__shfl(incl, 63), (uint32_t)kBins);
+      const uint32_t R = min(lane63(incl), (uint32_t)kBins);
       uint32_t k = incl - cnt;
       uint32_t f = fm;
       while (f && k < (uint32_t)kBins) {
