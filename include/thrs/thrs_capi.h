@@ -252,7 +252,7 @@ enum { THRS_PK_ZERO = 0, THRS_PK_HIST = 1, THRS_PK_SCAN = 2, THRS_PK_HIST_JOINT 
        THRS_PK_PASS = 5, THRS_PK_PASS_XB = 6, THRS_PK_PASS_SEG = 7, THRS_PK_LOCAL16 = 8, THRS_PK_LOCAL = 9,
        THRS_PK_LOCAL_PAIRS = 10, THRS_PK_LOCAL_KV = 11, THRS_PK_LOCAL_COUNT16 = 12, THRS_PK_BIG_PLAN = 13,
        THRS_PK_BIG_HIST = 14, THRS_PK_PASS_BIG = 15, THRS_PK_BIG_COPY = 16, THRS_PK_COPY = 17,
-       THRS_PK_SQUEEZE_SAMPLE = 18 };
+       THRS_PK_SQUEEZE_SAMPLE = 18, THRS_PK_HIST_REDUCE = 19 };
 int thrs_profile_read_launch_kernels(int kind, int32_t* kernel, uint64_t* bytes, int cap, int* count);
 /* The kernel function's name for a THRS_PK_* id ("" for an unknown id). */
 const char* thrs_profile_kernel_name(int kernel);

@@ -488,7 +488,7 @@ THRS_API const char* thrs_profile_kernel_name(int kernel) {
                                 "thrs_pass", "thrs_pass_xb", "thrs_pass_seg", "thrs_local16", "thrs_local",
                                 "thrs_local_pairs", "thrs_local_kv", "thrs_local_count16", "thrs_big_plan",
                                 "thrs_big_hist", "thrs_pass_big", "thrs_big_copy", "copy-back",
-                                "thrs_squeeze_sample"};
+                                "thrs_squeeze_sample", "thrs_hist_reduce"};
   return kernel >= 0 && kernel < (int)(sizeof(names) / sizeof(names[0])) ? names[kernel] : "";
 }
 

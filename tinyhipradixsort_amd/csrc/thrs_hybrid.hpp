@@ -158,7 +158,8 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
                                                                 uint32_t* __restrict__ rowHist /* [256] */,
                                                                 ZeroRanges tables, uint32_t* __restrict__ meta,
                                                                 const SqueezeWords* __restrict__ sq,
-                                                                uint32_t* __restrict__ zeroLog) {
+                                                                uint32_t* __restrict__ zeroLog,
+                                                                uint32_t* __restrict__ partial) {
   using U = typename KeyTraits<KT>::U;
   if constexpr (SECOND) {
     if (meta[kMetaRehist] == 0) return;
@@ -383,14 +384,24 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
       atomicAdd(&rowHist[b >> 8], mult * 0x8000u);
     }
   }
-  // the flush: one 64-bit add per LDS word (its two buckets are neighbours
-  // in joint, and no bucket's total reaches 2^32: no carry crosses them) --
-  // half the global atomics of one add per bucket
-  for (uint32_t wi = tid; wi < kJointWords; wi += kHistThreads) {
-    const uint32_t x = s_joint[wi];
-    if (x)
-      atomicAdd(reinterpret_cast<unsigned long long*>(joint) + wi,
-                (unsigned long long)(x & 0xFFFFu) | ((unsigned long long)(x >> 16) << 32));
+  // the flush.  partial (the temporary buffer's keyOut region, free until the
+  // first pass): the workgroup's 128 KiB of packed counts as plain 16-byte
+  // stores, summed by thrs_hist_reduce -- 65536 x 256 global atomics (64 MB
+  // of memory-side adds at ~1.3 TB/s) cost 45-78 us at the end of the kernel
+  // (docs/EXPERIMENTS.md row 113).  Otherwise (keyOut too small: n < 2^16)
+  // one 64-bit add per LDS word (its two buckets are neighbours in joint, and
+  // no bucket's total reaches 2^32: no carry crosses them).
+  if (partial) {
+    uint4* pv = reinterpret_cast<uint4*>(partial + (uint64_t)blockIdx.x * kJointWords);
+    const uint4* sv = reinterpret_cast<const uint4*>(s_joint);
+    for (uint32_t i = tid; i < kJointWords / 4; i += kHistThreads) pv[i] = sv[i];
+  } else {
+    for (uint32_t wi = tid; wi < kJointWords; wi += kHistThreads) {
+      const uint32_t x = s_joint[wi];
+      if (x)
+        atomicAdd(reinterpret_cast<unsigned long long*>(joint) + wi,
+                  (unsigned long long)(x & 0xFFFFu) | ((unsigned long long)(x >> 16) << 32));
+    }
   }
   // the range's second-digit counts (column sums; lanes d, d+1 share a word)
   static_assert(kHistThreads == 4 * kBins, "four top-digit quarters per second digit");
@@ -645,6 +656,47 @@ __device__ __forceinline__ void plan_big_prefix(const uint32_t* __restrict__ joi
   if (t == kPlanRowThreads - 1) {
     bigPos[M] = pk;
     bigTile[M] = pt;
+  }
+}
+
+// The bucket histogram's workgroup partials (thrs_hist_joint with partial):
+// G x 32768 words, each two 15-bit counts (buckets 2w, 2w + 1).  Workgroup r
+// owns buckets [256r, 256r + 256) = words [128r, 128r + 128): thread t sums
+// 16-byte column t & 31 over the partials g = t >> 5, + 32, ... (8 loads in
+// flight at G = 256), the 32 phases meet in LDS, and bucket 256r + t adds its
+// total to joint (which holds the workgroups' logged carries already).
+constexpr int kHistReduceThreads = 1024;
+template <bool SECOND>
+__global__ __launch_bounds__(kHistReduceThreads) void thrs_hist_reduce(const uint32_t* __restrict__ partial,
+                                                                        uint32_t G, uint32_t* __restrict__ joint,
+                                                                        const uint32_t* __restrict__ meta) {
+  if constexpr (SECOND) {
+    if (meta[kMetaRehist] == 0) return;
+  }
+  __shared__ uint32_t s_sum[32][kBins + 1];
+  const uint32_t t = threadIdx.x, q = t & 31u, p = t >> 5, r = blockIdx.x;
+  const uint4* pv = reinterpret_cast<const uint4*>(partial) + (uint64_t)r * 32 + q;
+  uint32_t f[8] = {};
+#pragma unroll 8
+  for (uint32_t g = p; g < G; g += 32) {
+    const uint4 x = pv[(uint64_t)g * (kJointWords / 4)];
+    f[0] += x.x & 0xFFFFu;
+    f[1] += x.x >> 16;
+    f[2] += x.y & 0xFFFFu;
+    f[3] += x.y >> 16;
+    f[4] += x.z & 0xFFFFu;
+    f[5] += x.z >> 16;
+    f[6] += x.w & 0xFFFFu;
+    f[7] += x.w >> 16;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s_sum[p][8 * q + i] = f[i];
+  __syncthreads();
+  if (t < kBins) {
+    uint32_t tot = 0;
+#pragma unroll 8
+    for (int i = 0; i < 32; ++i) tot += s_sum[i][t];
+    joint[kBins * r + t] += tot;
   }
 }
 
