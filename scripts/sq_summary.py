@@ -14,7 +14,8 @@ d = sys.argv[1]
 per = defaultdict(lambda: defaultdict(float))
 for p in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
     for r in read_csv(p):
-        name = col(r, "Kernel_Name", "Kernel-Name", "KernelName").replace("thrs_dev::", "").split("(")[0]
+        name = col(r, "Kernel_Name", "Kernel-Name", "KernelName").replace("thrs_dev::", "").replace(
+            "(anonymous namespace)::", "").split("(")[0]
         disp = col(r, "Dispatch_Id", "Dispatch-Id", "DispatchId", "Correlation_Id")
         per[(name, p, disp)][col(r, "Counter_Name", "Counter-Name", "CounterName")] += float(
             col(r, "Counter_Value", "Counter-Value", "CounterValue"))
