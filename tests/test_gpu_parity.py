@@ -449,7 +449,7 @@ def test_full_size_low_entropy(gpu, dist, kt, vb, n):
 
 
 @pytest.mark.parametrize("kt,vb", [(O.U32, 8), (O.U32, 16), (O.F32, 4), (O.F32, 8), (O.F32, 16), (O.U64, 4),
-                                   (O.U64, 16), (O.F64, 4), (O.F64, 16)])
+                                   (O.U64, 16), (O.F64, 4), (O.F64, 8), (O.F64, 16)])
 @pytest.mark.parametrize("desc", [False, True])
 def test_bucket_wide_payloads_vs_oracle(gpu, kt, vb, desc):
     """f1 (SURVEY.md s8): sortPairs with 8/16-byte payloads (ValueType::U128,

@@ -2251,7 +2251,14 @@ __device__ __forceinline__ void local_kv_chunk(typename KeyTraits<KT>::U* __rest
   using Item = typename std::conditional<KB == 4, uint32_t, uint64_t>::type;
   constexpr int KPT = LocKV::KPT;
   constexpr uint32_t CHUNK = 64 * KPT;
-  constexpr bool PERMUTE_KEYS = KT == 2 || KT == 3;  // floats travel by position (their -0 is not rebuilt)
+  // Float keys are rebuilt from their images like integer keys, except in
+  // the chunk holding +0's image: -0 shares it, so that chunk's keys travel
+  // by position (permuted through the stage).  (All float chunks permuted
+  // their keys -- a second, unprefetched load -- until row 114.)
+  bool permKeys = false;
+  if constexpr (KT == 2 || KT == 3)
+    permKeys = (uint32_t)(kimg<KT>(km, (typename KeyTraits<KT>::U)0) >> (8 * sizeof(typename KeyTraits<KT>::U) - 16)) ==
+               chunkB0[c];
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const U hiImg = (U)chunkB0[c] << (8 * KB - 16);  // the bucket: the image's top 16 bits
   const uint32_t tid = threadIdx.x, lane = tid & 63;
@@ -2278,7 +2285,9 @@ __device__ __forceinline__ void local_kv_chunk(typename KeyTraits<KT>::U* __rest
   };
   // 4- / 8-byte values with integer keys: loaded now, used after the sort
   // (the loads land while the workgroup works in LDS)
-  constexpr bool PREFETCH = (VB == 4 || VB == 8) && !PERMUTE_KEYS;
+  // (f64 keys with 8-byte values: the prefetched values spill ~25 VGPRs at
+  // the 128-VGPR cap, so those load theirs after the sort)
+  constexpr bool PREFETCH = (VB == 4 || VB == 8) && !(KT == 3 && VB == 8);
   using VW = typename ValueWord<VB>::T;
   VW xv[PREFETCH ? KPT : 1];
   // the sorted chunk, per output slot myOff + 64j: the image below the
@@ -2473,10 +2482,10 @@ __device__ __forceinline__ void local_kv_chunk(typename KeyTraits<KT>::U* __rest
   }
   loc_stamp(stp, 4);
   U* kdst = keys + start + myOff;
-  if constexpr (!PERMUTE_KEYS) {
+  if (!permKeys) {
 #pragma unroll
     for (int j = 0; j < KPT; ++j)
-      if (j * 64 < lim) kdst[j * 64] = kinv_int(km, (U)(hiImg | (U)img[j]));  // integer keys: rebuilt
+      if (j * 64 < lim) kdst[j * 64] = kinv_key<KT>(km, (U)(hiImg | (U)img[j]));  // rebuilt from the image
   }
   loc_stamp(stp, 5);
   // carried positions: two 16-bit halves per register
@@ -2502,7 +2511,7 @@ __device__ __forceinline__ void local_kv_chunk(typename KeyTraits<KT>::U* __rest
     for (int j = 0; j < KPT; ++j)
       if (j * 64 < lim) arr[start + myOff + j * 64] = x[j];
   };
-  if constexpr (PERMUTE_KEYS) permute(keys, nullptr);
+  if (permKeys) permute(keys, nullptr);
   if constexpr (PREFETCH) permute(vals, xv);
   else if constexpr (VB == 4 || VB == 8) permute(vals, nullptr);
   if constexpr (VB == 16) {
@@ -2562,8 +2571,9 @@ __global__ __launch_bounds__(LocKV::THREADS) void thrs_local_kv(typename KeyTrai
   uint64_t* st = stamps ? stamps + (uint64_t)c * kLocStampSlots : nullptr;
   loc_stamp(st, 0);
   if constexpr (kSqueezable<KT>) {
-    if (sq && sq->on) {
-      local_kv_chunk<KT, VB, ATOMIC_RANK>(keys, vals, with_squeeze(kmh, sq), c, start, size, chunkB0, st);
+    if (sq && sq->on) {  // (the squeeze fixed to the chunk's image half: fewer scalars, as thrs_local16)
+      const int h = (int)(chunkB0[c] >> 15);
+      local_kv_chunk<KT, VB, ATOMIC_RANK>(keys, vals, half_map(kmh, sq, h), c, start, size, chunkB0, st);
       return;
     }
   }

@@ -191,6 +191,17 @@ template <int KT> __device__ __forceinline__ uint32_t kinv(const KeyMapHalf<uint
   return unbits32<KT>(kinv_int(m, y));
 }
 
+// raw 8-byte key whose getKeyBits image is y (f64: as unbits32)
+template <int KT> __device__ __forceinline__ uint64_t unbits64(uint64_t y) {
+  if constexpr (KT == 3) return (y >> 63) ? (y ^ 0x8000000000000000ull) : ~y;
+  else return y;
+}
+// the key of any type whose image (under m: KeyMap or KeyMapHalf) is y
+template <int KT, typename M, typename U> __device__ __forceinline__ U kinv_key(const M& m, U y) {
+  if constexpr (sizeof(U) == 4) return unbits32<KT>(kinv_int(m, y));
+  else return unbits64<KT>(kinv_int(m, y));
+}
+
 // value payloads: 4, 8 or 16 bytes moved as opaque words
 template <int VB> struct ValueWord;
 template <> struct ValueWord<4> { using T = uint32_t; };
