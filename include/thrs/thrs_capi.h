@@ -79,7 +79,8 @@ typedef struct thrs_options {
                             COUNT16 = counting sort of the 16-bit items, RANK16 = two
                             LSD rounds on them; WIDE16 = 34816-key chunks (AUTO above
                             2^30 + 2^26, to 2^31 + 2^25); TINY16 = 4096-key chunks
-                            (AUTO for u32 up to 3 x 2^26).  Sorts with 8/16-byte values
+                            for 4-byte keys alone or with 4-byte values (AUTO for
+                            u32 up to 3 x 2^26).  Sorts with 8/16-byte values
                             or 8-byte keys use 17408-key chunks whatever is asked.    */
   int32_t segmented;     /* THRS_SEG_*: XCD-segmented top-digit passes (AUTO: both)   */
   int32_t tileClaims;    /* THRS_CLAIMS_*: XCD-block tile claims in the digit passes

@@ -159,8 +159,12 @@ def test_path_info_matches_the_configs():
     assert info(U32, T.ValueType.U32, 3 << 26, False)["local_cap"] == 4096
     assert info(U32, T.ValueType.U32, (3 << 26) + 1, False)["local_cap"] == 9216
     assert info(F32, T.ValueType.U32, 160000000, False)["local_cap"] == 9216
-    assert info(U32, T.ValueType.U32, 99999999, True)["path"] == "lsd"
-    assert info(U32, T.ValueType.U32, 100000000, True)["path"] == "bucket"
+    assert info(U32, T.ValueType.U32, 160000000, True)["local_cap"] == 4096   # pairs too (row 115)
+    assert info(F32, T.ValueType.U32, 160000000, True)["local_cap"] == 9216
+    assert info(U32, T.ValueType.U32, 49999999, True)["path"] == "lsd"
+    assert info(U32, T.ValueType.U32, 50000000, True)["path"] == "bucket"
+    assert info(F32, T.ValueType.U32, 99999999, True)["path"] == "lsd"
+    assert info(F32, T.ValueType.U32, 100000000, True)["path"] == "bucket"
     assert info(U64, T.ValueType.U32, (1 << 28) - 1, False)["path"] == "lsd"
     c5 = info(U64, T.ValueType.U64, 1 << 30, True)
     assert (c5["path"], c5["local"], c5["local_cap"]) == ("bucket", "thrs_local_kv", 17408)

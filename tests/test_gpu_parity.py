@@ -222,7 +222,7 @@ def test_hybrid_paths_vs_oracle(gpu, kt, desc, geom, seg):
 
 
 @pytest.mark.parametrize("desc", [False, True])
-@pytest.mark.parametrize("geom", ["big", "small"])
+@pytest.mark.parametrize("geom", ["big", "small", "tiny16"])
 def test_hybrid_pairs_vs_oracle(gpu, desc, geom):
     """sortPairs with u32 keys + u32 values over the whole key takes the hybrid
     path (single-bucket chunks, positions carried in the local sort's items);

@@ -41,6 +41,7 @@ constexpr uint64_t kBucketMinKeys4 = 150000000ull;   // f32 keys without values
 constexpr uint64_t kBucketMinKeysU32 = 90000000ull;  // u32 keys without values (4096-key chunks: row 112)
 constexpr uint64_t kTiny16MaxKeys = 3ull << 26;      // u32 keys-only: 4096-key chunks (Loc16Tiny) up to here
 constexpr uint64_t kBucketMinPairs4 = 100000000ull;  // 4-byte keys with 4-byte values
+constexpr uint64_t kBucketMinPairsU32 = 50000000ull;  // u32 keys + 4-byte values (4096-key chunks: row 115)
 constexpr uint64_t kHistOff = 0;                       // u32 [8][256]
 constexpr uint64_t kBaseOff = 8 * 256 * 4;             // u32 [8][256]
 constexpr uint64_t kCounterOff = 2 * 8 * 256 * 4;      // u32 [8]
@@ -138,7 +139,8 @@ inline Plan make_plan(int keyType, int valueBytesOrZero, uint32_t n) {
   // the per-bucket fallback (thrs_fallback.hpp): big chunks hold more keys
   // than the smallest local capacity each (4-byte keys-only: Loc16Tiny's),
   // and there are at most 65536 buckets
-  const uint64_t minCap = (p.kb == 4 && p.vb == 0) ? (uint64_t)Loc16Tiny::CAP : kMinLocalCap;
+  static_assert(LocTiny::CAP == Loc16Tiny::CAP, "one smallest capacity for 4-byte keys");
+  const uint64_t minCap = (p.kb == 4 && p.vb <= 4) ? (uint64_t)Loc16Tiny::CAP : kMinLocalCap;
   p.bigMax = std::min<uint64_t>(kBuckets, (uint64_t)n / (minCap + 1) + 1);
   // status rows: a tile id per tile, + the segmented passes' extra ids (each
   // segment rounds up to a look-back group) or the fallback's (a partial tile
@@ -225,7 +227,7 @@ hipError_t allow_lds(F kernel, size_t bytes) {
 // The path one sort takes (host decision, no device work): run_sort and
 // thrs_path_info (thrs_capi.hip) share it.
 struct PathSel {
-  bool bucket, fullWindow, smallLocal, local16, wide16, tiny16, small16, count16, local32, segTop, segA, planes, ranged, useXb;
+  bool bucket, fullWindow, smallLocal, local16, wide16, tiny16, tinyPairs, small16, count16, local32, segTop, segA, planes, ranged, useXb;
   int nLow;
   uint32_t cap;
 };
@@ -269,7 +271,7 @@ PathSel select_path(uint32_t n, int startBits, int nPass, const thrs_options& op
   // values, the C2 finish; other key / value types keep their own bounds)
   const uint64_t minN = (rangedReq && kKeys4) ? (1ull << 27)
                         : kKeys4  ? (KT == 0 ? kBucketMinKeysU32 : kBucketMinKeys4)
-                        : (KB == 4 && VB == 4) ? kBucketMinPairs4
+                        : (KB == 4 && VB == 4) ? (KT == 0 ? kBucketMinPairsU32 : kBucketMinPairs4)
                                                : (1ull << 28);
   const bool sizeOk = nn >= minN && nn <= (1ull << 30) + (kKV ? (1ull << 24) : (1ull << 26));
   const bool wideOk = kKeys4 && fullWindow && nn > (1ull << 30) + (1ull << 26) && nn <= (1ull << 31) + (1ull << 25);
@@ -305,6 +307,10 @@ PathSel select_path(uint32_t n, int startBits, int nPass, const thrs_options& op
                       (opt.localGeometry == THRS_LOCAL_TINY16 ||
                        (opt.localGeometry == THRS_LOCAL_AUTO && KT == 0 && nEff <= (double)kTiny16MaxKeys));
   const bool small16 = local16 && !wide16 && !tiny16 && smallLocal;
+  // u32 keys + 4-byte values likewise (thrs_local_pairs in LocTiny chunks)
+  const bool tinyPairs = KB == 4 && VB == 4 && bucket && fullWindow &&
+                         (opt.localGeometry == THRS_LOCAL_TINY16 ||
+                          (opt.localGeometry == THRS_LOCAL_AUTO && KT == 0 && nEff <= (double)kTiny16MaxKeys));
   // ... u32 only: sorted by counting (thrs_local_count16) when asked (it
   // measured slower, docs/EXPERIMENTS.md row 56)
   const bool count16 = local16 && KT == 0 && !wide16 && !small16 && opt.localGeometry == THRS_LOCAL_COUNT16;
@@ -324,7 +330,8 @@ PathSel select_path(uint32_t n, int startBits, int nPass, const thrs_options& op
                                     : tiny16  ? Loc16Tiny::CAP
                                     : small16 ? Loc16Small::CAP
                                               : Loc16::CAP)
-                                 : (smallLocal ? LocSmall::CAP : LocBig::CAP);
+                       : tinyPairs ? LocTiny::CAP
+                                   : (smallLocal ? LocSmall::CAP : LocBig::CAP);
   // The key range (thrs_options.keyRange, thrs_kernels.hpp KeyMap): for
   // full-window sorts, except the 32-bit local sort (it sorts the keys
   // themselves and pads with keys)
@@ -342,6 +349,7 @@ PathSel select_path(uint32_t n, int startBits, int nPass, const thrs_options& op
   P.local16 = local16;
   P.wide16 = wide16;
   P.tiny16 = tiny16;
+  P.tinyPairs = tinyPairs;
   P.small16 = small16;
   P.count16 = count16;
   P.local32 = local32;
@@ -744,7 +752,8 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                              reinterpret_cast<uint32_t*>(K), reinterpret_cast<uint32_t*>(V), km32, chunkOff, chunkB0,
                              meta, sqw, zeroLog ? meta + kMetaNegZero : nullptr);
         };
-        if (smallLocal) launch_pairs(LocSmall{});
+        if (P.tinyPairs) launch_pairs(LocTiny{});
+        else if (smallLocal) launch_pairs(LocSmall{});
         else launch_pairs(LocBig{});
       } else if constexpr (kKeys4) {
         auto launch16 = [&](auto geom) {

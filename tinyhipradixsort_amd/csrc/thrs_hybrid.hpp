@@ -1095,13 +1095,16 @@ constexpr int kLocCfg[2] = {THRS_LOC_CFG};
 //            buckets of 2^30-key sorts (~16K keys)
 //   LocSmall 4 x 36 = 9216 keys, 4 WGs / CU (36 KiB + 4 KiB): buckets of
 //            2^27..2^29-key sorts, where a large chunk's fixed cost dominates
-template <int W, int K> struct LocG {
-  static constexpr int WAVES = W, KPT = K, THREADS = 64 * W;
+template <int W, int K, int WPE_ = 4> struct LocG {
+  static constexpr int WAVES = W, KPT = K, THREADS = 64 * W, WPE = WPE_;
   static constexpr uint32_t CAP = (uint32_t)THREADS * K;
   template <typename U> static constexpr size_t lds() { return (size_t)CAP * sizeof(U) + (size_t)W * kBins * 4; }
 };
 using LocBig = LocG<kLocCfg[0], kLocCfg[1]>;
 using LocSmall = LocG<4, 36>;
+// u32 pairs up to 3 x 2^26 keys: 4096-key chunks, 8 WGs per CU (as Loc16Tiny,
+// docs/EXPERIMENTS.md row 115)
+using LocTiny = LocG<4, 16, 6>;
 constexpr int kLocWaves = LocBig::WAVES, kLocThreads = LocBig::THREADS, kLocKpt = LocBig::KPT;
 constexpr uint32_t kLocCap = LocBig::CAP;  // 18432 keys
 // chunking windows T = 2^logT (<= CAP/2): uniform buckets of the size range a
@@ -1984,7 +1987,7 @@ __device__ __forceinline__ void pairs_items(uint32_t (&it)[KPT], KM km, uint32_t
 }
 
 template <int KT, bool ATOMIC_RANK, typename LG>
-__global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(4))) void thrs_local_pairs(
+__global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(LG::WPE))) void thrs_local_pairs(
     uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, KeyMap<uint32_t> km,
     const uint32_t* __restrict__ chunkOff, const uint32_t* __restrict__ chunkB0, const uint32_t* __restrict__ meta,
     const SqueezeWords* __restrict__ sq, const uint32_t* __restrict__ zeroFlag) {
