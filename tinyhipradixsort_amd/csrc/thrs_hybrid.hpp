@@ -2119,6 +2119,8 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(LG:
 // 16-B access per lane, full lines) and pass the 8-byte stage in two halves.
 // One workgroup of 16 waves x 17 items = 17408 slots: 136 KiB of 8-byte
 // stage + 16 KiB of per-wave counters, one per CU.
+// (8 waves x 34 items, 248 VGPRs at two waves per SIMD: u64 keys 5.76 vs
+// 5.00 ms, C5 shape 7.82 vs 7.29 -- docs/EXPERIMENTS.md row 116)
 struct LocKV {
   static constexpr int WAVES = 16, KPT = 17, THREADS = 64 * WAVES;
   static constexpr uint32_t CAP = (uint32_t)THREADS * KPT;  // 17408
@@ -2386,7 +2388,8 @@ __device__ __forceinline__ void local_kv_chunk(typename KeyTraits<KT>::U* __rest
       x = lo;
       y = hi;
     };
-    uint32_t fm = 0;
+    static_assert(LocKV::KPT <= 64, "one mask bit per slot of the lane");
+    uint64_t fm = 0;
     constexpr int FB = 6;
 #pragma unroll
     for (int j0 = 0; j0 < KPT; j0 += FB) {
@@ -2405,7 +2408,7 @@ __device__ __forceinline__ void local_kv_chunk(typename KeyTraits<KT>::U* __rest
         if (j0 + jj < KPT) {
           const uint32_t s = myOff + 64 * (j0 + jj), pre = c[jj] >> 16;
           const bool f = s + 1 < size && (n1[jj] >> 16) == pre && (s == 0 || (pv[jj] >> 16) != pre);
-          fm |= (f ? 1u : 0u) << (j0 + jj);
+          fm |= (f ? 1ull : 0ull) << (j0 + jj);
         }
       }
     }
@@ -2440,21 +2443,21 @@ __device__ __forceinline__ void local_kv_chunk(typename KeyTraits<KT>::U* __rest
       // the wave's runs listed in its (now free) counter words, then taken
       // one per lane: ~2 passes instead of the busiest lane's ~6 runs
       uint32_t* list = reinterpret_cast<uint32_t*>(smem + (size_t)LocKV::CAP * 8) + w * kBins;
-      const uint32_t cnt = (uint32_t)__builtin_popcount(fm);
+      const uint32_t cnt = (uint32_t)__builtin_popcountll(fm);
       const uint32_t incl = wave_incl_scan(cnt, lane);
       const uint32_t R = min(lane63(incl), (uint32_t)kBins);
       uint32_t k = incl - cnt;
-      uint32_t f = fm;
+      uint64_t f = fm;
       while (f && k < (uint32_t)kBins) {
-        const uint32_t j = (uint32_t)__builtin_ctz(f);
+        const uint32_t j = (uint32_t)__builtin_ctzll(f);
         f &= f - 1;
         list[k++] = myOff + 64u * j;
-        fm &= ~(1u << j);
+        fm &= ~(1ull << j);
       }
       for (uint32_t i = lane; i < R; i += 64) fix_run(list[i]);
     }
     while (fm) {  // (more runs than list words: the rest by their own lane)
-      const uint32_t h = myOff + 64u * (uint32_t)__builtin_ctz(fm);
+      const uint32_t h = myOff + 64u * (uint32_t)__builtin_ctzll(fm);
       fm &= fm - 1;
       fix_run(h);
     }
