@@ -561,12 +561,6 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
       uint32_t* partial = (uint64_t)hgrid * kJointWords * 4 <= (uint64_t)n * sizeof(U)
                               ? reinterpret_cast<uint32_t*>(keyOutBuf)
                               : nullptr;
-      auto reduce = [&](auto second, uint32_t* jt) {
-        if (!partial) return;
-        ProfScope prof(stream, 0, THRS_PK_HIST_REDUCE, (uint64_t)hgrid * kJointWords * 4);
-        hipLaunchKernelGGL(thrs_hist_reduce<decltype(second)::value>, dim3(kJointWords / 128),
-                           dim3(kHistReduceThreads), 0, stream, partial, (uint32_t)hgrid, jt, meta);
-      };
       {
         ProfScope prof(stream, 0, THRS_PK_HIST_JOINT, keyBytes);
         hipLaunchKernelGGL(thrs_hist_joint<KT>, dim3(hgrid), dim3(kHistThreads), kJointLds, stream,
@@ -574,7 +568,11 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                          reinterpret_cast<uint32_t*>(hyb + kSegHistAOff), reinterpret_cast<uint32_t*>(hyb + kRowHistOff),
                          tables, meta, sample, zeroLog, partial);
       }
-      reduce(std::false_type{}, joint);
+      if (partial) {
+        ProfScope prof(stream, 0, THRS_PK_HIST_REDUCE, (uint64_t)hgrid * kJointWords * 4);
+        hipLaunchKernelGGL(thrs_hist_reduce, dim3(kJointWords / 128), dim3(kHistReduceThreads), 0, stream, partial,
+                           (uint32_t)hgrid, joint);
+      }
       // single-bucket chunks: one workgroup per top digit; float keys with
       // the whole key decide the squeeze (sqMode 1) and, if it went on,
       // histogram and plan once more under it (gated: a few us otherwise)
@@ -594,14 +592,15 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
       };
       if (!local32 && squeeze) {
         plan_rows(1, 0, kSegHistAOff, kRowHistOff);
+        // (the second histogram runs only on a wrong guess: it flushes with
+        // global atomics, so no gated reduce launch follows it every sort)
         {
           ProfScope prof(stream, 0, THRS_PK_HIST_JOINT, keyBytes);
           hipLaunchKernelGGL((thrs_hist_joint<KT, true>), dim3(hgrid), dim3(kHistThreads), kJointLds, stream,
                              static_cast<const U*>(keys), n, km, startBits + 8 * nLow, vec,
                              reinterpret_cast<uint32_t*>(hyb + kJoint2Off), reinterpret_cast<uint32_t*>(hyb + kSegHistA2Off),
-                             reinterpret_cast<uint32_t*>(hyb + kRowHist2Off), ZeroRanges{}, meta, sqw, nullptr, partial);
+                             reinterpret_cast<uint32_t*>(hyb + kRowHist2Off), ZeroRanges{}, meta, sqw, nullptr, nullptr);
         }
-        reduce(std::true_type{}, reinterpret_cast<uint32_t*>(hyb + kJoint2Off));
         plan_rows(2, kJoint2Off, kSegHistA2Off, kRowHist2Off);
       } else if (!local32) {
         plan_rows(0, 0, kSegHistAOff, kRowHistOff);

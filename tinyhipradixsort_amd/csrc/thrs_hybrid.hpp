@@ -666,13 +666,8 @@ __device__ __forceinline__ void plan_big_prefix(const uint32_t* __restrict__ joi
 // flight at G = 256), the 32 phases meet in LDS, and bucket 256r + t adds its
 // total to joint (which holds the workgroups' logged carries already).
 constexpr int kHistReduceThreads = 1024;
-template <bool SECOND>
 __global__ __launch_bounds__(kHistReduceThreads) void thrs_hist_reduce(const uint32_t* __restrict__ partial,
-                                                                        uint32_t G, uint32_t* __restrict__ joint,
-                                                                        const uint32_t* __restrict__ meta) {
-  if constexpr (SECOND) {
-    if (meta[kMetaRehist] == 0) return;
-  }
+                                                                        uint32_t G, uint32_t* __restrict__ joint) {
   __shared__ uint32_t s_sum[32][kBins + 1];
   const uint32_t t = threadIdx.x, q = t & 31u, p = t >> 5, r = blockIdx.x;
   const uint4* pv = reinterpret_cast<const uint4*>(partial) + (uint64_t)r * 32 + q;
