@@ -295,6 +295,13 @@ int thrs_debug_bucket_mode(const void* temporaryBuffer, int keyType, int valueBy
 int thrs_debug_big_keys(const void* temporaryBuffer, int keyType, int valueBytes, uint32_t n, hipStream_t stream,
                         uint64_t* keys);
 
+/* Diagnostic: synchronises `stream`; *tiles = the tiles of the LAST
+ * keys-only bucket-path sort on `temporaryBuffer` whose top-digit pass read the
+ * key planes with vector loads (whole tiles inside one second-digit region;
+ * 0 when the planes did not run).  Tests use it to prove that branch ran. */
+int thrs_debug_vector_tiles(const void* temporaryBuffer, int keyType, uint32_t n, hipStream_t stream,
+                            uint32_t* tiles);
+
 /* Diagnostic: resident workgroups per CU of the 3-pass path's local bucket
  * sort kernel (4-byte keys), from the runtime's occupancy calculator. */
 int thrs_debug_local_occupancy(void);

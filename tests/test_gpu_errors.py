@@ -258,3 +258,45 @@ def test_stale_big_chunk_entry_is_reported():
     print(res)
     assert res[1]["status"] == -6 and res[1]["word"] == 2 and res[1]["guards"], res
     assert res[0] == dict(status=0, word=0, guards=True, exact=True), res
+
+
+CLAIMS = r"""
+import sys, torch
+sys.path.insert(0, {root!r})
+import tinyhipradixsort_amd as T
+from tinyhipradixsort_amd import testutil as TU
+T.LIB_PATH = {lib!r}
+torch.cuda.set_device(0)
+rs = T.RadixSort([], T.RadixSort.Config(), T.Options(tileClaims="xcd_blocks", path="lsd"))
+n = 1 << 24
+keys = torch.empty(4 * n, dtype=torch.uint8, device="cuda")
+tmp = torch.empty(rs.getTemporaryBufferBytes(n).getTemporaryBufferBytesForSortKeys(), dtype=torch.uint8, device="cuda")
+res = dict(failed=0, timeout=0, other=0, attempts=6)
+for attempt in range(res["attempts"]):
+    TU.fill_keys(0, keys, n, start=attempt * n)
+    try:
+        rs.sortKeys(keys, n, tmp, 0, 8, checked=True)   # ONE pass (8-bit window), XCD-block tile claims
+    except T.ThrsError as e:
+        res["failed"] += 1
+        res["timeout"] += e.status == -5
+        res["other"] += e.status != -5
+    try:
+        T.take_device_error()
+    except T.ThrsError:
+        pass
+print(res)
+"""
+
+
+def test_claim_timeout_reports_lookback_timeout():
+    """a tile-claim wait that gives up on the XCD-block path
+    (thrs_pass_xb's xb_claim) sets the spin bit of the error word, so the
+    caller sees THRS_ERROR_LOOKBACK_TIMEOUT (-5), not THRS_ERROR_DEVICE_CHECK
+    (-6, a clamped run).  One pass (8-bit window) with the XCD-block claims
+    forced, built with THRS_SPIN_MAX=0 (libthrs_spin0.so): every failing sort
+    must report -5."""
+    lib = os.path.join(ROOT, "tinyhipradixsort_amd", "libthrs_spin0.so")
+    assert os.path.exists(lib), "build it first (make)"
+    res = _run(CLAIMS.format(root=ROOT, lib=lib))
+    print(res)
+    assert res["failed"] >= 1 and res["timeout"] == res["failed"] and res["other"] == 0, res

@@ -193,12 +193,15 @@ def test_hybrid_paths_vs_oracle(gpu, kt, desc, geom, seg):
     # only; local-sort geometry: 18432- or 9216-key chunks; u32 keys over the
     # whole key sort 16-bit items in the big geometry unless "big32" -- by two
     # LSD rounds (default, "rank16") or by counting ("count16"), or in 34816-key
-    # chunks ("wide16", the default above 2^30 + 2^26); u32 keys
-    # there travel as u16/u8 planes through the top-digit passes unless
-    # "noplanes" (thrs_options.planes)
+    # chunks ("wide16", the default above 2^30 + 2^26); with both top passes
+    # segmented ("1") the 16-bit local sorts' keys travel as u16/u8 planes
+    # through the top-digit passes (the temporary buffer holds the u8 plane at
+    # every size) unless "noplanes" (thrs_options.planes)
     rs = make_sorter(kt, 0, desc, path="bucket",
                      segmented={"1": "auto", "0": "none", "top": "top_only"}[seg.split("-")[0]], localGeometry=geom,
                      planes="off" if seg.endswith("noplanes") else "auto")
+    want_planes = seg == "1" and geom != "big32"
+    assert rs.pathInfo(1 << 20, 0, 32, False)["planes"] == want_planes
     dists = {
         "uniform": lambda k: k,
         "low20": lambda k: k & np.array(0xFFFFF, k.dtype),        # 16 buckets -> fallback above 295k keys
@@ -223,12 +226,16 @@ def test_hybrid_paths_vs_oracle(gpu, kt, desc, geom, seg):
 
 @pytest.mark.parametrize("desc", [False, True])
 @pytest.mark.parametrize("geom", ["big", "small", "tiny16"])
-def test_hybrid_pairs_vs_oracle(gpu, desc, geom):
-    """sortPairs with u32 keys + u32 values over the whole key takes the hybrid
-    path (single-bucket chunks, positions carried in the local sort's items);
-    stability on ties, the gated LSD fallback, and partial windows (plain LSD)."""
+@pytest.mark.parametrize("kt", [O.U32, O.F32])
+def test_hybrid_pairs_vs_oracle(gpu, kt, desc, geom):
+    """sortPairs with 4-byte keys + u32 values over the whole key takes the
+    hybrid path (single-bucket chunks, positions carried in the local sort's
+    items); stability on ties, the gated LSD fallback, and partial windows
+    (plain LSD).  f32 keys in every geometry too (a forced "tiny16" sends them
+    through thrs_local_pairs<LocTiny>, whose keys are rebuilt from their
+    images unless some key is -0: the "ties" stream holds +-0)."""
     torch = gpu
-    rs = make_sorter(O.U32, 4, desc, path="bucket", localGeometry=geom)  # forced for every size
+    rs = make_sorter(kt, 4, desc, path="bucket", localGeometry=geom)  # forced for every size
     dists = {
         "uniform": lambda k: k,
         "low20": lambda k: k & np.array(0xFFFFF, k.dtype),
@@ -241,10 +248,12 @@ def test_hybrid_pairs_vs_oracle(gpu, desc, geom):
         for n in [1, 100, 18432, 18433, 70001, 300007, 1 << 20]:
             for (s, e) in [(0, 32), (8, 32)]:
                 j += 1
-                keys = f(O.randomize_np(O.U32, O.splitmix64_stream(9191 * j, n)))
+                keys = f(O.randomize_np(kt, O.splitmix64_stream(9191 * j, n)))
+                if kt == O.F32 and name == "ties":                 # +0 and -0 among the ties
+                    keys[3::11] = np.where(np.arange(keys[3::11].shape[0]) % 2, np.uint32(0x80000000), np.uint32(0))
                 vals = np.arange(n, dtype=np.uint32) * np.uint32(2654435761)
-                k, v = gpu_sort(torch, rs, {"keys": keys, "values": vals}, O.U32, 4, s, e)
-                ek, ev = O.lsd_sort(O.U32, keys, vals, s, e, desc)
+                k, v = gpu_sort(torch, rs, {"keys": keys, "values": vals}, kt, 4, s, e)
+                ek, ev = O.lsd_sort(kt, keys, vals, s, e, desc)
                 assert np.array_equal(k, ek), (name, n, s, e)
                 assert np.array_equal(v, ev), (name, n, s, e)
 

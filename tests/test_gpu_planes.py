@@ -1,0 +1,185 @@
+"""GPU parity of the key-plane codecs, element-wise against the oracle.
+
+The bucket path for u32 / f32 keys without values carries each key's image
+through the two top-digit passes as planes (thrs_kernels.hpp kCodecSplit /
+kCodecPlanes: a u16 + u8 plane, then a u16 plane), and the top-digit pass
+reads whole tiles inside one second-digit region with vector loads, which walk
+the keys out of input order.  The headline (C2), C4, u32Large and the
+reference's own timed shape (160M keys, unittest.cpp:490-571) all run these
+codecs, so they are compared here with the oracle's pass-by-pass restatement
+of RadixSort::sort (tinyhipradixsort.hpp:854-944), key for key:
+
+* the DEFAULT path at the sizes where it runs them: u32 keys at 90,000,000 and
+  160,000,000 (4096-key chunks, Loc16Tiny) and 2^28 (9216-key chunks), f32
+  keys at 150,000,000 with raw NaN / Inf / denormal bits and signed zeros,
+  u32 pairs at 160M (LocTiny; pairs carry whole keys);
+* a FORCED bucket path at small n with a distribution that puts the keys in
+  four second-digit regions, so nearly every top-pass tile is a vector tile.
+
+Each planes case asserts pathInfo()['planes'] and that the vector branch ran
+(thrs_debug_vector_tiles, a counter the top-digit pass keeps)."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _sorter(kt, vb, desc, **options):
+    import tinyhipradixsort_amd as T
+    cfg = T.RadixSort.Config()
+    cfg.keyType = T.KeyType(kt)
+    cfg.valueType = T.ValueType.U32
+    cfg.sortOrder = T.SortOrder.Descending if desc else T.SortOrder.Ascending
+    return T.RadixSort([], cfg, T.Options(**options))
+
+
+def _sort_on_gpu(torch, rs, kt, keys, vals=None):
+    """(sorted keys, sorted values, tmp) through the C-ABI; keys/vals are host arrays."""
+    n = keys.shape[0]
+    kd = torch.from_numpy(keys.view(np.uint8)).to("cuda")
+    d = rs.getTemporaryBufferBytes(n)
+    if vals is not None:
+        vd = torch.from_numpy(vals.view(np.uint8)).to("cuda")
+        tmp = torch.empty(d.getTemporaryBufferBytesForSortPairs(), dtype=torch.uint8, device="cuda")
+        rs.sortPairs(kd, vd, n, tmp, 0, 32)
+    else:
+        vd = None
+        tmp = torch.empty(d.getTemporaryBufferBytesForSortKeys(), dtype=torch.uint8, device="cuda")
+        rs.sortKeys(kd, n, tmp, 0, 32)
+    torch.cuda.synchronize()
+    rs.checkDeviceError(tmp)
+    k = kd.cpu().numpy().view(keys.dtype)
+    v = None if vd is None else vd.cpu().numpy().view(vals.dtype)
+    return k, v, tmp
+
+
+def _u32_keys(n, seed):
+    return O.randomize_np(O.U32, O.splitmix64_stream(seed, n))
+
+
+def _f32_raw_keys(n, seed):
+    """Uniform raw bit patterns as f32 keys (NaNs ~1/256, denormals ~1/256, both
+    signs), plus +-Inf, +-NaN payloads and 600 signed zeros (under the zero
+    log's 1024: the planes keep running, mode 0)."""
+    k = _u32_keys(n, seed)
+    k[k & np.uint32(0x7FFFFFFF) == 0] = 1                     # the stream's own zeros, if any
+    rng = np.random.default_rng(seed)
+    specials = np.array([0x7F800000, 0xFF800000, 0x7FC00000, 0xFFC00000, 0x7F800001, 0xFFFFFFFF,
+                         0x00000001, 0x80000001, 0x007FFFFF, 0x807FFFFF], np.uint32)
+    pos = rng.choice(n, 4000, replace=False)
+    k[pos[:3400]] = specials[np.arange(3400) % specials.shape[0]]
+    k[pos[3400:]] = np.where(np.arange(600) % 3 == 0, np.uint32(0x80000000), np.uint32(0))
+    return k                                                   # raw f32 bits, as the oracle takes them
+
+
+def _expect_planes(rs, T, tmp, kt, n, min_frac):
+    assert rs.pathInfo(n, 0, 32, False)["planes"]
+    assert rs.debugBucketMode(tmp, n, False)[0] == 0           # mode 0: the planes ran
+    tiles = T.debug_vector_tiles(tmp, kt, n)
+    total = -(-n // 32768)
+    print(f"vector tiles {tiles} of ~{total}")
+    assert tiles >= min_frac * total, (tiles, total)
+
+
+@pytest.mark.large
+@pytest.mark.parametrize("desc", [False, True])
+@pytest.mark.parametrize("n", [90_000_000, 160_000_000, 1 << 28])
+def test_u32_keys_default_path_planes_vs_oracle(gpu, n, desc):
+    """u32 keys-only on the DEFAULT path at the sizes where it takes the
+    planes: 4096-key chunks (<= 3 x 2^26 keys; 160M is the reference's own
+    bench size, unittest.cpp:490-571) and 9216-key chunks (2^28).  Uniform
+    keys: every second-digit region spans many tiles, so most top-pass tiles
+    take the vector loads."""
+    import tinyhipradixsort_amd as T
+    torch = gpu
+    keys = _u32_keys(n, 6100 + int(desc))
+    rs = _sorter(O.U32, 0, desc)
+    info = rs.pathInfo(n, 0, 32, False)
+    assert (info["path"], info["local"]) == ("bucket", "thrs_local16")
+    assert info["local_cap"] == (4096 if n <= 3 << 26 else 9216)
+    k, _, tmp = _sort_on_gpu(torch, rs, O.U32, keys)
+    _expect_planes(rs, T, tmp, O.U32, n, 0.75)
+    ek, _ = O.lsd_sort(O.U32, keys, None, 0, 32, desc)
+    assert np.array_equal(k, ek)
+
+
+@pytest.mark.large
+@pytest.mark.parametrize("desc", [False, True])
+def test_f32_keys_default_path_planes_vs_oracle(gpu, desc):
+    """f32 keys-only at 150M on the default path (planes; the squeeze may go
+    on): raw NaN / Inf / denormal bits and 600 signed zeros, whose signs the
+    zero log restores in input order (getKeyBits maps -0 to +0,
+    kernel.cu:46-69).  Bit-exact against the oracle."""
+    import tinyhipradixsort_amd as T
+    torch = gpu
+    n = 150_000_000
+    keys = _f32_raw_keys(n, 6200 + int(desc))
+    rs = _sorter(O.F32, 0, desc)
+    k, _, tmp = _sort_on_gpu(torch, rs, O.F32, keys)
+    _expect_planes(rs, T, tmp, O.F32, n, 0.75)
+    ek, _ = O.lsd_sort(O.F32, keys, None, 0, 32, desc)
+    assert np.array_equal(k, ek)
+
+
+@pytest.mark.large
+@pytest.mark.parametrize("desc", [False, True])
+def test_u32_pairs_default_path_vs_oracle(gpu, desc):
+    """u32 keys + u32 values at the reference's bench size, 160M (the default
+    bucket path with 4096-key chunks, LocTiny): keys and values bit-exact
+    against the oracle, so the stable order of equal keys is checked too."""
+    torch = gpu
+    n = 160_000_000
+    keys = _u32_keys(n, 6300 + int(desc))
+    keys[::7] &= np.uint32(0xFFFF00FF)                         # ties: stability visible
+    vals = np.arange(n, dtype=np.uint32)
+    rs = _sorter(O.U32, 4, desc)
+    info = rs.pathInfo(n, 0, 32, True)
+    assert (info["path"], info["local"], info["local_cap"]) == ("bucket", "thrs_local_pairs", 4096)
+    k, v, _ = _sort_on_gpu(torch, rs, O.U32, keys, vals)
+    ek, ev = O.lsd_sort(O.U32, keys, vals, 0, 32, desc)
+    assert np.array_equal(k, ek)
+    assert np.array_equal(v, ev)
+
+
+@pytest.mark.parametrize("desc", [False, True])
+@pytest.mark.parametrize("kt", [O.U32, O.F32])
+@pytest.mark.parametrize("geom", ["tiny16", "small", "big"])
+@pytest.mark.parametrize("n", [1 << 20, 3 * (1 << 20) + 12345])
+def test_forced_bucket_vector_tiles_vs_oracle(gpu, n, geom, kt, desc):
+    """A forced bucket path at sizes the oracle finishes at once, with the
+    keys in four second-digit regions (raw bits 18-23 cleared): every region
+    spans 8+ tiles, so nearly every top-pass tile takes the vector loads, and
+    the 1024+ buckets stay within the local capacity (mode 0: planes on).
+    f32 adds signed zeros and specials."""
+    import tinyhipradixsort_amd as T
+    torch = gpu
+    seed = 6400 + n % 97 + 3 * int(desc) + 7 * kt
+    keys = _u32_keys(n, seed) if kt == O.U32 else _f32_raw_keys(n, seed)
+    keys &= np.uint32(0xFF03FFFF)
+    rs = _sorter(kt, 0, desc, path="bucket", localGeometry=geom)
+    k, _, tmp = _sort_on_gpu(torch, rs, kt, keys)
+    _expect_planes(rs, T, tmp, kt, n, 0.5)
+    ek, _ = O.lsd_sort(kt, keys, None, 0, 32, desc)
+    assert np.array_equal(k, ek)
+
+
+@pytest.mark.parametrize("desc", [False, True])
+@pytest.mark.parametrize("kt", [O.U32, O.F32])
+def test_forced_bucket_planes_vs_noplanes(gpu, kt, desc):
+    """The same forced-bucket sorts with the planes on and off
+    (thrs_options.planes): both equal the oracle, and only the first takes the
+    vector tiles."""
+    import tinyhipradixsort_amd as T
+    torch = gpu
+    n = 1 << 21
+    keys = _u32_keys(n, 6500 + kt + int(desc)) & np.uint32(0xFF07FFFF)
+    ek, _ = O.lsd_sort(kt, keys, None, 0, 32, desc)
+    for planes in ("auto", "off"):
+        rs = _sorter(kt, 0, desc, path="bucket", planes=planes)
+        k, _, tmp = _sort_on_gpu(torch, rs, kt, keys)
+        assert np.array_equal(k, ek), planes
+        assert rs.pathInfo(n, 0, 32, False)["planes"] == (planes == "auto")
+        tiles = T.debug_vector_tiles(tmp, kt, n)
+        assert (tiles > 0) == (planes == "auto"), (planes, tiles)

@@ -104,6 +104,8 @@ def lib() -> ctypes.CDLL:
         L.thrs_get_path_info.restype = i32
         L.thrs_debug_bucket_mode.argtypes = [vp, i32, i32, u32, vp, ctypes.POINTER(i32), ctypes.POINTER(i32)]
         L.thrs_debug_bucket_mode.restype = i32
+        L.thrs_debug_vector_tiles.argtypes = [vp, i32, u32, vp, ctypes.POINTER(u32)]
+        L.thrs_debug_vector_tiles.restype = i32
         for f in ("thrs_profile_enable", "thrs_profile_read", "thrs_profile_read_kind",
                   "thrs_get_temporary_buffer_bytes", "thrs_sort_keys", "thrs_sort_pairs", "thrs_sort_keys_ex",
                   "thrs_sort_pairs_ex", "thrs_check_device_error", "thrs_accumulate_device_error",
@@ -482,6 +484,16 @@ def debug_big_keys(temporaryBuffer, keyType: int, valueBytes: int, n: int, strea
     out = ctypes.c_uint64()
     _check(lib().thrs_debug_big_keys(_ptr(temporaryBuffer), int(keyType), int(valueBytes), int(n),
                                      _stream(stream), ctypes.byref(out)))
+    return int(out.value)
+
+
+def debug_vector_tiles(temporaryBuffer, keyType: int, n: int, stream=None) -> int:
+    """Tiles of the last keys-only bucket-path sort on this buffer whose
+    top-digit pass took the planes codec's vector loads
+    (thrs_debug_vector_tiles; synchronising)."""
+    out = ctypes.c_uint32()
+    _check(lib().thrs_debug_vector_tiles(_ptr(temporaryBuffer), int(keyType), int(n), _stream(stream),
+                                         ctypes.byref(out)))
     return int(out.value)
 
 

@@ -403,6 +403,18 @@ THRS_API int thrs_debug_big_keys(const void* tmp, int keyType, int valueBytes, u
   return THRS_SUCCESS;
 }
 
+THRS_API int thrs_debug_vector_tiles(const void* tmp, int keyType, uint32_t n, hipStream_t stream, uint32_t* tiles) {
+  if (!tmp || !tiles || !valid_key(keyType)) return THRS_ERROR_INVALID_VALUE;
+  const Plan plan = make_plan(keyType, 0, n);
+  uint32_t v = 0;
+  if (hipMemcpyAsync(&v, static_cast<const char*>(tmp) + plan.hybridOff + kSegInfoOff + kSegVecWord * 4, 4,
+                     hipMemcpyDeviceToHost, stream) != hipSuccess ||
+      hipStreamSynchronize(stream) != hipSuccess)
+    return THRS_ERROR_HIP;
+  *tiles = v;
+  return THRS_SUCCESS;
+}
+
 THRS_API int thrs_check_device_error(void* tmp, hipStream_t stream) {
   if (!tmp) return THRS_ERROR_INVALID_VALUE;
   uint32_t err = 0;

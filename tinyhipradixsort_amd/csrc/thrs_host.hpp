@@ -162,14 +162,13 @@ inline Plan make_plan(int keyType, int valueBytesOrZero, uint32_t n) {
   p.scratchBytes = p.bigHistOff + round_up(p.bigMax * (p.kb - 2) * kBins * 4, kAlign);
   // the u8 plane of the planes codecs (thrs_kernels.hpp kCodecSplit): the u16
   // planes fill keyOut, which is all a sortKeys caller must allocate
-  // (getTemporaryBufferBytesForSortKeys = pSumBuffer + keyOutBuffer).  Only
-  // where the default takes the bucket path with planes (u32 / f32 keys-only,
-  // n in [kBucketMinKeysU32 (u32) / kBucketMinKeys4 (f32), 2^31 + 2^25]); a
-  // forced bucket path elsewhere runs
-  // without them.
+  // (getTemporaryBufferBytesForSortKeys = pSumBuffer + keyOutBuffer).  For
+  // u32 / f32 keys-only at every n up to 2^31 + 2^25 (the bucket path's
+  // range): the default takes it from kBucketMinKeysU32 / kBucketMinKeys4, and
+  // a bucket path forced below that carries the planes too, so the codecs the
+  // headline runs are tested element-wise at sizes the oracle finishes.
   p.hiPlaneOff = p.scratchBytes;
   if ((keyType == THRS_KEY_U32 || keyType == THRS_KEY_F32) && valueBytesOrZero == 0 &&
-      (uint64_t)n >= (keyType == THRS_KEY_U32 ? kBucketMinKeysU32 : kBucketMinKeys4) &&
       (uint64_t)n <= (1ull << 31) + (1ull << 25))
     p.scratchBytes += round_up(n, kAlign);
   return p;
@@ -342,7 +341,7 @@ PathSel select_path(uint32_t n, int startBits, int nPass, const thrs_options& op
   const bool useXb = opt.tileClaims == THRS_CLAIMS_XCD_BLOCKS ? true
                      : opt.tileClaims == THRS_CLAIMS_TICKET ? false
                                                             : (sizeof(U) == 4 && VB == 0 && n >= (1u << 29));
-  PathSel P;
+  PathSel P{};
   P.bucket = bucket;
   P.fullWindow = fullWindow;
   P.smallLocal = smallLocal;

@@ -817,13 +817,18 @@ __global__ __launch_bounds__(kPlanRowThreads) void thrs_plan_rows(
       return top ? s_b2[32 * sg] : hj_seg_pos(n, histGrid, (uint32_t)sg);
     };
     uint32_t tiles = 0;
-    info[kSegAlignWord] = top ? 1u : 0u;  // the top-digit pass's tiles are aligned (thrs_pass_seg_body)
+    // the top-digit pass's tiles are aligned when it reads the key planes
+    // (their vector loads, thrs_pass_seg_body); other codecs count tiles from
+    // the segment start (aligned tiles measured slower, docs/EXPERIMENTS.md row 85)
+    const bool align = top && planes;
+    info[kSegAlignWord] = align ? 1u : 0u;
+    info[kSegVecWord] = 0;  // vector-load tiles of the top-digit pass (diagnostics)
     for (int sg = 0; sg <= kSegs; ++sg) {
       const uint32_t pos = pos_of(sg);
       info[sg] = pos;
       info[kSegs + 1 + sg] = tiles;
       if (sg < kSegs) {
-        const uint32_t nT = seg_tiles(pos, pos_of(sg + 1), tileKeys, top);
+        const uint32_t nT = seg_tiles(pos, pos_of(sg + 1), tileKeys, align);
         tiles += (nT + kGroup - 1) / kGroup * kGroup;
         info[64 + sg] = 0;  // ticket (own cache line)
       }
@@ -986,19 +991,25 @@ __global__ __launch_bounds__(kPlanThreads) void thrs_plan(const uint32_t* __rest
   // second-digit pass (position ranges)
   if (tid == 0 || tid == 64) {
     const bool top = tid == 0;
+    constexpr bool planes = false;  // the 32-bit local sort's passes move keys
     uint32_t* info = top ? segInfo : segInfoA;
     auto pos_of = [&](int sg) -> uint32_t {
       if (sg >= kSegs) return n;
       return top ? s_b2[32 * sg] : hj_seg_pos(n, histGrid, (uint32_t)sg);
     };
     uint32_t tiles = 0;
-    info[kSegAlignWord] = top ? 1u : 0u;  // the top-digit pass's tiles are aligned (thrs_pass_seg_body)
+    // the top-digit pass's tiles are aligned when it reads the key planes
+    // (their vector loads, thrs_pass_seg_body); other codecs count tiles from
+    // the segment start (aligned tiles measured slower, docs/EXPERIMENTS.md row 85)
+    const bool align = top && planes;
+    info[kSegAlignWord] = align ? 1u : 0u;
+    info[kSegVecWord] = 0;  // vector-load tiles of the top-digit pass (diagnostics)
     for (int sg = 0; sg <= kSegs; ++sg) {
       const uint32_t pos = pos_of(sg);
       info[sg] = pos;
       info[kSegs + 1 + sg] = tiles;
       if (sg < kSegs) {
-        const uint32_t nT = seg_tiles(pos, pos_of(sg + 1), tileKeys, top);
+        const uint32_t nT = seg_tiles(pos, pos_of(sg + 1), tileKeys, align);
         tiles += (nT + kGroup - 1) / kGroup * kGroup;
         info[64 + sg] = 0;  // ticket (own cache line)
       }

@@ -83,22 +83,27 @@ template <> struct KeyTraits<3> {  // F64
 // 16-bit buckets then take one more varying bit.  The reference's own float
 // generator clears the lowest exponent bit of every key (unittest.cpp:103,
 // 108), which is such a bit: without the squeeze half the buckets are empty.
+// (kernel-argument structs: every field has a default initialiser and there
+// is no implicit padding, so a struct the host fills field by field never
+// carries indeterminate bytes; tests/cpp/struct_init.cpp checks both)
 template <typename U, bool SQ = false> struct KeyMap {
-  U mask;
-  U lo;
-  uint32_t sh;
+  U mask = 0;
+  U lo = 0;
+  uint32_t sh = 0;
+  uint32_t pad = 0;
 };
 template <typename U> struct KeyMap<U, true> {
-  U mask;
-  U lo;
-  uint32_t sh;
-  U hiM[2], loM[2], cst[2];
+  U mask = 0;
+  U lo = 0;
+  uint32_t sh = 0;
+  uint32_t pad = 0;
+  U hiM[2] = {}, loM[2] = {}, cst[2] = {};
 };
 // the squeeze as thrs_plan_rows (or the sample, thrs_squeeze_sample) writes
 // it: on, and per half the masks and the dropped bit's value (cst)
 struct SqueezeWords {
-  uint32_t on, pad;
-  uint64_t hiM[2], loM[2], cst[2];
+  uint32_t on = 0, pad = 0;
+  uint64_t hiM[2] = {}, loM[2] = {}, cst[2] = {};
 };
 template <int KT> constexpr bool kSqueezable = KT == 2 || KT == 3;  // float keys
 template <typename U> __device__ __forceinline__ KeyMap<U, true> with_squeeze(const KeyMap<U>& m,
@@ -495,10 +500,10 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist(const typename KeyTrai
 // device atomic per bin and workgroup.
 constexpr int kMaxHistTargets = 16;
 struct HistTargets {
-  uint64_t off[kMaxHistTargets];
-  uint64_t mask[kMaxHistTargets];
-  uint64_t value[kMaxHistTargets];
-  uint32_t n[kMaxHistTargets];
+  uint64_t off[kMaxHistTargets] = {};
+  uint64_t mask[kMaxHistTargets] = {};
+  uint64_t value[kMaxHistTargets] = {};
+  uint32_t n[kMaxHistTargets] = {};
 };
 template <typename U>
 __global__ __launch_bounds__(kHistThreads) void thrs_digit_hist(const U* __restrict__ keys, HistTargets tg,
@@ -597,11 +602,11 @@ constexpr uint32_t kArrival = 1u << 20;
 // a run reserved past the output end was clamped
 constexpr uint32_t kErrSpin = 1u, kErrRunClamped = 2u;
 template <typename ST> struct GroupTables {
-  uint32_t* ga;      // [nGroups][256] count | arrivals << 20   (this pass)
-  ST* gp;            // [nGroups][256] Status<ST>::pre(inclusive prefix)
+  uint32_t* ga = nullptr;  // [nGroups][256] count | arrivals << 20   (this pass)
+  ST* gp = nullptr;        // [nGroups][256] Status<ST>::pre(inclusive prefix)
   uint32_t* gaNext = nullptr;  // next pass's tables, cleared by each group's last tile
   ST* gpNext = nullptr;
-  uint32_t nTiles;    // end of this tile's chain (tile ids)
+  uint32_t nTiles = 0;  // end of this tile's chain (tile ids)
   uint32_t gmin = 0;  // first group of this tile's chain (segmented passes)
 };
 
@@ -801,7 +806,7 @@ struct GroupWalk {
 #endif
       if (stall && walking()) {
         if (++spins > kSpinMax) {  // bounded spin: never hang the GPU
-          atomicOr(errFlag, 1u);
+          atomicOr(errFlag, kErrSpin);
           break;
         }
 #if THRS_WALK_BACKOFF
@@ -1278,7 +1283,7 @@ __device__ __forceinline__ void pass_tile(
         if (done) break;
         if (stall) {
           if (++spins > kSpinMax) {  // bounded spin: never hang the GPU
-            atomicOr(errFlag, 1u);
+            atomicOr(errFlag, kErrSpin);
             break;
           }
           __builtin_amdgcn_s_sleep(1);
@@ -1500,7 +1505,7 @@ __device__ __forceinline__ uint32_t xb_claim(uint32_t* claimState, uint32_t stri
   uint32_t e = load_agent(&tab[j]);
   for (uint32_t spin = 0; e == 0; ++spin) {
     if (spin >= kSpinMax) {  // bounded: never hang the GPU
-      atomicOr(errFlag, 2u);
+      atomicOr(errFlag, kErrSpin);  // a claim spin that gave up: THRS_ERROR_LOOKBACK_TIMEOUT
       return kXbDone;
     }
     __builtin_amdgcn_s_sleep(1);
@@ -1586,6 +1591,9 @@ constexpr int kSegs = 8;
 // planes codec's vector loads need a multiple of 4; the first tile (and the
 // last) may be partial.  Otherwise tiles are counted from pos.
 constexpr int kSegAlignWord = 32;
+// segInfo[kSegVecWord]: tiles of the top-digit pass that took the planes
+// codec's vector loads (zeroed by the plan; thrs_debug_vector_tiles)
+constexpr int kSegVecWord = 96;
 __host__ __device__ __forceinline__ uint64_t seg_tile_base(uint32_t pos, uint32_t T, bool align) {
   return align ? (uint64_t)pos / T * T : (uint64_t)pos;
 }
@@ -1625,6 +1633,7 @@ __device__ __forceinline__ void thrs_pass_seg_body(
   const uint32_t home = xcc_id() & (kSegs - 1);
   with_map<KT>(km, sq, [&](auto kmx) __attribute__((always_inline)) {
   uint32_t done = 0;  // thread 0: segments found exhausted
+  uint32_t nVec = 0;  // thread 0: vector-load tiles (kVec)
   U k[G::KPT];
   VW v[VB ? G::KPT : 1];
   for (;;) {
@@ -1657,7 +1666,10 @@ __device__ __forceinline__ void thrs_pass_seg_body(
     for (uint32_t i = tid; i < (uint32_t)(G::WAVES * kBins); i += G::THREADS) s_cnt[i] = 0;
     lds_barrier();
     const uint32_t seg = s_misc[8], t = s_misc[9];
-    if (seg >= (uint32_t)kSegs) break;
+    if (seg >= (uint32_t)kSegs) {
+      if (kVec && tid == 0 && nVec) atomicAdd(&segInfo[kSegVecWord], nVec);  // one add per workgroup
+      break;
+    }
     const uint32_t segStart = segPos[seg], segEnd = segPos[seg + 1];
     const uint64_t t0 = seg_tile_base(segStart, T, salign) + (uint64_t)t * T;
     const uint64_t keyStart = max((uint64_t)segStart, t0);
@@ -1672,6 +1684,7 @@ __device__ __forceinline__ void thrs_pass_seg_body(
         const uint32_t b = lane < kBins / kSegs - 1 ? s_b2[(kBins / kSegs) * seg + 1 + lane] : 0u;
         vec = __ballot(lane < kBins / kSegs - 1 && b > keyStart && (uint64_t)b < keyStart + T) == 0;
       }
+      nVec += vec ? 1u : 0u;
     }
     const uint32_t chain = segTiles[seg];
     GroupTables<ST> g = grp;
@@ -1706,8 +1719,8 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
 // Zeroing of up to three 16-byte-aligned ranges in one launch (the scratch
 // header and look-back tables at the start of every sort).
 struct ZeroRanges {
-  char* ptr[3];
-  uint64_t words[3];  // 16-byte words
+  char* ptr[3] = {};
+  uint64_t words[3] = {};  // 16-byte words
 };
 __global__ __launch_bounds__(256) void thrs_zero_ranges(ZeroRanges z) {
   const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x, stride = (uint64_t)gridDim.x * 256;
