@@ -30,9 +30,11 @@ def main():
     ap.add_argument("--workload", default="c2")
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--nocheck", default="")
+    ap.add_argument("--n", type=int, default=None, help="keys (default: the workload's)")
     ap.add_argument("libs", nargs="+")
     a = ap.parse_args()
     kt, vb, n, dist, _ = WORKLOADS[a.workload]
+    n = a.n or n
     kb = 4 if kt in (0, 2) else 8
     libs = []
     for name in a.libs:

@@ -8,6 +8,7 @@
 #   bench=WORKLOAD[,ARGS]   bench.py --workload WORKLOAD ARGS (commas -> spaces)
 #                           -> gpurun_out/bench_WORKLOAD.json
 #   prof=TAG,WORKLOAD       scripts/profile.sh TAG WORKLOAD (kernel trace + PMC)
+#   ab=WORKLOAD,LIB,...     scripts/ab_libs.py A/B of libthrs builds (main | exp/variants names)
 #   cpp                     the C++ UTEST port (tests/cpp/unittest_thrs)
 #
 # e.g. gpurun -- bash scripts/gpu.sh tests smoke bench=c2 bench=c2_sorted,--steps,5
@@ -63,6 +64,17 @@ for p in glob.glob(f"gpurun_out/stats_{wl}/**/*kernel_stats.csv", recursive=True
     for r in csv.DictReader(open(p)):
         print(f"{r.get('Name','')[:70]:70s} calls={r.get('Calls')} avg_ns={float(r.get('AverageNs', 0)):.0f}")
 PY
+      ;;
+    ab)
+      # ab=WORKLOAD,libA,libB,...: interleaved A/B of libthrs builds (scripts/ab_libs.py)
+      # (WORKLOAD may carry a key count: c2:268435456)
+      wl=${arg%%,*}
+      libs=$(echo "${arg#*,}" | tr ',' ' ')
+      nopt=""
+      [[ "$wl" == *:* ]] && { nopt="--n ${wl#*:}"; wl=${wl%%:*}; }
+      timeout -k 10 600 python -u scripts/ab_libs.py --workload $wl $nopt --rounds 6 $libs > gpurun_out/ab_$wl${nopt:+_n}.txt 2>&1 \
+        || { echo "AB $wl FAILED"; tail -20 gpurun_out/ab_$wl.txt; exit 1; }
+      cat gpurun_out/ab_$wl${nopt:+_n}.txt
       ;;
     cpp)
       timeout -k 10 600 tests/cpp/unittest_thrs > gpurun_out/cpp_tests.txt 2>&1 \

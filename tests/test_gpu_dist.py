@@ -27,6 +27,10 @@ NP_KEY = {O.U32: np.uint32, O.U64: np.uint64, O.F32: np.uint32, O.F64: np.uint64
 @pytest.mark.parametrize("kt,vb,desc,bit,n", [
     (O.U32, 0, False, 24, 100003), (O.U32, 4, False, 0, 70001), (O.F32, 4, True, 24, 65536 + 3),
     (O.U64, 8, False, 56, 50000), (O.F64, 16, False, 40, 33333), (O.U32, 4, False, 8, 1),
+    # digits at bit 8 and above take the segmented pass over the bucket
+    # histogram's position segments (thrs_partition_plan): many tiles per segment
+    (O.U32, 0, False, 24, (1 << 24) + 7), (O.U64, 8, True, 56, (1 << 22) + 5), (O.U32, 4, False, 16, 3 << 20),
+    (O.F32, 0, True, 24, 1 << 23), (O.F64, 8, False, 8, (1 << 21) + 1),
 ])
 def test_partition_pass_vs_oracle(gpu, kt, vb, desc, bit, n):
     import tinyhipradixsort_amd as T

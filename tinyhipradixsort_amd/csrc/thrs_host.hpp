@@ -433,6 +433,11 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                           : opt.rank == THRS_RANK_BALLOT ? false
                                                          : probe_rank_mode(stream) != 0;
   uint32_t* sticky = sticky_dev(stream);
+  // Partition mode by a digit at bit 8 or above (thrs_partition_pass, the
+  // multi-GPU exchange): the bucket histogram in segRows mode gives the digit's
+  // counts per position segment, and one segmented pass (thrs_pass_seg, keys
+  // codec, as the bucket path's second-digit pass) moves the keys.
+  const bool segPart = counts != nullptr && startBits >= 8 && opt.segmented != THRS_SEG_NONE;
 
   // ---- kernels and their LDS opt-ins, before anything is enqueued
   const size_t lds = G::LDS_BYTES;
@@ -455,7 +460,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   if (allow_lds(thrs_hist<KT>, histLds) != hipSuccess || allow_lds(kernel, lds) != hipSuccess ||
       allow_lds(kernelXb, lds) != hipSuccess || allow_lds(kernelBig, lds) != hipSuccess)
     return THRS_ERROR_HIP;
-  if (bucket) {
+  if (bucket || segPart) {
     if (allow_lds(thrs_hist_joint<KT>, kJointLds) != hipSuccess || allow_lds(sk, lds) != hipSuccess ||
         (squeeze && allow_lds(thrs_hist_joint<KT, true>, kJointLds) != hipSuccess))
       return THRS_ERROR_HIP;
@@ -500,7 +505,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   const uint32_t gridBig = bucket ? persistent_grid(kernelBig) : 1u;
   const uint32_t grid = useXb ? gridXb : (uint32_t)plan.nTiles;
   int segPerCU = 0;
-  if (bucket &&
+  if ((bucket || segPart) &&
       (hipOccupancyMaxActiveBlocksPerMultiprocessor(&segPerCU, sk, G::THREADS, lds) != hipSuccess || segPerCU < 1))
     segPerCU = 1;
 
@@ -518,7 +523,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   {
     const uint64_t set0 = kHeaderBytes, set1 = kHeaderBytes + plan.setBytes;
     ZeroRanges z{};
-    if (bucket) {
+    if (bucket || segPart) {
       z.ptr[0] = scratch;  // header
       z.words[0] = kHeaderBytes / 16;
       z.ptr[1] = scratch + set1 + plan.setBytes;  // claim areas, bucket histogram, meta
@@ -565,7 +570,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
         hipLaunchKernelGGL(thrs_hist_joint<KT>, dim3(hgrid), dim3(kHistThreads), kJointLds, stream,
                          static_cast<const U*>(keys), n, km, startBits + 8 * nLow, vec, joint,
                          reinterpret_cast<uint32_t*>(hyb + kSegHistAOff), reinterpret_cast<uint32_t*>(hyb + kRowHistOff),
-                         tables, meta, sample, zeroLog, partial);
+                         tables, meta, sample, zeroLog, partial, 0);
       }
       if (partial) {
         ProfScope prof(stream, 0, THRS_PK_HIST_REDUCE, (uint64_t)hgrid * kJointWords * 4);
@@ -598,7 +603,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
           hipLaunchKernelGGL((thrs_hist_joint<KT, true>), dim3(hgrid), dim3(kHistThreads), kJointLds, stream,
                              static_cast<const U*>(keys), n, km, startBits + 8 * nLow, vec,
                              reinterpret_cast<uint32_t*>(hyb + kJoint2Off), reinterpret_cast<uint32_t*>(hyb + kSegHistA2Off),
-                             reinterpret_cast<uint32_t*>(hyb + kRowHist2Off), ZeroRanges{}, meta, sqw, nullptr, nullptr);
+                             reinterpret_cast<uint32_t*>(hyb + kRowHist2Off), ZeroRanges{}, meta, sqw, nullptr, nullptr, 0);
         }
         plan_rows(2, kJoint2Off, kSegHistA2Off, kRowHist2Off);
       } else if (!local32) {
@@ -613,6 +618,19 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                            reinterpret_cast<uint32_t*>(hyb + kSegInfoAOff), reinterpret_cast<uint32_t*>(hyb + kSegBaseAOff),
                            reinterpret_cast<uint32_t*>(hyb + kBigBOff));
       }
+    } else if (segPart) {
+      {
+        ProfScope prof(stream, 0, THRS_PK_HIST_JOINT, keyBytes);
+        hipLaunchKernelGGL(thrs_hist_joint<KT>, dim3(hgrid), dim3(kHistThreads), kJointLds, stream,
+                           static_cast<const U*>(keys), n, km, startBits - 8, vec, nullptr,
+                           reinterpret_cast<uint32_t*>(hyb + kSegHistAOff), reinterpret_cast<uint32_t*>(hyb + kRowHistOff),
+                           tables, meta, nullptr, nullptr, nullptr, 1);
+      }
+      ProfScope prof(stream, 0, THRS_PK_PLAN, 3 * kBins * 4);
+      hipLaunchKernelGGL(thrs_partition_plan, dim3(1), dim3(kBins), 0, stream,
+                         reinterpret_cast<const uint32_t*>(hyb + kRowHistOff),
+                         reinterpret_cast<const uint32_t*>(hyb + kSegHistAOff), n, (uint32_t)hgrid, segTileKeys, counts,
+                         reinterpret_cast<uint32_t*>(hyb + kSegInfoAOff), reinterpret_cast<uint32_t*>(hyb + kSegBaseAOff));
     } else {
       {
         ProfScope prof(stream, 0, THRS_PK_HIST, keyBytes);
@@ -622,7 +640,8 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
       ProfScope prof(stream, 0, THRS_PK_SCAN, 2 * (uint64_t)nPass * kBins * 4);
       hipLaunchKernelGGL(thrs_scan, dim3(1), dim3(kThreads), 0, stream, hist, base, nPass);
     }
-    if (counts && hipMemcpyAsync(counts, hist, kBins * sizeof(uint32_t), hipMemcpyDeviceToDevice, stream) != hipSuccess)
+    if (counts && !segPart &&
+        hipMemcpyAsync(counts, hist, kBins * sizeof(uint32_t), hipMemcpyDeviceToDevice, stream) != hipSuccess)
       return THRS_ERROR_HIP;
   }
 
@@ -646,6 +665,16 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     return hipGetLastError() == hipSuccess ? THRS_SUCCESS : THRS_ERROR_HIP;
   };
 
+  if (segPart) {  // the one pass: keys (and values) to the caller's output buffers
+    ProfScope prof(stream, 1, THRS_PK_PASS_SEG, moveBytes);
+    hipLaunchKernelGGL(sk, dim3((uint32_t)segPerCU * cu_count()), dim3(G::THREADS), lds, stream,
+                       static_cast<const U*>(keys), keyOut, static_cast<const VW*>(vals), valOut, km, startBits,
+                       reinterpret_cast<uint32_t*>(hyb + kSegInfoAOff), reinterpret_cast<const uint32_t*>(hyb + kSegBaseAOff),
+                       status[0], err, grp[0], nullptr, 0u, nullptr,
+                       g_stamps ? g_stamps : nullptr, nullptr, nullptr);
+    if (hipGetLastError() != hipSuccess) return THRS_ERROR_HIP;
+    return publish_error();
+  }
   if (!bucket) {
     U* kin = static_cast<U*>(keys);
     U* kout = keyOut;

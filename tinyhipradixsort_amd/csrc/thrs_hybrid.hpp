@@ -142,6 +142,9 @@ __device__ __attribute__((noinline)) void hist_log_zeros(const uint4* __restrict
   }
 }
 
+// segRows (thrs_partition_pass): segHist gets the position segments' counts of
+// the bucket's TOP byte (its row) instead of its low byte, and joint may be
+// null (no bucket totals: nothing is flushed).
 // Float keys (the squeeze, KeyMap<U, true>): the map is sq's when sq->on.
 // First histogram (SECOND = false): sq = the sample's guess
 // (thrs_squeeze_sample); every key of a squeezed half is checked to carry the
@@ -159,7 +162,7 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
                                                                 ZeroRanges tables, uint32_t* __restrict__ meta,
                                                                 const SqueezeWords* __restrict__ sq,
                                                                 uint32_t* __restrict__ zeroLog,
-                                                                uint32_t* __restrict__ partial) {
+                                                                uint32_t* __restrict__ partial, int segRows) {
   using U = typename KeyTraits<KT>::U;
   if constexpr (SECOND) {
     if (meta[kMetaRehist] == 0) return;
@@ -242,8 +245,8 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
       if (slot < kCarryLog) {
         s_log[slot] = b;
       } else {
-        atomicAdd(&joint[b], 0x8000u);
-        atomicAdd(&segH[b & 255u], 0x8000u);
+        if (joint) atomicAdd(&joint[b], 0x8000u);
+        atomicAdd(&segH[segRows ? b >> 8 : b & 255u], 0x8000u);
         atomicAdd(&rowHist[b >> 8], 0x8000u);
       }
     }
@@ -379,8 +382,8 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
       first = first && !(x == b && u < t);
     }
     if (first) {
-      atomicAdd(&joint[b], mult * 0x8000u);
-      atomicAdd(&segH[b & 255u], mult * 0x8000u);
+      if (joint) atomicAdd(&joint[b], mult * 0x8000u);
+      atomicAdd(&segH[segRows ? b >> 8 : b & 255u], mult * 0x8000u);
       atomicAdd(&rowHist[b >> 8], mult * 0x8000u);
     }
   }
@@ -395,7 +398,7 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
     uint4* pv = reinterpret_cast<uint4*>(partial + (uint64_t)blockIdx.x * kJointWords);
     const uint4* sv = reinterpret_cast<const uint4*>(s_joint);
     for (uint32_t i = tid; i < kJointWords / 4; i += kHistThreads) pv[i] = sv[i];
-  } else {
+  } else if (joint) {
     for (uint32_t wi = tid; wi < kJointWords; wi += kHistThreads) {
       const uint32_t x = s_joint[wi];
       if (x)
@@ -405,7 +408,7 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
   }
   // the range's second-digit counts (column sums; lanes d, d+1 share a word)
   static_assert(kHistThreads == 4 * kBins, "four top-digit quarters per second digit");
-  {
+  if (!segRows) {
     const uint32_t d = tid & (kBins - 1), top0 = (tid >> 8) * 64;
     uint32_t c = 0;
 #pragma unroll 8
@@ -427,10 +430,13 @@ __global__ __launch_bounds__(kHistThreads) void thrs_hist_joint(const typename K
     }
     c += __shfl_xor(c, 1);
     c += __shfl_xor(c, 2);
-    if (q == 0 && c) atomicAdd(&rowHist[r], c);
+    if (q == 0 && c) {
+      atomicAdd(&rowHist[r], c);
+      if (segRows) atomicAdd(&segH[r], c);
+    }
   }
   __syncthreads();
-  if (tid < kBins && s_d2[tid]) atomicAdd(&segH[tid], s_d2[tid]);
+  if (!segRows && tid < kBins && s_d2[tid]) atomicAdd(&segH[tid], s_d2[tid]);
   if constexpr (kCheck) {
     if (__ballot(viol != 0)) {
       if (lane == 0) atomicOr(&meta[kMetaSqViol], 1u);
@@ -522,6 +528,52 @@ __global__ __launch_bounds__(kSqSampleThreads) void thrs_squeeze_sample(const ty
   }
   out->pad = 0;
   out->on = any ? 1u : 0u;
+}
+
+// ------------------------------------------------------- partition plan
+// thrs_partition_pass (the multi-GPU bucket exchange's first step, one stable
+// pass by one digit): after thrs_hist_joint in segRows mode (the bucket's top
+// byte = the pass's digit, per position segment), one 256-thread workgroup
+// turns the digit totals into bases and the 256 counts the caller gets, and
+// the position segments into the segmented pass's tables (as thrs_plan_rows
+// does for the second-digit pass): segBase[s][d] = base(d) + (keys of digit d
+// in earlier segments), segment positions, first tile ids, tickets.
+__global__ __launch_bounds__(kBins) void thrs_partition_plan(const uint32_t* __restrict__ rowHist,
+                                                             const uint32_t* __restrict__ segHist, uint32_t n,
+                                                             uint32_t histGrid, uint32_t tileKeys,
+                                                             uint32_t* __restrict__ counts,
+                                                             uint32_t* __restrict__ segInfo,
+                                                             uint32_t* __restrict__ segBase) {
+  __shared__ uint32_t s_w[4];
+  const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const uint32_t tot = rowHist[t];
+  const uint32_t inc = wave_incl_scan(tot, lane);
+  if (lane == 63) s_w[w] = inc;
+  __syncthreads();
+  uint32_t b = inc - tot;
+  for (uint32_t ww = 0; ww < w; ++ww) b += s_w[ww];
+  counts[t] = tot;
+#pragma unroll
+  for (int sg = 0; sg < kSegs; ++sg) {
+    segBase[sg * kBins + t] = b;
+    b += segHist[sg * kBins + t];
+  }
+  if (t == 0) {
+    uint32_t tiles = 0;
+    segInfo[kSegAlignWord] = 0;
+    segInfo[kSegVecWord] = 0;
+    for (int sg = 0; sg <= kSegs; ++sg) {
+      const uint32_t pos = sg < kSegs ? hj_seg_pos(n, histGrid, (uint32_t)sg) : n;
+      segInfo[sg] = pos;
+      segInfo[kSegs + 1 + sg] = tiles;
+      if (sg < kSegs) {
+        const uint32_t next = sg + 1 < kSegs ? hj_seg_pos(n, histGrid, (uint32_t)sg + 1) : n;
+        const uint32_t nT = seg_tiles(pos, next, tileKeys, false);
+        tiles += (nT + kGroup - 1) / kGroup * kGroup;
+        segInfo[64 + sg] = 0;  // ticket (own cache line)
+      }
+    }
+  }
 }
 
 // ------------------------------------------------------------- plan, rows
@@ -1400,23 +1452,47 @@ __global__ __launch_bounds__(LG::THREADS) void thrs_local(typename KeyTraits<KT>
 // at (s / 64) * 66 + s % 64.  Structured inputs scatter with regular strides
 // (sorted keys: a wave's 64 slots ~288 apart, all on 2 of the 32 store banks);
 // the pad spreads them.  A wave's 64 consecutive slots stay contiguous.
-template <int W, int K, int WPE_ = 6, int LB_ = K> struct Loc16G {
-  static constexpr int WAVES = W, KPT = K, THREADS = 64 * W, NP = (K + 1) / 2, WPE = WPE_, LB = LB_;
+// The first round (the low byte) need not be stable: equal 16-bit items are
+// indistinguishable, and only the second round must keep the first's order.
+// It counts and ranks into ONE workgroup-wide table of TC copies of the 256
+// digit counters, copy = lane % TC, as 16-bit halves (digits 2i and 2i+1
+// share word i * TC + copy; copy_table_scan).  The second round keeps the
+// per-wave counters and the lane-ordered rank (stable).  The table shares
+// the counters' LDS: 128 x TC words (TC = 8: 4 KiB, within every geometry's
+// per-wave counters).  Measured (docs/EXPERIMENTS.md row 119): local16 C2
+// 1.741 -> 1.660 ms, C4 0.446 -> 0.410, ref160m 0.317 -> 0.300; TC = 4 and
+// TC = 16 (16 KiB: a workgroup fewer per CU at 9216-key chunks) are slower.
+#ifndef THRS_LOC16_TC
+#define THRS_LOC16_TC 8
+#endif
+template <int W, int K, int WPE_ = 6, int LB_ = K, int TC_ = THRS_LOC16_TC> struct Loc16G {
+  static constexpr int WAVES = W, KPT = K, THREADS = 64 * W, NP = (K + 1) / 2, WPE = WPE_, LB = LB_, TC = TC_;
   static constexpr uint32_t CAP = (uint32_t)THREADS * K;
+  static_assert(TC == 0 || (CAP < 65536 && (TC & (TC - 1)) == 0 && TC % 4 == 0 && TC <= 64),
+                "16-bit table halves; whole uint4 rows");
   static constexpr uint32_t ROW = 66;                                // u16 slots per 64 items
   static constexpr size_t STAGE_BYTES = (size_t)(CAP / 64) * ROW * 2;
-  static constexpr size_t LDS = STAGE_BYTES + (size_t)W * kBins * 4;
+  static constexpr size_t CNT_BYTES = (size_t)W * kBins * 4 > (size_t)(kBins / 2) * TC * 4
+                                          ? (size_t)W * kBins * 4
+                                          : (size_t)(kBins / 2) * TC * 4;
+  static constexpr size_t LDS = STAGE_BYTES + CNT_BYTES;
   __device__ static uint32_t at(uint32_t s) { return (s >> 6) * ROW + (s & 63u); }
 };
 using Loc16 = Loc16G<8, 36>;
 // n <= 2^29: 9216-key chunks (uniform buckets of <= 8K keys), 6 WGs per CU
-using Loc16Small = Loc16G<4, 36, 6, 36>;
+#ifndef THRS_L16S_CFG
+#define THRS_L16S_CFG 4, 36, 6, 36
+#endif
+using Loc16Small = Loc16G<THRS_L16S_CFG>;
 // u32 keys-only up to 3 x 2^26 keys (uniform buckets of <= 3072 keys): 4096-
 // key chunks, 8 WGs per CU.  A chunk's items spread over all four waves
 // (~10 per lane at 160M keys instead of 36 in wave 0 and ~2 in wave 1 of a
 // 9216-key chunk): the rounds' critical path is 2-3x shorter
 // (docs/EXPERIMENTS.md row 112)
-using Loc16Tiny = Loc16G<4, 16, 8, 16>;
+#ifndef THRS_L16T_CFG
+#define THRS_L16T_CFG 4, 16, 8, 16
+#endif
+using Loc16Tiny = Loc16G<THRS_L16T_CFG>;
 static_assert(Loc16::CAP == LocBig::CAP, "same chunk capacity as the 32-bit geometry (thrs_plan's cap)");
 // Wide chunks for u32 keys-only sorts above 2^30 + 2^26, whose uniform
 // buckets (n / 65536 keys) outgrow Loc16's 18432 slots: 34816 keys (8 waves x
@@ -1535,6 +1611,123 @@ __device__ __attribute__((noinline)) void loc16_write_zero_log(uint32_t* __restr
   }
 }
 
+// The copy table of a non-stable first round (Loc16G::TC, thrs_local_kv):
+// 256 digits x TC copies of their counters as 16-bit halves, word
+// (d >> 1) * TC + copy, copy = lane % TC.  After the count, one exclusive
+// scan in (digit, copy) order turns every counter into its copy's first slot;
+// a returning add then hands each item its slot.  Every thread calls it (two
+// barriers inside; the count's barrier is the caller's, before).
+// thrs_local16 / thrs_local_kv: no half reaches 65536 (CAP < 65536).
+template <int TC>
+__device__ __forceinline__ void copy_table_scan(uint32_t* __restrict__ tbl, unsigned char* smem, uint32_t tid,
+                                                uint32_t lane, uint32_t w) {
+  // exclusive scan in (digit, copy) order: thread t < 128 owns digits 2t
+  // (low halves) and 2t + 1 (high halves) of row t; the rows' totals are
+  // scanned over the first two waves (stage words carry wave 0's total).
+  // The row is read twice (sums, then prefixes + bases) so that no row stays
+  // in registers across the barrier.
+  uint32_t* s_wt = reinterpret_cast<uint32_t*>(smem);
+  uint32_t t0 = 0, t1 = 0, tot = 0, inc = 0;
+  uint4* row = reinterpret_cast<uint4*>(tbl + (tid & (kBins / 2 - 1)) * TC);
+  if (tid < kBins / 2) {
+#pragma unroll
+    for (int q = 0; q < TC / 4; ++q) {
+      const uint4 x = row[q];
+      const uint32_t s4 = x.x + x.y + x.z + x.w;  // (four 16-bit halves each: no carry, every half < CAP)
+      t0 += s4 & 0xFFFFu;
+      t1 += s4 >> 16;
+    }
+    tot = t0 + t1;
+    inc = wave_incl_scan(tot, lane);
+    if (lane == 63 && w == 0) s_wt[0] = inc;
+  }
+  lds_barrier();
+  if (tid < kBins / 2) {
+    const uint32_t b0 = inc - tot + (w == 1 ? s_wt[0] : 0u), b1 = b0 + t0;  // digit 2t's base, digit 2t+1's
+    uint32_t run = b0 | (b1 << 16);  // (every half stays below CAP < 65536: no carry between halves)
+#pragma unroll
+    for (int q = 0; q < TC / 4; ++q) {
+      const uint4 x = row[q];
+      uint4 y;
+      y.x = run;
+      run += x.x;
+      y.y = run;
+      run += x.y;
+      y.z = run;
+      run += x.z;
+      y.w = run;
+      run += x.w;
+      row[q] = y;
+    }
+  }
+  lds_barrier();
+}
+__device__ __forceinline__ uint32_t* copy_cell(uint32_t* tbl, uint32_t d, uint32_t cp, int tc) {
+  return &tbl[(d >> 1) * (uint32_t)tc + cp];
+}
+__device__ __forceinline__ uint32_t copy_inc(uint32_t d) { return 1u << ((d & 1u) << 4); }
+
+// thrs_local16's first round (the items' low byte) from the copy table
+// (Loc16G::TC): count, scan, rank and scatter into the stage.  Every thread
+// of the workgroup calls it; on return the stage holds the chunk's items
+// ordered by their low byte (equal low bytes in no particular order) and a
+// barrier is due before the stage is read.
+template <typename LG>
+__device__ __forceinline__ void local16_table_round(const uint32_t (&it)[LG::NP], uint32_t* __restrict__ tbl,
+                                                    uint16_t* __restrict__ stage, unsigned char* smem, int nItems,
+                                                    uint32_t lane, uint32_t tid, uint32_t w) {
+  constexpr int KPT = LG::KPT, TC = LG::TC;
+  constexpr uint32_t WORDS = (kBins / 2) * TC;
+  auto digit_of = [&](int j) -> uint32_t { return (it[j >> 1] >> ((j & 1) * 16)) & 0xFFu; };
+  const uint32_t cp = lane & (uint32_t)(TC - 1);
+  for (uint32_t i = tid; i < WORDS / 4; i += LG::THREADS) reinterpret_cast<uint4*>(tbl)[i] = make_uint4(0, 0, 0, 0);
+  lds_barrier();
+  auto cell = [&](uint32_t d) -> uint32_t* { return &tbl[(d >> 1) * TC + cp]; };
+  auto inc_of = [](uint32_t d) -> uint32_t { return 1u << ((d & 1u) << 4); };
+  // (whole waves without per-item tests: see the second round's count)
+  if (nItems == KPT) {
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) {
+      const uint32_t d = digit_of(j);
+      __hip_atomic_fetch_add(cell(d), inc_of(d), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) {
+      const uint32_t d = digit_of(j);
+      if (j < nItems) __hip_atomic_fetch_add(cell(d), inc_of(d), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  }
+  lds_barrier();
+  copy_table_scan<TC>(tbl, smem, tid, lane, w);
+  // rank (the returned half is the slot) + scatter, RB atomics in flight
+  constexpr int RB = THRS_LOC_RB;
+  auto rank_scatter = [&](auto fullc) __attribute__((always_inline)) {
+    constexpr bool FULL = decltype(fullc)::value;
+#pragma unroll
+    for (int j0 = 0; j0 < KPT; j0 += RB) {
+      uint32_t sl[RB];
+#pragma unroll
+      for (int jj = 0; jj < RB; ++jj) {
+        const int j = j0 + jj;
+        if (j < KPT && (FULL || j < nItems)) {
+          const uint32_t d = digit_of(j);
+          sl[jj] = (__hip_atomic_fetch_add(cell(d), inc_of(d), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >>
+                    ((d & 1u) << 4)) & 0xFFFFu;
+        }
+      }
+#pragma unroll
+      for (int jj = 0; jj < RB; ++jj) {
+        const int j = j0 + jj;
+        if (j < KPT && (FULL || j < nItems)) stage[LG::at(sl[jj])] = (uint16_t)((it[j >> 1] >> ((j & 1) * 16)) & 0xFFFFu);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  if (nItems == KPT) rank_scatter(std::true_type{});
+  else rank_scatter(std::false_type{});
+}
+
 // One chunk of thrs_local16 under the key map km: the plain map, or the
 // squeeze fixed to the chunk's image half (KeyMapHalf).  A device function on
 // a plain branch, not a with_map lambda: the closure and the two-half map
@@ -1601,7 +1794,27 @@ __device__ __forceinline__ void local16_chunk(uint32_t* __restrict__ keys, KM km
   }
   auto item = [&](int j) -> uint32_t { return (it[j >> 1] >> ((j & 1) * 16)) & 0xFFFFu; };
 
-  for (int r = 0; r < 2; ++r) {
+  constexpr int TC = LG::TC;
+  if constexpr (TC > 0) {  // the first round from the copy table (Loc16G): not stable, fewer bank conflicts
+    local16_table_round<LG>(it, s_cnt, stage, smem, nItems, lane, tid, w);
+    lds_barrier();
+    if (limw >= (int32_t)CHUNK) {
+#pragma unroll
+      for (int j = 0; j < KPT; j += 2) {
+        const uint32_t a = stw[j * LG::ROW];
+        const uint32_t b = (j + 1 < KPT) ? (uint32_t)stw[(j + 1) * LG::ROW] : 0xFFFFu;
+        it[j >> 1] = a | (b << 16);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < KPT; j += 2) {
+        const uint32_t a = (j * 64 < limw) ? (uint32_t)stw[j * LG::ROW] : 0xFFFFu;
+        const uint32_t b = (j + 1 < KPT && (j + 1) * 64 < limw) ? (uint32_t)stw[(j + 1) * LG::ROW] : 0xFFFFu;
+        it[j >> 1] = a | (b << 16);
+      }
+    }
+  }
+  for (int r = TC > 0 ? 1 : 0; r < 2; ++r) {
     const int shift = 8 * r;
     auto digit_of = [&](int j) -> uint32_t { return (it[j >> 1] >> ((j & 1) * 16 + shift)) & 0xFFu; };
 #pragma unroll
