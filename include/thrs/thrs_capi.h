@@ -28,7 +28,7 @@ extern "C" {
 typedef struct ihipStream_t* hipStream_t; /* identical to HIP's own typedef */
 #endif
 
-#define THRS_ABI_VERSION 5
+#define THRS_ABI_VERSION 6
 
 typedef enum thrs_status {
   THRS_SUCCESS = 0,

@@ -31,7 +31,7 @@ from dataclasses import dataclass
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libthrs.so")
 TESTUTIL_PATH = os.path.join(_HERE, "libthrs_testutil.so")
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 __all__ = ["KeyType", "ValueType", "SortOrder", "bytesOf", "div_round_up64", "next_multiple64", "Buffer",
            "RadixSort", "Options", "ThrsError", "lib", "LIB_PATH", "take_device_error"]

@@ -1459,7 +1459,7 @@ __global__ __launch_bounds__(LG::THREADS) void thrs_local(typename KeyTraits<KT>
 // share word i * TC + copy; copy_table_scan).  The second round keeps the
 // per-wave counters and the lane-ordered rank (stable).  The table shares
 // the counters' LDS: 128 x TC words (TC = 8: 4 KiB, within every geometry's
-// per-wave counters).  Measured (docs/EXPERIMENTS.md row 119): local16 C2
+// per-wave counters).  Measured (docs/EXPERIMENTS.md row 120): local16 C2
 // 1.741 -> 1.660 ms, C4 0.446 -> 0.410, ref160m 0.317 -> 0.300; TC = 4 and
 // TC = 16 (16 KiB: a workgroup fewer per CU at 9216-key chunks) are slower.
 #ifndef THRS_LOC16_TC
