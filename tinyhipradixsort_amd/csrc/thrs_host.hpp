@@ -452,6 +452,14 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   constexpr int kPlaneKT = kPlanes4 ? 0 : KT;
   auto skSplit = atomicRank ? thrs_pass_seg<KT, VB, ST, true, kPlanes4 ? kCodecSplit : kCodecKeys>
                             : thrs_pass_seg<KT, VB, ST, false, kPlanes4 ? kCodecSplit : kCodecKeys>;
+  // (both codecs of one top-digit pass in one launch: thrs_pass_seg2; the
+  // 4-byte keys-only instantiations serve the planes, the others are never
+  // launched)
+  constexpr int kKT4 = kPlanes4 ? KT : 0;
+  auto sk2Split = atomicRank ? thrs_pass_seg2<kKT4, kKT4, 0, ST, true, kCodecSplit>
+                             : thrs_pass_seg2<kKT4, kKT4, 0, ST, false, kCodecSplit>;
+  auto sk2Planes = atomicRank ? thrs_pass_seg2<0, kKT4, 0, ST, true, kCodecPlanes>
+                              : thrs_pass_seg2<0, kKT4, 0, ST, false, kCodecPlanes>;
   auto skPlanes = atomicRank ? thrs_pass_seg<kPlaneKT, VB, ST, true, kPlanes4 ? kCodecPlanes : kCodecKeys>
                              : thrs_pass_seg<kPlaneKT, VB, ST, false, kPlanes4 ? kCodecPlanes : kCodecKeys>;
   const uint32_t segTileKeys = (uint32_t)seg_tile_keys(KB, VB);
@@ -464,7 +472,8 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     if (allow_lds(thrs_hist_joint<KT>, kJointLds) != hipSuccess || allow_lds(sk, lds) != hipSuccess ||
         (squeeze && allow_lds(thrs_hist_joint<KT, true>, kJointLds) != hipSuccess))
       return THRS_ERROR_HIP;
-    if (planes && (allow_lds(skSplit, lds) != hipSuccess || allow_lds(skPlanes, lds) != hipSuccess))
+    if (planes && (allow_lds(skSplit, lds) != hipSuccess || allow_lds(skPlanes, lds) != hipSuccess ||
+                   allow_lds(sk2Split, lds) != hipSuccess || allow_lds(sk2Planes, lds) != hipSuccess))
       return THRS_ERROR_HIP;
     if constexpr (kKV) {
       if (allow_lds(atomicRank ? thrs_local_kv<KT, VB, true> : thrs_local_kv<KT, VB, false>, LocKV::LDS) != hipSuccess)
@@ -721,15 +730,31 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                                   : nullptr,
                          sqw, codec == kCodecPlanes ? base + nLow * kBins : nullptr);
     };
+    // planes: the codec and the whole-key body of one pass in one launch
+    // (thrs_pass_seg2, mode-dispatched)
+    auto launch_seg2 = [&](int p, bool top) {
+      ProfScope prof(stream, 1, THRS_PK_PASS_SEG, moveBytes);
+      uint32_t* kA = top ? reinterpret_cast<uint32_t*>(loP) : reinterpret_cast<uint32_t*>(K);
+      uint32_t* oA = reinterpret_cast<uint32_t*>(top ? lo2P : loP);
+      uint32_t* kB = reinterpret_cast<uint32_t*>(top ? keyOut : K);
+      uint32_t* oB = reinterpret_cast<uint32_t*>(top ? K : keyOut);
+      hipLaunchKernelGGL(top ? sk2Planes : sk2Split, dim3((uint32_t)segPerCU * cu_count()), dim3(G::THREADS), lds,
+                         stream, kA, oA, top ? KeyMap<uint32_t>{} : km32, top ? 16 : startBits + 8 * p,
+                         top ? base + nLow * kBins : nullptr, kB, oB, km32, startBits + 8 * p,
+                         reinterpret_cast<uint32_t*>(hyb + (top ? kSegInfoOff : kSegInfoAOff)),
+                         reinterpret_cast<const uint32_t*>(hyb + (top ? kSegBaseOff : kSegBaseAOff)), status[p & 1], err,
+                         grp[p & 1], static_cast<const uint32_t*>(mode), hiP,
+                         g_stamps ? g_stamps + (uint64_t)(p - nLow) * (plan.nTiles + kSegTilePad) * kStampSlots
+                                  : nullptr,
+                         sqw);
+    };
     const uint64_t sw = plan.wideStatus ? 8 : 4;
     const int setB = (nLow + 1) & 1;
     if (segA) {
       // Both table sets are clean (zeroed up front); the segmented passes'
       // extra tile ids (rows past nTiles) are touched by nothing else.
       if (planes) {
-        launch_seg(nLow, K, reinterpret_cast<U*>(loP), V, valOut, kSegInfoAOff, kSegBaseAOff, mode, kGateMode0,
-                   kCodecSplit);
-        launch_seg(nLow, K, keyOut, V, valOut, kSegInfoAOff, kSegBaseAOff, mode, kGateMode1 | kGateMode3);
+        launch_seg2(nLow, false);
       } else {
         launch_seg(nLow, K, keyOut, V, valOut, kSegInfoAOff, kSegBaseAOff, mode, kGateMode0 | kGateMode1 | kGateMode3);
       }
@@ -747,9 +772,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
         return THRS_ERROR_HIP;
     }
     if (planes) {  // mode 0: planes -> lo2; mode 1 (big chunks) / 3 (f32 -0): keys
-      launch_seg(nLow + 1, reinterpret_cast<U*>(loP), reinterpret_cast<U*>(lo2P), valOut, V, kSegInfoOff, kSegBaseOff,
-                 mode, kGateMode0, kCodecPlanes);
-      launch_seg(nLow + 1, keyOut, K, valOut, V, kSegInfoOff, kSegBaseOff, mode, kGateMode1 | kGateMode3);
+      launch_seg2(nLow + 1, true);
     } else if (segTop)
       launch_seg(nLow + 1, keyOut, K, valOut, V, kSegInfoOff, kSegBaseOff, mode, kGateMode0 | kGateMode1 | kGateMode3);
     else

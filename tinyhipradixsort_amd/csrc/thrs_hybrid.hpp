@@ -764,6 +764,7 @@ __global__ __launch_bounds__(kPlanRowThreads) void thrs_plan_rows(
   if (sqMode == 2 && meta[kMetaRehist] == 0) return;
   __shared__ uint32_t s_w[2][4], s_base, s_b2[kBins], s_sq[3], s_last;
   const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6, r = blockIdx.x;
+  const uint32_t x = joint[kBins * r + t];
   // 256-thread exclusive scan (4 waves)
   auto scan256 = [&](uint32_t v, int slot, uint32_t* total) -> uint32_t {
     const uint32_t inc = wave_incl_scan(v, lane);
@@ -783,7 +784,6 @@ __global__ __launch_bounds__(kPlanRowThreads) void thrs_plan_rows(
   const uint32_t rowTot = rowHist[t];
   const uint32_t rowEx = scan256(rowTot, 0, nullptr);
   if (t == r) s_base = rowEx;
-  const uint32_t x = joint[kBins * r + t];
   const uint32_t pre = scan256(x, 1, nullptr);  // (its barrier also publishes s_base)
   const uint32_t base = s_base;
   chunkOff[kBins * r + t] = base + pre;

@@ -1716,6 +1716,33 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
                                                       status, errFlag, grp, hiPlane, stamps, sq, secondBase);
 }
 
+// The bucket path's two launches of one top-digit pass in ONE (u32 / f32 keys
+// without values, planes on): the plan's mode picks the body -- mode 0 the
+// key-plane codec CODEC_A (kCodecSplit: keys in, planes out; kCodecPlanes:
+// planes in, a plane out, image space KTA), modes 1 / 3 whole keys
+// (kCodecKeys, KTB), mode 2 neither.  A gated launch that does nothing still
+// costs ~4.7 us of device time (rocprof timeline, docs/EXPERIMENTS.md row
+// 124), so each top-digit pass is one launch whatever the plan decides.
+template <int KTA, int KTB, int VB, typename ST, bool ATOMIC_RANK, int CODEC_A>
+__global__ __launch_bounds__((PassGeom<4, VB>::THREADS))
+__attribute__((amdgpu_waves_per_eu(PassGeom<4, VB>::WPE))) void thrs_pass_seg2(
+    const uint32_t* __restrict__ kinA, uint32_t* __restrict__ koutA, KeyMap<uint32_t> kmA, int shiftA,
+    const uint32_t* __restrict__ secondBaseA, const uint32_t* __restrict__ kinB, uint32_t* __restrict__ koutB,
+    KeyMap<uint32_t> kmB, int shiftB, uint32_t* __restrict__ segInfo, const uint32_t* __restrict__ segBase,
+    ST* __restrict__ status, uint32_t* __restrict__ errFlag, GroupTables<ST> grp, const uint32_t* __restrict__ mode,
+    uint8_t* __restrict__ hiPlane, uint64_t* __restrict__ stamps, const SqueezeWords* __restrict__ sq) {
+  static_assert(sizeof(typename KeyTraits<KTA>::U) == 4 && sizeof(typename KeyTraits<KTB>::U) == 4 && VB == 0,
+                "4-byte keys without values");
+  const uint32_t m = *mode;
+  if (m == 0)
+    thrs_pass_seg_body<KTA, VB, ST, ATOMIC_RANK, CODEC_A>(kinA, koutA, nullptr, nullptr, kmA, shiftA, segInfo, segBase,
+                                                          status, errFlag, grp, hiPlane, stamps, sq, secondBaseA);
+  else if (m == 1 || m == 3)
+    thrs_pass_seg_body<KTB, VB, ST, ATOMIC_RANK, kCodecKeys>(kinB, koutB, nullptr, nullptr, kmB, shiftB, segInfo,
+                                                             segBase, status, errFlag, grp, nullptr, stamps, sq,
+                                                             nullptr);
+}
+
 // Zeroing of up to three 16-byte-aligned ranges in one launch (the scratch
 // header and look-back tables at the start of every sort).
 struct ZeroRanges {
