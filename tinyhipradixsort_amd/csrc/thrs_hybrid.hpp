@@ -809,11 +809,13 @@ __global__ __launch_bounds__(kPlanRowThreads) void thrs_plan_rows(
     if (x > cap) atomicAdd(&s_sq[2], 1u);
     __syncthreads();
     if (t == 0) {
+      // (128 workgroups per half OR into the same two words: an atomic only
+      // where it adds bits -- same-address device atomics serialise, ~5 us
+      // over the launch when every workgroup issues them)
       const uint32_t h = r >> 7;
-      if (s_sq[0] | s_sq[1]) {
-        atomicOr(&meta[kMetaOr1 + h], s_sq[0]);
-        atomicOr(&meta[kMetaOr0 + h], s_sq[1]);
-      }
+      const uint32_t o1 = load_agent(&meta[kMetaOr1 + h]), o0 = load_agent(&meta[kMetaOr0 + h]);
+      if (s_sq[0] & ~o1) atomicOr(&meta[kMetaOr1 + h], s_sq[0]);
+      if (s_sq[1] & ~o0) atomicOr(&meta[kMetaOr0 + h], s_sq[1]);
       if (s_sq[2]) atomicAdd(&meta[kMetaBigHalf + h], s_sq[2]);
     }
   }
