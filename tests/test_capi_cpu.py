@@ -143,7 +143,14 @@ def test_path_info_matches_the_configs():
     assert (c2["path"], c2["local"], c2["planes"], c2["device_passes"]) == ("bucket", "thrs_local16", True, 2)
     assert c2["min_bytes"] == (4 + 7 + 5 + 6) * (1 << 30)           # hist 4, passes 4+3 and 3+2, local 2+4
     c3 = info(U32, T.ValueType.U32, 1 << 30, True)
-    assert (c3["path"], c3["local"]) == ("bucket", "thrs_local_pairs")
+    assert (c3["path"], c3["local"], c3["planes"]) == ("bucket", "thrs_local_pairs", True)
+    # keys as planes, values as they are: hist 4, passes (4+4)+(3+4) and
+    # (3+4)+(2+4), local (2+4)+(4+4)
+    assert c3["min_bytes"] == (4 + 15 + 13 + 14) * (1 << 30)
+    c3off = info(U32, T.ValueType.U32, 1 << 30, True, planes="off")
+    assert not c3off["planes"] and c3off["min_bytes"] == (4 + 16 + 16 + 16) * (1 << 30)
+    assert not info(F32, T.ValueType.U32, 1 << 30, True)["planes"]        # f32 pairs: whole keys
+    assert not info(U32, T.ValueType.U64, 1 << 30, True)["planes"]        # 8-byte values: whole keys
     c4 = info(F32, T.ValueType.U32, 1 << 28, False)
     assert (c4["path"], c4["local"], c4["planes"], c4["local_cap"]) == ("bucket", "thrs_local16", True, 9216)
     assert c4["min_bytes"] == (4 + 7 + 5 + 6) * (1 << 28)

@@ -16,6 +16,10 @@ of RadixSort::sort (tinyhipradixsort.hpp:854-944), key for key:
 * a FORCED bucket path at small n with a distribution that puts the keys in
   four second-digit regions, so nearly every top-pass tile is a vector tile.
 
+u32 keys with u32 values carry the keys as the same planes (no vector tiles:
+the values keep input order), so their keys AND values are compared with the
+oracle's, which checks the stable order of equal keys through the codecs.
+
 Each planes case asserts pathInfo()['planes'] and that the vector branch ran
 (thrs_debug_vector_tiles, a counter the top-digit pass keeps)."""
 import numpy as np
@@ -136,8 +140,72 @@ def test_u32_pairs_default_path_vs_oracle(gpu, desc):
     vals = np.arange(n, dtype=np.uint32)
     rs = _sorter(O.U32, 4, desc)
     info = rs.pathInfo(n, 0, 32, True)
-    assert (info["path"], info["local"], info["local_cap"]) == ("bucket", "thrs_local_pairs", 4096)
-    k, v, _ = _sort_on_gpu(torch, rs, O.U32, keys, vals)
+    assert (info["path"], info["local"], info["local_cap"], info["planes"]) == ("bucket", "thrs_local_pairs", 4096,
+                                                                                True)
+    k, v, tmp = _sort_on_gpu(torch, rs, O.U32, keys, vals)
+    assert rs.debugBucketMode(tmp, n, True)[0] == 0            # mode 0: the planes ran
+    ek, ev = O.lsd_sort(O.U32, keys, vals, 0, 32, desc)
+    assert np.array_equal(k, ek)
+    assert np.array_equal(v, ev)
+
+
+@pytest.mark.parametrize("desc", [False, True])
+@pytest.mark.parametrize("geom", ["tiny16", "small", "big"])
+@pytest.mark.parametrize("n", [1 << 20, 3 * (1 << 20) + 12345])
+def test_forced_bucket_pairs_planes_vs_oracle(gpu, n, geom, desc):
+    """u32 pairs on a forced bucket path (planes on, mode 0) in every pairs
+    chunk geometry: ties in the low 16 bits every 5th key, so the values'
+    stable order through the split / planes codecs and the plane-fed local
+    sort is visible.  Keys and values bit-exact against the oracle."""
+    torch = gpu
+    keys = _u32_keys(n, 6600 + n % 89 + int(desc) + 3 * len(geom))
+    keys[::5] &= np.uint32(0xFFFF0000)
+    vals = np.arange(n, dtype=np.uint32) ^ np.uint32(0x5A5A5A5A)
+    rs = _sorter(O.U32, 4, desc, path="bucket", localGeometry=geom)
+    assert rs.pathInfo(n, 0, 32, True)["planes"]
+    k, v, tmp = _sort_on_gpu(torch, rs, O.U32, keys, vals)
+    assert rs.debugBucketMode(tmp, n, True)[0] == 0
+    ek, ev = O.lsd_sort(O.U32, keys, vals, 0, 32, desc)
+    assert np.array_equal(k, ek)
+    assert np.array_equal(v, ev)
+
+
+@pytest.mark.parametrize("desc", [False, True])
+def test_forced_bucket_pairs_planes_ranged_and_off(gpu, desc):
+    """u32 pairs with a key range (the codecs carry the RANGED images,
+    thrs_options.keyRange) and with the planes off: both equal the oracle."""
+    torch = gpu
+    n = (1 << 21) + 777
+    lo = 0x01230000
+    keys = (lo + (_u32_keys(n, 6700 + int(desc)) >> np.uint32(8))).astype(np.uint32)   # images in [lo, lo + 2^24)
+    vals = np.arange(n, dtype=np.uint32)
+    ek, ev = O.lsd_sort(O.U32, keys, vals, 0, 32, desc)
+    img = keys ^ np.uint32(0xFFFFFFFF) if desc else keys
+    rng = (int(img.min()), int(img.max()))
+    for kw in ({"keyRange": rng}, {"planes": "off"}):
+        rs = _sorter(O.U32, 4, desc, path="bucket", **kw)
+        assert rs.pathInfo(n, 0, 32, True)["planes"] == ("planes" not in kw)
+        k, v, _ = _sort_on_gpu(torch, rs, O.U32, keys, vals)
+        assert np.array_equal(k, ek), kw
+        assert np.array_equal(v, ev), kw
+
+
+@pytest.mark.parametrize("desc", [False, True])
+def test_forced_bucket_pairs_big_chunks_vs_oracle(gpu, desc):
+    """u32 pairs where a few buckets exceed the local capacity (mode 1: the
+    single top-digit launches run their whole-key bodies, with the values, and
+    the per-bucket fallback sorts the big chunks): keys and values against the
+    oracle."""
+    torch = gpu
+    n = 3 << 20
+    keys = _u32_keys(n, 6800 + int(desc))
+    keys[: n // 3] = (keys[: n // 3] & np.uint32(0x0000FFFF)) | np.uint32(0x77770000)   # one 1M-key bucket
+    perm = np.random.default_rng(6800).permutation(n)
+    keys = keys[perm]
+    vals = np.arange(n, dtype=np.uint32)
+    rs = _sorter(O.U32, 4, desc, path="bucket")
+    k, v, tmp = _sort_on_gpu(torch, rs, O.U32, keys, vals)
+    assert rs.debugBucketMode(tmp, n, True)[0] == 1
     ek, ev = O.lsd_sort(O.U32, keys, vals, 0, 32, desc)
     assert np.array_equal(k, ek)
     assert np.array_equal(v, ev)

@@ -167,9 +167,12 @@ inline Plan make_plan(int keyType, int valueBytesOrZero, uint32_t n) {
   // range): the default takes it from kBucketMinKeysU32 / kBucketMinKeys4, and
   // a bucket path forced below that carries the planes too, so the codecs the
   // headline runs are tested element-wise at sizes the oracle finishes.
+  // u32 keys with 4-byte values likewise, up to 2^30 + 2^26 (the u16 planes
+  // fill keyOut, the values take valueOut as ever).
   p.hiPlaneOff = p.scratchBytes;
-  if ((keyType == THRS_KEY_U32 || keyType == THRS_KEY_F32) && valueBytesOrZero == 0 &&
-      (uint64_t)n <= (1ull << 31) + (1ull << 25))
+  if (((keyType == THRS_KEY_U32 || keyType == THRS_KEY_F32) && valueBytesOrZero == 0 &&
+       (uint64_t)n <= (1ull << 31) + (1ull << 25)) ||
+      (keyType == THRS_KEY_U32 && valueBytesOrZero == 4 && (uint64_t)n <= (1ull << 30) + (1ull << 26)))
     p.scratchBytes += round_up(n, kAlign);
   return p;
 }
@@ -321,8 +324,10 @@ PathSel select_path(uint32_t n, int startBits, int nPass, const thrs_options& op
   // keyOut (4n bytes) = lo u16[n] | lo2 u16[n], the u8 plane hi[n] at the end
   // of the scratch.  f32: -0 and +0 share one image, so a plan that saw a -0
   // key (thrs_hist_joint) runs the whole-key passes instead (mode 3)
-  const bool planes = local16 && (KT == 0 || KT == 2) && segA && opt.planes != THRS_PLANES_OFF &&
-                      plan.scratchBytes - plan.hiPlaneOff >= (uint64_t)n;
+  // (u32 keys + 4-byte values: thrs_local_pairs over the lo2 plane, the
+  // values as they are)
+  const bool planes = ((local16 && (KT == 0 || KT == 2)) || (KT == 0 && VB == 4 && bucket && fullWindow)) && segA &&
+                      opt.planes != THRS_PLANES_OFF && plan.scratchBytes - plan.hiPlaneOff >= (uint64_t)n;
   // the local sort's chunk capacity (a bigger bucket is a big chunk)
   const uint32_t cap = kKV ? LocKV::CAP
                        : local16 ? (wide16    ? Loc16Wide::CAP
@@ -424,7 +429,6 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     km.lo = (U)opt.rangeLo;
     km.sh = sizeof(U) == 4 ? (uint32_t)__builtin_clz((uint32_t)span) : (uint32_t)__builtin_clzll((uint64_t)span);
   }
-  const KeyMap<U> kid{(U)0, (U)0, 0u};  // image-space input (the planes codec)
   const KeyMap<uint32_t> km32{(uint32_t)km.mask, (uint32_t)km.lo, km.sh};
   uint16_t* loP = static_cast<uint16_t*>(keyOutBuf);
   uint16_t* lo2P = loP + n;
@@ -445,23 +449,19 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   auto kernelBig = atomicRank ? thrs_pass_big<KT, VB, ST, true> : thrs_pass_big<KT, VB, ST, false>;
   auto kernel = useXb ? kernelXb : (atomicRank ? thrs_pass<KT, VB, ST, true> : thrs_pass<KT, VB, ST, false>);
   auto sk = atomicRank ? thrs_pass_seg<KT, VB, ST, true> : thrs_pass_seg<KT, VB, ST, false>;
-  // plane codecs (u32 / f32 keys-only instantiations only; `planes` is false
-  // elsewhere).  The planes codec reads images (identity map): the u32 kernel
-  // serves both key types.
-  constexpr bool kPlanes4 = (KT == 0 || KT == 2) && VB == 0;
-  constexpr int kPlaneKT = kPlanes4 ? 0 : KT;
-  auto skSplit = atomicRank ? thrs_pass_seg<KT, VB, ST, true, kPlanes4 ? kCodecSplit : kCodecKeys>
-                            : thrs_pass_seg<KT, VB, ST, false, kPlanes4 ? kCodecSplit : kCodecKeys>;
-  // (both codecs of one top-digit pass in one launch: thrs_pass_seg2; the
-  // 4-byte keys-only instantiations serve the planes, the others are never
-  // launched)
-  constexpr int kKT4 = kPlanes4 ? KT : 0;
-  auto sk2Split = atomicRank ? thrs_pass_seg2<kKT4, kKT4, 0, ST, true, kCodecSplit>
-                             : thrs_pass_seg2<kKT4, kKT4, 0, ST, false, kCodecSplit>;
-  auto sk2Planes = atomicRank ? thrs_pass_seg2<0, kKT4, 0, ST, true, kCodecPlanes>
-                              : thrs_pass_seg2<0, kKT4, 0, ST, false, kCodecPlanes>;
-  auto skPlanes = atomicRank ? thrs_pass_seg<kPlaneKT, VB, ST, true, kPlanes4 ? kCodecPlanes : kCodecKeys>
-                             : thrs_pass_seg<kPlaneKT, VB, ST, false, kPlanes4 ? kCodecPlanes : kCodecKeys>;
+  // plane codecs, each top-digit pass one launch with its whole-key body
+  // (thrs_pass_seg2; u32 / f32 keys-only and u32 + 4-byte-value
+  // instantiations only: `planes` is false elsewhere, and the others are
+  // never launched).  The planes codec reads images (identity map): the u32
+  // kernel serves both key types.
+  constexpr bool kPlanesK = (KT == 0 || KT == 2) && VB == 0;
+  constexpr bool kPlanesP = KT == 0 && VB == 4;
+  constexpr int kKT4 = kPlanesK ? KT : 0;
+  constexpr int kVB4 = kPlanesP ? 4 : 0;
+  auto sk2Split = atomicRank ? thrs_pass_seg2<kKT4, kKT4, kVB4, ST, true, kCodecSplit>
+                             : thrs_pass_seg2<kKT4, kKT4, kVB4, ST, false, kCodecSplit>;
+  auto sk2Planes = atomicRank ? thrs_pass_seg2<0, kKT4, kVB4, ST, true, kCodecPlanes>
+                              : thrs_pass_seg2<0, kKT4, kVB4, ST, false, kCodecPlanes>;
   const uint32_t segTileKeys = (uint32_t)seg_tile_keys(KB, VB);
   const int histPasses = nPass;
   const size_t histLds = (size_t)histPasses * kBins * hist_copies<(int)sizeof(U)>() * 4;
@@ -472,8 +472,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     if (allow_lds(thrs_hist_joint<KT>, kJointLds) != hipSuccess || allow_lds(sk, lds) != hipSuccess ||
         (squeeze && allow_lds(thrs_hist_joint<KT, true>, kJointLds) != hipSuccess))
       return THRS_ERROR_HIP;
-    if (planes && (allow_lds(skSplit, lds) != hipSuccess || allow_lds(skPlanes, lds) != hipSuccess ||
-                   allow_lds(sk2Split, lds) != hipSuccess || allow_lds(sk2Planes, lds) != hipSuccess))
+    if (planes && (allow_lds(sk2Split, lds) != hipSuccess || allow_lds(sk2Planes, lds) != hipSuccess))
       return THRS_ERROR_HIP;
     if constexpr (kKV) {
       if (allow_lds(atomicRank ? thrs_local_kv<KT, VB, true> : thrs_local_kv<KT, VB, false>, LocKV::LDS) != hipSuccess)
@@ -600,7 +599,8 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                            reinterpret_cast<uint32_t*>(hyb + kBigBOff), sqMode, 8 * KB,
                            reinterpret_cast<uint32_t*>(hyb + kBigPosOff), reinterpret_cast<uint32_t*>(hyb + kBigTileOff),
                            reinterpret_cast<uint4*>(scratch + plan.bigHistOff), nLow,
-                           sqMode == 1 ? static_cast<const SqueezeWords*>(sample) : nullptr, planes ? 1 : 0,
+                           sqMode == 1 ? static_cast<const SqueezeWords*>(sample) : nullptr,
+                           planes && VB == 0 ? 1 : 0,  // (aligned top-pass tiles: the vector loads, keys only)
                            err, g_inject);
       };
       if (!local32 && squeeze) {
@@ -718,20 +718,19 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     // every key: both top digits constant) neither -- both are identities,
     // and skipping both keeps the keys in K.
     auto launch_seg = [&](int p, U* kin, U* kout, VW* vin, VW* vout, uint64_t infoOff, uint64_t baseOff,
-                          const uint32_t* gate, uint32_t gateMask, int codec = kCodecKeys) {
+                          const uint32_t* gate, uint32_t gateMask) {
       ProfScope prof(stream, 1, THRS_PK_PASS_SEG, moveBytes);
-      auto kern = codec == kCodecSplit ? skSplit : codec == kCodecPlanes ? skPlanes : sk;
-      // kCodecPlanes: image-space input (identity map), digit at bits 16-23 of k'
-      hipLaunchKernelGGL(kern, dim3((uint32_t)segPerCU * cu_count()), dim3(G::THREADS), lds, stream, kin, kout, vin,
-                         vout, codec == kCodecPlanes ? kid : km, codec == kCodecPlanes ? 16 : startBits + 8 * p,
-                         reinterpret_cast<uint32_t*>(hyb + infoOff), reinterpret_cast<const uint32_t*>(hyb + baseOff),
-                         status[p & 1], err, grp[p & 1], gate, gateMask, hiP,
+      hipLaunchKernelGGL(sk, dim3((uint32_t)segPerCU * cu_count()), dim3(G::THREADS), lds, stream, kin, kout, vin,
+                         vout, km, startBits + 8 * p, reinterpret_cast<uint32_t*>(hyb + infoOff),
+                         reinterpret_cast<const uint32_t*>(hyb + baseOff), status[p & 1], err, grp[p & 1], gate,
+                         gateMask, hiP,
                          g_stamps ? g_stamps + (uint64_t)(p - nLow) * (plan.nTiles + kSegTilePad) * kStampSlots
                                   : nullptr,
-                         sqw, codec == kCodecPlanes ? base + nLow * kBins : nullptr);
+                         sqw, nullptr);
     };
     // planes: the codec and the whole-key body of one pass in one launch
-    // (thrs_pass_seg2, mode-dispatched)
+    // (thrs_pass_seg2, mode-dispatched; kCodecPlanes: image-space input,
+    // identity map, digit at bits 16-23 of k')
     auto launch_seg2 = [&](int p, bool top) {
       ProfScope prof(stream, 1, THRS_PK_PASS_SEG, moveBytes);
       uint32_t* kA = top ? reinterpret_cast<uint32_t*>(loP) : reinterpret_cast<uint32_t*>(K);
@@ -746,7 +745,8 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                          grp[p & 1], static_cast<const uint32_t*>(mode), hiP,
                          g_stamps ? g_stamps + (uint64_t)(p - nLow) * (plan.nTiles + kSegTilePad) * kStampSlots
                                   : nullptr,
-                         sqw);
+                         sqw, reinterpret_cast<const typename ValueWord<kVB4>::T*>(top ? valOut : V),
+                         reinterpret_cast<typename ValueWord<kVB4>::T*>(top ? V : valOut));
     };
     const uint64_t sw = plan.wideStatus ? 8 : 4;
     const int setB = (nLow + 1) & 1;
@@ -800,7 +800,8 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
           auto lk = atomicRank ? thrs_local_pairs<KT, true, LG> : thrs_local_pairs<KT, false, LG>;
           hipLaunchKernelGGL(lk, lgrid, dim3(LG::THREADS), LG::template lds<U>(), stream,
                              reinterpret_cast<uint32_t*>(K), reinterpret_cast<uint32_t*>(V), km32, chunkOff, chunkB0,
-                             meta, sqw, zeroLog ? meta + kMetaNegZero : nullptr);
+                             meta, sqw, zeroLog ? meta + kMetaNegZero : nullptr,
+                             planes ? static_cast<const uint16_t*>(lo2P) : nullptr);
         };
         if (P.tinyPairs) launch_pairs(LocTiny{});
         else if (smallLocal) launch_pairs(LocSmall{});

@@ -1210,18 +1210,19 @@ __device__ __forceinline__ uint32_t loc_pad(uint32_t b0, int nLow, int startBits
 // chunk (repeats of its last key: no extra HBM traffic); a wave past the
 // chunk's end loads nothing.  Callers select per lane (r[j] is garbage for
 // slots past the chunk).
-template <int KPT, typename T>
-__device__ __forceinline__ void load_run(T (&r)[KPT], const T* __restrict__ chunk, uint32_t myOff, uint32_t size,
+// (R: the register type, e.g. u16 plane entries loaded into u32 registers)
+template <int KPT, typename R, typename T>
+__device__ __forceinline__ void load_run(R (&r)[KPT], const T* __restrict__ chunk, uint32_t myOff, uint32_t size,
                                          int32_t avail) {
   if (avail <= 0) return;
   if (avail >= 64 * KPT) {
     const T* p = chunk + myOff;
 #pragma unroll
-    for (int j = 0; j < KPT; ++j) r[j] = p[j * 64];
+    for (int j = 0; j < KPT; ++j) r[j] = (R)p[j * 64];
   } else {
     const uint32_t last = size - 1;
 #pragma unroll
-    for (int j = 0; j < KPT; ++j) r[j] = chunk[min(myOff + (uint32_t)(j * 64), last)];
+    for (int j = 0; j < KPT; ++j) r[j] = (R)chunk[min(myOff + (uint32_t)(j * 64), last)];
   }
 }
 
@@ -2198,12 +2199,14 @@ __global__ __launch_bounds__(LocCount::THREADS) void thrs_local_count16(
 // image, so they cannot be rebuilt bit-exactly) are permuted the same way.
 // thrs_local_pairs' items: low 16 image bits << 16 | chunk position.  (A
 // function, not a with_map lambda: the closure costs registers.)
+// plane: it[] holds the u16 plane's entries (the images' low 16 bits) already
 template <int KT, int KPT, typename KM>
-__device__ __forceinline__ void pairs_items(uint32_t (&it)[KPT], KM km, uint32_t myOff, int32_t lim) {
+__device__ __forceinline__ void pairs_items(uint32_t (&it)[KPT], KM km, uint32_t myOff, int32_t lim, bool plane = false) {
 #pragma unroll
   for (int j = 0; j < KPT; ++j) {
     const uint32_t pos = myOff + j * 64;
-    it[j] = (j * 64 < lim) ? (((uint32_t)kimg<KT>(km, it[j]) << 16) | pos) : 0xFFFF0000u;  // padding: digits 255
+    const uint32_t lo16 = plane ? it[j] : (uint32_t)kimg<KT>(km, it[j]);
+    it[j] = (j * 64 < lim) ? ((lo16 << 16) | pos) : 0xFFFF0000u;  // padding: digits 255
   }
 }
 
@@ -2211,7 +2214,7 @@ template <int KT, bool ATOMIC_RANK, typename LG>
 __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(LG::WPE))) void thrs_local_pairs(
     uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, KeyMap<uint32_t> km,
     const uint32_t* __restrict__ chunkOff, const uint32_t* __restrict__ chunkB0, const uint32_t* __restrict__ meta,
-    const SqueezeWords* __restrict__ sq, const uint32_t* __restrict__ zeroFlag) {
+    const SqueezeWords* __restrict__ sq, const uint32_t* __restrict__ zeroFlag, const uint16_t* __restrict__ lo) {
   constexpr int KPT = LG::KPT;
   constexpr uint32_t CHUNK = 64 * KPT;
   const uint32_t c = blockIdx.x;
@@ -2235,13 +2238,19 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(LG:
   const uint32_t myOff = w * CHUNK + lane;
   const int32_t avail = __builtin_amdgcn_readfirstlane((int32_t)ch.size - (int32_t)(w * CHUNK));
   uint32_t it[KPT];
-  load_run<KPT>(it, keys + ch.start, myOff, ch.size, avail);
-  // (the squeeze, f32 keys: only the items' images depend on it)
+  // lo != nullptr (u32 keys): the top-digit passes wrote the images' low 16
+  // bits to the u16 plane lo (kCodecPlanes) -- unless they ran on whole keys
+  // (mode 1, big chunks) or not at all (mode 2), which leaves the keys
   if constexpr (kSqueezable<KT>) {
+    // (the squeeze, f32 keys: only the items' images depend on it)
+    load_run<KPT>(it, keys + ch.start, myOff, ch.size, avail);
     if (sq && sq->on) pairs_items<KT, KPT>(it, half_map(km, sq, (int)(hiImg >> 31)), myOff, lim);
     else pairs_items<KT, KPT>(it, km, myOff, lim);
   } else {
-    pairs_items<KT, KPT>(it, km, myOff, lim);
+    const bool plane = KT == 0 && lo && meta[kMetaMode] == 0;
+    if (plane) load_run<KPT>(it, lo + ch.start, myOff, ch.size, avail);
+    else load_run<KPT>(it, keys + ch.start, myOff, ch.size, avail);
+    pairs_items<KT, KPT>(it, km, myOff, lim, plane);
   }
   loc_rounds<0, ATOMIC_RANK, LG>(it, ch, KeyMap<uint32_t>{0u, 0u, 0u}, 16, 2, smem, nullptr);
   pin(reinterpret_cast<uint32_t&>(lim));

@@ -852,9 +852,10 @@ struct GroupWalk {
 // which is the order the stable rank walks.  Keys past n read as 0.
 // keyStart / valid: the tile's first key and key count (tile * TILE and
 // min(TILE, n - tile * TILE) except in segmented passes).
-// Key codecs of the pass kernels.  The bucket path for u32 keys without
-// values (thrs_hybrid.hpp, thrs_local16) carries only what the next step
-// reads, in two planes instead of the 4-byte keys:
+// Key codecs of the pass kernels.  The bucket path for u32 / f32 keys without
+// values (thrs_hybrid.hpp, thrs_local16) and for u32 keys with 4-byte values
+// (thrs_local_pairs; the values travel as they are) carries only what the
+// next step reads, in two planes instead of the 4-byte keys:
 //   kCodecKeys    keys in, keys out
 //   kCodecSplit   keys in; out: the image's low 16 bits to the u16 plane
 //                 (keysOut) and its top byte to the u8 plane (hiPlane) -- the
@@ -884,8 +885,15 @@ __device__ __forceinline__ void load_tile(const typename KeyTraits<KT>::U* __res
   const uint64_t chunkBase = keyStart + w * CHUNK;
   int32_t lim = (int32_t)valid - (int32_t)(w * CHUNK + lane);  // item j is real iff j*64 < lim
   pin(reinterpret_cast<uint32_t&>(lim));
+  // the values (pairs): issued after the keys, before anything waits on them
+  auto load_vals = [&]() __attribute__((always_inline)) {
+    if constexpr (VB != 0) {
+#pragma unroll
+      for (int j = 0; j < KPT; ++j) v[j] = (valid == T || j * 64 < lim) ? valsIn[chunkBase + j * 64 + lane] : VW{};
+    }
+  };
   if constexpr (CODEC == kCodecPlanes) {
-    static_assert(sizeof(U) == 4 && VB == 0, "planes: u32 keys without values");
+    static_assert(sizeof(U) == 4 && (VB == 0 || VB == 4), "planes: u32 keys, no values or 4-byte values");
     const uint16_t* lo = reinterpret_cast<const uint16_t*>(keysIn);
     if constexpr (KPT % 4 == 0) {
       // vec (a whole tile, keyStart a multiple of 4, inside ONE second-digit
@@ -897,7 +905,7 @@ __device__ __forceinline__ void load_tile(const typename KeyTraits<KT>::U* __res
       // a keys-only sort can see: every key of the tile lands in the same
       // bucket run, and the order inside a bucket is the local sort's
       // (docs/EXPERIMENTS.md row 107).
-      if (vec) {
+      if (vec) {  // (keys only: thrs_pass_seg_body)
         const uint2* lq = reinterpret_cast<const uint2*>(lo + chunkBase) + lane;
         const uint32_t* hq = reinterpret_cast<const uint32_t*>(hiIn + chunkBase) + lane;
         uint2 l2[KPT / 4];
@@ -945,6 +953,7 @@ __device__ __forceinline__ void load_tile(const typename KeyTraits<KT>::U* __res
 #pragma unroll
         for (int j = 0; j < KPT; ++j) k[j] = (j * 64 < lim) ? (U)lo[chunkBase + j * 64 + lane] : (U)0;
       }
+      load_vals();
       // byte (a + 64j + lane) of the window: dword 16j + (a + lane) / 4 --
       // lane (that & 63) of load j/4, or of load j/4 + 1 past the end of a
       // 256-byte load (j % 4 == 3, a + lane >= 64)
@@ -972,6 +981,7 @@ __device__ __forceinline__ void load_tile(const typename KeyTraits<KT>::U* __res
 #pragma unroll
       for (int j = 0; j < KPT; ++j) k[j] = (j * 64 < lim) ? ld(chunkBase + j * 64 + lane) : (U)0;
     }
+    load_vals();
     return;
   }
   if (valid == T) {
@@ -981,10 +991,7 @@ __device__ __forceinline__ void load_tile(const typename KeyTraits<KT>::U* __res
 #pragma unroll
     for (int j = 0; j < KPT; ++j) k[j] = (j * 64 < lim) ? keysIn[chunkBase + j * 64 + lane] : (U)0;
   }
-  if constexpr (VB != 0) {
-#pragma unroll
-    for (int j = 0; j < KPT; ++j) v[j] = (valid == T || j * 64 < lim) ? valsIn[chunkBase + j * 64 + lane] : VW{};
-  }
+  load_vals();
 }
 
 // keys in tile `tile` of an unsegmented pass over n keys
@@ -1012,7 +1019,7 @@ __device__ __forceinline__ void pass_tile(
   using U = typename KeyTraits<KT>::U;
   using VW = typename ValueWord<VB>::T;
   using G = PassGeom<sizeof(U), VB>;
-  static_assert(CODEC == kCodecKeys || (sizeof(U) == 4 && VB == 0), "codecs: u32 keys only");
+  static_assert(CODEC == kCodecKeys || (sizeof(U) == 4 && (VB == 0 || VB == 4)), "codecs: 4-byte keys, <= 4-byte values");
   constexpr int WAVES = G::WAVES, KPT = G::KPT, ROUNDS = G::ROUNDS, THREADS = G::THREADS;
   constexpr uint32_t T = G::TILE, STAGE = G::STAGE, CHUNK = 64 * KPT;
   constexpr int STAGE_SHIFT = __builtin_ctz(STAGE);
@@ -1614,7 +1621,8 @@ __device__ __forceinline__ void thrs_pass_seg_body(
   constexpr uint32_t T = G::TILE;
   // the planes codec (the top-digit pass over second-digit regions): whole,
   // aligned tiles inside one region take the vector loads (load_tile)
-  constexpr bool kVec = CODEC == kCodecPlanes && G::KPT % 4 == 0;
+  // (keys only: with values the rank must walk the keys in input order)
+  constexpr bool kVec = CODEC == kCodecPlanes && VB == 0 && G::KPT % 4 == 0;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint32_t* s_cnt = reinterpret_cast<uint32_t*>(smem + G::STAGE * (sizeof(U) + VB));
   uint32_t* s_misc = s_cnt + (G::WAVES + 1) * kBins;
@@ -1717,7 +1725,8 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
 }
 
 // The bucket path's two launches of one top-digit pass in ONE (u32 / f32 keys
-// without values, planes on): the plan's mode picks the body -- mode 0 the
+// without values, or u32 keys with 4-byte values, planes on; the values move
+// the same way in both bodies): the plan's mode picks the body -- mode 0 the
 // key-plane codec CODEC_A (kCodecSplit: keys in, planes out; kCodecPlanes:
 // planes in, a plane out, image space KTA), modes 1 / 3 whole keys
 // (kCodecKeys, KTB), mode 2 neither.  A gated launch that does nothing still
@@ -1730,15 +1739,17 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<4, VB>::WPE))) void thrs_pass_seg2(
     const uint32_t* __restrict__ secondBaseA, const uint32_t* __restrict__ kinB, uint32_t* __restrict__ koutB,
     KeyMap<uint32_t> kmB, int shiftB, uint32_t* __restrict__ segInfo, const uint32_t* __restrict__ segBase,
     ST* __restrict__ status, uint32_t* __restrict__ errFlag, GroupTables<ST> grp, const uint32_t* __restrict__ mode,
-    uint8_t* __restrict__ hiPlane, uint64_t* __restrict__ stamps, const SqueezeWords* __restrict__ sq) {
-  static_assert(sizeof(typename KeyTraits<KTA>::U) == 4 && sizeof(typename KeyTraits<KTB>::U) == 4 && VB == 0,
-                "4-byte keys without values");
+    uint8_t* __restrict__ hiPlane, uint64_t* __restrict__ stamps, const SqueezeWords* __restrict__ sq,
+    const typename ValueWord<VB>::T* __restrict__ valsIn, typename ValueWord<VB>::T* __restrict__ valsOut) {
+  static_assert(sizeof(typename KeyTraits<KTA>::U) == 4 && sizeof(typename KeyTraits<KTB>::U) == 4 &&
+                    (VB == 0 || VB == 4),
+                "4-byte keys, no values or 4-byte values");
   const uint32_t m = *mode;
   if (m == 0)
-    thrs_pass_seg_body<KTA, VB, ST, ATOMIC_RANK, CODEC_A>(kinA, koutA, nullptr, nullptr, kmA, shiftA, segInfo, segBase,
+    thrs_pass_seg_body<KTA, VB, ST, ATOMIC_RANK, CODEC_A>(kinA, koutA, valsIn, valsOut, kmA, shiftA, segInfo, segBase,
                                                           status, errFlag, grp, hiPlane, stamps, sq, secondBaseA);
   else if (m == 1 || m == 3)
-    thrs_pass_seg_body<KTB, VB, ST, ATOMIC_RANK, kCodecKeys>(kinB, koutB, nullptr, nullptr, kmB, shiftB, segInfo,
+    thrs_pass_seg_body<KTB, VB, ST, ATOMIC_RANK, kCodecKeys>(kinB, koutB, valsIn, valsOut, kmB, shiftB, segInfo,
                                                              segBase, status, errFlag, grp, nullptr, stamps, sq,
                                                              nullptr);
 }
