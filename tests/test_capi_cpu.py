@@ -149,7 +149,7 @@ def test_path_info_matches_the_configs():
     assert c3["min_bytes"] == (4 + 15 + 13 + 14) * (1 << 30)
     c3off = info(U32, T.ValueType.U32, 1 << 30, True, planes="off")
     assert not c3off["planes"] and c3off["min_bytes"] == (4 + 16 + 16 + 16) * (1 << 30)
-    assert not info(F32, T.ValueType.U32, 1 << 30, True)["planes"]        # f32 pairs: whole keys
+    assert info(F32, T.ValueType.U32, 1 << 30, True)["planes"]            # f32 pairs too
     assert not info(U32, T.ValueType.U64, 1 << 30, True)["planes"]        # 8-byte values: whole keys
     c4 = info(F32, T.ValueType.U32, 1 << 28, False)
     assert (c4["path"], c4["local"], c4["planes"], c4["local_cap"]) == ("bucket", "thrs_local16", True, 9216)

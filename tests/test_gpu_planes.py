@@ -16,9 +16,10 @@ of RadixSort::sort (tinyhipradixsort.hpp:854-944), key for key:
 * a FORCED bucket path at small n with a distribution that puts the keys in
   four second-digit regions, so nearly every top-pass tile is a vector tile.
 
-u32 keys with u32 values carry the keys as the same planes (no vector tiles:
-the values keep input order), so their keys AND values are compared with the
-oracle's, which checks the stable order of equal keys through the codecs.
+u32 / f32 keys with u32 values carry the keys as the same planes (no vector
+tiles: the values keep input order), so their keys AND values are compared
+with the oracle's, which checks the stable order of equal keys through the
+codecs.  f32 pairs with a -0 key run whole keys (mode 3).
 
 Each planes case asserts pathInfo()['planes'] and that the vector branch ran
 (thrs_debug_vector_tiles, a counter the top-digit pass keeps)."""
@@ -251,3 +252,51 @@ def test_forced_bucket_planes_vs_noplanes(gpu, kt, desc):
         assert rs.pathInfo(n, 0, 32, False)["planes"] == (planes == "auto")
         tiles = T.debug_vector_tiles(tmp, kt, n)
         assert (tiles > 0) == (planes == "auto"), (planes, tiles)
+
+
+def _f32_pairs_keys(n, seed, neg_zero):
+    """Raw f32 bits with NaN / Inf / denormal specials, +0 keys and, if asked,
+    -0 keys (which send f32 pairs to mode 3: +0 and -0 share one image)."""
+    k = _f32_raw_keys(n, seed)
+    if not neg_zero:
+        k[k == np.uint32(0x80000000)] = 0
+    return k
+
+
+@pytest.mark.parametrize("desc", [False, True])
+@pytest.mark.parametrize("neg_zero", [False, True])
+@pytest.mark.parametrize("geom", ["small", "big"])
+def test_forced_bucket_f32_pairs_planes_vs_oracle(gpu, geom, neg_zero, desc):
+    """f32 pairs on a forced bucket path: planes (mode 0) without a -0, whole
+    keys (mode 3) with one; keys (raw bits: NaN payloads, signed zeros) and
+    values bit-exact against the oracle."""
+    torch = gpu
+    n = 3 * (1 << 20) + 4321
+    keys = _f32_pairs_keys(n, 6900 + int(desc) + 2 * int(neg_zero), neg_zero)
+    vals = np.arange(n, dtype=np.uint32)
+    rs = _sorter(O.F32, 4, desc, path="bucket", localGeometry=geom)
+    assert rs.pathInfo(n, 0, 32, True)["planes"]
+    k, v, tmp = _sort_on_gpu(torch, rs, O.F32, keys, vals)
+    assert rs.debugBucketMode(tmp, n, True)[0] == (3 if neg_zero else 0)
+    ek, ev = O.lsd_sort(O.F32, keys, vals, 0, 32, desc)
+    assert np.array_equal(k, ek)
+    assert np.array_equal(v, ev)
+
+
+@pytest.mark.large
+@pytest.mark.parametrize("neg_zero", [False, True])
+def test_f32_pairs_default_path_vs_oracle(gpu, neg_zero):
+    """f32 pairs at 100M, the default bucket path's lower bound (planes, the
+    squeeze may go on): keys and values against the oracle."""
+    torch = gpu
+    n = 100_000_000
+    keys = _f32_pairs_keys(n, 7000 + int(neg_zero), neg_zero)
+    vals = np.arange(n, dtype=np.uint32)
+    rs = _sorter(O.F32, 4, False)
+    info = rs.pathInfo(n, 0, 32, True)
+    assert (info["path"], info["local"], info["planes"]) == ("bucket", "thrs_local_pairs", True)
+    k, v, tmp = _sort_on_gpu(torch, rs, O.F32, keys, vals)
+    assert rs.debugBucketMode(tmp, n, True)[0] == (3 if neg_zero else 0)
+    ek, ev = O.lsd_sort(O.F32, keys, vals, 0, 32, False)
+    assert np.array_equal(k, ek)
+    assert np.array_equal(v, ev)

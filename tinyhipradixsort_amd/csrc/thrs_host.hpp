@@ -167,12 +167,13 @@ inline Plan make_plan(int keyType, int valueBytesOrZero, uint32_t n) {
   // range): the default takes it from kBucketMinKeysU32 / kBucketMinKeys4, and
   // a bucket path forced below that carries the planes too, so the codecs the
   // headline runs are tested element-wise at sizes the oracle finishes.
-  // u32 keys with 4-byte values likewise, up to 2^30 + 2^26 (the u16 planes
+  // u32 / f32 keys with 4-byte values likewise, up to 2^30 + 2^26 (the u16 planes
   // fill keyOut, the values take valueOut as ever).
   p.hiPlaneOff = p.scratchBytes;
   if (((keyType == THRS_KEY_U32 || keyType == THRS_KEY_F32) && valueBytesOrZero == 0 &&
        (uint64_t)n <= (1ull << 31) + (1ull << 25)) ||
-      (keyType == THRS_KEY_U32 && valueBytesOrZero == 4 && (uint64_t)n <= (1ull << 30) + (1ull << 26)))
+      ((keyType == THRS_KEY_U32 || keyType == THRS_KEY_F32) && valueBytesOrZero == 4 &&
+       (uint64_t)n <= (1ull << 30) + (1ull << 26)))
     p.scratchBytes += round_up(n, kAlign);
   return p;
 }
@@ -324,9 +325,9 @@ PathSel select_path(uint32_t n, int startBits, int nPass, const thrs_options& op
   // keyOut (4n bytes) = lo u16[n] | lo2 u16[n], the u8 plane hi[n] at the end
   // of the scratch.  f32: -0 and +0 share one image, so a plan that saw a -0
   // key (thrs_hist_joint) runs the whole-key passes instead (mode 3)
-  // (u32 keys + 4-byte values: thrs_local_pairs over the lo2 plane, the
-  // values as they are)
-  const bool planes = ((local16 && (KT == 0 || KT == 2)) || (KT == 0 && VB == 4 && bucket && fullWindow)) && segA &&
+  // (u32 / f32 keys + 4-byte values: thrs_local_pairs over the lo2 plane,
+  // the values as they are; f32 with a -0 likewise runs whole keys, mode 3)
+  const bool planes = (KT == 0 || KT == 2) && ((local16) || (VB == 4 && bucket && fullWindow)) && segA &&
                       opt.planes != THRS_PLANES_OFF && plan.scratchBytes - plan.hiPlaneOff >= (uint64_t)n;
   // the local sort's chunk capacity (a bigger bucket is a big chunk)
   const uint32_t cap = kKV ? LocKV::CAP
@@ -455,8 +456,8 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   // never launched).  The planes codec reads images (identity map): the u32
   // kernel serves both key types.
   constexpr bool kPlanesK = (KT == 0 || KT == 2) && VB == 0;
-  constexpr bool kPlanesP = KT == 0 && VB == 4;
-  constexpr int kKT4 = kPlanesK ? KT : 0;
+  constexpr bool kPlanesP = (KT == 0 || KT == 2) && VB == 4;
+  constexpr int kKT4 = kPlanesK || kPlanesP ? KT : 0;
   constexpr int kVB4 = kPlanesP ? 4 : 0;
   auto sk2Split = atomicRank ? thrs_pass_seg2<kKT4, kKT4, kVB4, ST, true, kCodecSplit>
                              : thrs_pass_seg2<kKT4, kKT4, kVB4, ST, false, kCodecSplit>;
@@ -600,7 +601,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                            reinterpret_cast<uint32_t*>(hyb + kBigPosOff), reinterpret_cast<uint32_t*>(hyb + kBigTileOff),
                            reinterpret_cast<uint4*>(scratch + plan.bigHistOff), nLow,
                            sqMode == 1 ? static_cast<const SqueezeWords*>(sample) : nullptr,
-                           planes && VB == 0 ? 1 : 0,  // (aligned top-pass tiles: the vector loads, keys only)
+                           planes ? (VB ? 2 : 1) : 0,  // (2: pairs, any -0 -> mode 3)
                            err, g_inject);
       };
       if (!local32 && squeeze) {

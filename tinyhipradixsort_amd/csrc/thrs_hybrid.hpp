@@ -836,10 +836,11 @@ __global__ __launch_bounds__(kPlanRowThreads) void thrs_plan_rows(
     if (!(sqMode == 1 && load_agent(&meta[kMetaRehist]) != 0u)) {
       plan_big_prefix(joint, meta, bigB, bigPos, bigTile, tileKeys, cap, s_w, errFlag, inject);
       // f32 with a -0 key: whole keys through the top-digit passes (mode 3)
-      // (more zeros than the zero log holds: thrs_local16 could not restore
-      // the -0 signs from the planes)
+      // (keys only: more zeros than the zero log holds, thrs_local16 could
+      // not restore the -0 signs from the planes; pairs, planes == 2: any -0,
+      // thrs_local_pairs then moves the keys by position)
       if (t == 0 && planes && load_agent(&meta[kMetaNegZero]) != 0u &&
-          load_agent(&meta[kMetaZeroCount]) > kZeroLogCap && load_agent(&meta[kMetaMode]) == 0u)
+          (planes == 2 || load_agent(&meta[kMetaZeroCount]) > kZeroLogCap) && load_agent(&meta[kMetaMode]) == 0u)
         meta[kMetaMode] = 3;
     }
     __syncthreads();  // s_w is reused below
@@ -2238,18 +2239,19 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(LG:
   const uint32_t myOff = w * CHUNK + lane;
   const int32_t avail = __builtin_amdgcn_readfirstlane((int32_t)ch.size - (int32_t)(w * CHUNK));
   uint32_t it[KPT];
-  // lo != nullptr (u32 keys): the top-digit passes wrote the images' low 16
-  // bits to the u16 plane lo (kCodecPlanes) -- unless they ran on whole keys
-  // (mode 1, big chunks) or not at all (mode 2), which leaves the keys
+  // lo != nullptr: the top-digit passes wrote the images' low 16 bits to the
+  // u16 plane lo (kCodecPlanes) -- unless they ran on whole keys (mode 1, big
+  // chunks; mode 3, f32 with a -0) or not at all (mode 2), which leaves the
+  // keys
+  const bool plane = lo && meta[kMetaMode] == 0;
+  if (plane) load_run<KPT>(it, lo + ch.start, myOff, ch.size, avail);
+  else load_run<KPT>(it, keys + ch.start, myOff, ch.size, avail);
   if constexpr (kSqueezable<KT>) {
-    // (the squeeze, f32 keys: only the items' images depend on it)
-    load_run<KPT>(it, keys + ch.start, myOff, ch.size, avail);
-    if (sq && sq->on) pairs_items<KT, KPT>(it, half_map(km, sq, (int)(hiImg >> 31)), myOff, lim);
-    else pairs_items<KT, KPT>(it, km, myOff, lim);
+    // (the squeeze, f32 keys: only the items' images depend on it; the
+    // plane holds squeezed images already)
+    if (!plane && sq && sq->on) pairs_items<KT, KPT>(it, half_map(km, sq, (int)(hiImg >> 31)), myOff, lim);
+    else pairs_items<KT, KPT>(it, km, myOff, lim, plane);
   } else {
-    const bool plane = KT == 0 && lo && meta[kMetaMode] == 0;
-    if (plane) load_run<KPT>(it, lo + ch.start, myOff, ch.size, avail);
-    else load_run<KPT>(it, keys + ch.start, myOff, ch.size, avail);
     pairs_items<KT, KPT>(it, km, myOff, lim, plane);
   }
   loc_rounds<0, ATOMIC_RANK, LG>(it, ch, KeyMap<uint32_t>{0u, 0u, 0u}, 16, 2, smem, nullptr);
