@@ -88,11 +88,12 @@ typedef struct thrs_options {
   int32_t rank;          /* THRS_RANK_*: in-tile rank by lane-ordered LDS atomics
                             (AUTO: where the per-device probe confirms the order) or
                             by the 8-ballot match                                    */
-  int32_t planes;        /* THRS_PLANES_*: u32 keys-only bucket path with 16-bit items:
-                            the top-digit passes carry the keys as a u16 + a u8
-                            plane (12 instead of 16 bytes per key over the two
-                            passes, 6 instead of 8 in the local sort).  AUTO = ON
-                            where it applies; OFF = full keys                      */
+  int32_t planes;        /* THRS_PLANES_*: u32 / f32 keys on the bucket path, without
+                            values or with 4-byte values: the top-digit passes carry
+                            the keys as a u16 + a u8 plane (12 instead of 16 bytes
+                            per key over the two passes, 6 instead of 8 in the local
+                            sort; values as they are).  AUTO = ON where it applies;
+                            OFF = full keys                                         */
   int32_t keyRange;      /* 1: the caller promises rangeLo <= img(k) <= rangeHi for every
                             key, img(k) = getKeyBits(k) ^ (descending ? ~0 : 0) (fpKey.hpp
                             and kernel.cu:18-24), and a full-window sort orders by
@@ -266,7 +267,7 @@ enum { THRS_LOCALK_NONE = 0, THRS_LOCALK_16 = 1, THRS_LOCALK_32 = 2, THRS_LOCALK
 typedef struct thrs_path_info {
   int32_t path;          /* 0 = one device pass per digit (LSD), 1 = bucket path          */
   int32_t local;         /* the bucket path's local sort: THRS_LOCALK_*                     */
-  int32_t planes;        /* 1: u32 keys cross the top-digit passes as a u16 + u8 plane     */
+  int32_t planes;        /* 1: 4-byte keys cross the top-digit passes as u16 + u8 planes   */
   int32_t devicePasses;  /* device-wide digit passes of one sort                           */
   uint64_t minBytes;     /* HBM bytes read + written by one sort, histogram included      */
   uint64_t localCap;     /* keys per local-sort chunk (a bigger bucket takes the fallback) */

@@ -19,7 +19,8 @@ of RadixSort::sort (tinyhipradixsort.hpp:854-944), key for key:
 u32 / f32 keys with u32 values carry the keys as the same planes (no vector
 tiles: the values keep input order), so their keys AND values are compared
 with the oracle's, which checks the stable order of equal keys through the
-codecs.  f32 pairs with a -0 key run whole keys (mode 3).
+codecs.  f32 pairs take the zeros' signs from the zero log (mode 0) up to
+1024 zeros, and run whole keys (mode 3) past that when a -0 is among them.
 
 Each planes case asserts pathInfo()['planes'] and that the vector branch ran
 (thrs_debug_vector_tiles, a counter the top-digit pass keeps)."""
@@ -254,49 +255,58 @@ def test_forced_bucket_planes_vs_noplanes(gpu, kt, desc):
         assert (tiles > 0) == (planes == "auto"), (planes, tiles)
 
 
-def _f32_pairs_keys(n, seed, neg_zero):
-    """Raw f32 bits with NaN / Inf / denormal specials, +0 keys and, if asked,
-    -0 keys (which send f32 pairs to mode 3: +0 and -0 share one image)."""
+def _f32_pairs_keys(n, seed, zeros):
+    """Raw f32 bits with NaN / Inf / denormal specials and signed zeros:
+    "plus" (600 +0), "signed" (600 zeros, a third -0: within the zero log) or
+    "many" (3000 zeros, a third -0: past the log's 1024, mode 3)."""
     k = _f32_raw_keys(n, seed)
-    if not neg_zero:
+    if zeros == "plus":
         k[k == np.uint32(0x80000000)] = 0
+    elif zeros == "many":
+        pos = np.random.default_rng(seed + 1).choice(n, 3000, replace=False)
+        k[pos] = np.where(np.arange(3000) % 3 == 1, np.uint32(0x80000000), np.uint32(0))
     return k
 
 
+_F32_PAIRS_MODE = {"plus": 0, "signed": 0, "many": 3}
+
+
 @pytest.mark.parametrize("desc", [False, True])
-@pytest.mark.parametrize("neg_zero", [False, True])
-@pytest.mark.parametrize("geom", ["small", "big"])
-def test_forced_bucket_f32_pairs_planes_vs_oracle(gpu, geom, neg_zero, desc):
-    """f32 pairs on a forced bucket path: planes (mode 0) without a -0, whole
-    keys (mode 3) with one; keys (raw bits: NaN payloads, signed zeros) and
-    values bit-exact against the oracle."""
+@pytest.mark.parametrize("zeros", ["plus", "signed", "many"])
+@pytest.mark.parametrize("geom", ["tiny16", "small", "big"])
+def test_forced_bucket_f32_pairs_planes_vs_oracle(gpu, geom, zeros, desc):
+    """f32 pairs on a forced bucket path (every pairs geometry, tiny16
+    included): planes (mode 0) with +0 only or up to 1024 signed zeros (the
+    zero log restores their signs in the zeros' chunk), whole keys (mode 3)
+    past that; keys (raw bits: NaN payloads, signed zeros) and values
+    bit-exact against the oracle."""
     torch = gpu
     n = 3 * (1 << 20) + 4321
-    keys = _f32_pairs_keys(n, 6900 + int(desc) + 2 * int(neg_zero), neg_zero)
+    keys = _f32_pairs_keys(n, 6900 + int(desc) + 2 * len(zeros) + len(geom), zeros)
     vals = np.arange(n, dtype=np.uint32)
     rs = _sorter(O.F32, 4, desc, path="bucket", localGeometry=geom)
     assert rs.pathInfo(n, 0, 32, True)["planes"]
     k, v, tmp = _sort_on_gpu(torch, rs, O.F32, keys, vals)
-    assert rs.debugBucketMode(tmp, n, True)[0] == (3 if neg_zero else 0)
+    assert rs.debugBucketMode(tmp, n, True)[0] == _F32_PAIRS_MODE[zeros]
     ek, ev = O.lsd_sort(O.F32, keys, vals, 0, 32, desc)
     assert np.array_equal(k, ek)
     assert np.array_equal(v, ev)
 
 
 @pytest.mark.large
-@pytest.mark.parametrize("neg_zero", [False, True])
-def test_f32_pairs_default_path_vs_oracle(gpu, neg_zero):
+@pytest.mark.parametrize("zeros", ["plus", "signed", "many"])
+def test_f32_pairs_default_path_vs_oracle(gpu, zeros):
     """f32 pairs at 100M, the default bucket path's lower bound (planes, the
     squeeze may go on): keys and values against the oracle."""
     torch = gpu
     n = 100_000_000
-    keys = _f32_pairs_keys(n, 7000 + int(neg_zero), neg_zero)
+    keys = _f32_pairs_keys(n, 7000 + len(zeros), zeros)
     vals = np.arange(n, dtype=np.uint32)
     rs = _sorter(O.F32, 4, False)
     info = rs.pathInfo(n, 0, 32, True)
     assert (info["path"], info["local"], info["planes"]) == ("bucket", "thrs_local_pairs", True)
     k, v, tmp = _sort_on_gpu(torch, rs, O.F32, keys, vals)
-    assert rs.debugBucketMode(tmp, n, True)[0] == (3 if neg_zero else 0)
+    assert rs.debugBucketMode(tmp, n, True)[0] == _F32_PAIRS_MODE[zeros]
     ek, ev = O.lsd_sort(O.F32, keys, vals, 0, 32, False)
     assert np.array_equal(k, ek)
     assert np.array_equal(v, ev)

@@ -601,7 +601,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
                            reinterpret_cast<uint32_t*>(hyb + kBigPosOff), reinterpret_cast<uint32_t*>(hyb + kBigTileOff),
                            reinterpret_cast<uint4*>(scratch + plan.bigHistOff), nLow,
                            sqMode == 1 ? static_cast<const SqueezeWords*>(sample) : nullptr,
-                           planes ? (VB ? 2 : 1) : 0,  // (2: pairs, any -0 -> mode 3)
+                           planes ? (VB ? 2 : 1) : 0,  // (2: with values, no aligned tiles)
                            err, g_inject);
       };
       if (!local32 && squeeze) {
@@ -802,7 +802,7 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
           hipLaunchKernelGGL(lk, lgrid, dim3(LG::THREADS), LG::template lds<U>(), stream,
                              reinterpret_cast<uint32_t*>(K), reinterpret_cast<uint32_t*>(V), km32, chunkOff, chunkB0,
                              meta, sqw, zeroLog ? meta + kMetaNegZero : nullptr,
-                             planes ? static_cast<const uint16_t*>(lo2P) : nullptr);
+                             planes ? static_cast<const uint16_t*>(lo2P) : nullptr, zeroLog);
         };
         if (P.tinyPairs) launch_pairs(LocTiny{});
         else if (smallLocal) launch_pairs(LocSmall{});

@@ -760,7 +760,8 @@ __global__ __launch_bounds__(kPlanRowThreads) void thrs_plan_rows(
     uint32_t* __restrict__ segInfo, uint32_t* __restrict__ segBase, uint32_t tileKeys, uint32_t histGrid,
     uint32_t* __restrict__ segInfoA, uint32_t* __restrict__ segBaseA, uint32_t* __restrict__ bigB, int sqMode,
     int keyBits, uint32_t* __restrict__ bigPos, uint32_t* __restrict__ bigTile, uint4* __restrict__ bigHist,
-    int nLow, const SqueezeWords* __restrict__ sample, int planes, uint32_t* __restrict__ errFlag, int inject) {
+    int nLow, const SqueezeWords* __restrict__ sample, int planes /* 0 none, 1 keys only, 2 with values */,
+    uint32_t* __restrict__ errFlag, int inject) {
   if (sqMode == 2 && meta[kMetaRehist] == 0) return;
   __shared__ uint32_t s_w[2][4], s_base, s_b2[kBins], s_sq[3], s_last;
   const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6, r = blockIdx.x;
@@ -836,11 +837,10 @@ __global__ __launch_bounds__(kPlanRowThreads) void thrs_plan_rows(
     if (!(sqMode == 1 && load_agent(&meta[kMetaRehist]) != 0u)) {
       plan_big_prefix(joint, meta, bigB, bigPos, bigTile, tileKeys, cap, s_w, errFlag, inject);
       // f32 with a -0 key: whole keys through the top-digit passes (mode 3)
-      // (keys only: more zeros than the zero log holds, thrs_local16 could
-      // not restore the -0 signs from the planes; pairs, planes == 2: any -0,
-      // thrs_local_pairs then moves the keys by position)
+      // (more zeros than the zero log holds: thrs_local16 / thrs_local_pairs
+      // could not restore the -0 signs from the planes)
       if (t == 0 && planes && load_agent(&meta[kMetaNegZero]) != 0u &&
-          (planes == 2 || load_agent(&meta[kMetaZeroCount]) > kZeroLogCap) && load_agent(&meta[kMetaMode]) == 0u)
+          load_agent(&meta[kMetaZeroCount]) > kZeroLogCap && load_agent(&meta[kMetaMode]) == 0u)
         meta[kMetaMode] = 3;
     }
     __syncthreads();  // s_w is reused below
@@ -873,9 +873,10 @@ __global__ __launch_bounds__(kPlanRowThreads) void thrs_plan_rows(
     };
     uint32_t tiles = 0;
     // the top-digit pass's tiles are aligned when it reads the key planes
-    // (their vector loads, thrs_pass_seg_body); other codecs count tiles from
-    // the segment start (aligned tiles measured slower, docs/EXPERIMENTS.md row 85)
-    const bool align = top && planes;
+    // without values (their vector loads, thrs_pass_seg_body; planes == 2,
+    // pairs, take none); other codecs count tiles from the segment start
+    // (aligned tiles measured slower, docs/EXPERIMENTS.md row 85)
+    const bool align = top && planes == 1;
     info[kSegAlignWord] = align ? 1u : 0u;
     info[kSegVecWord] = 0;  // vector-load tiles of the top-digit pass (diagnostics)
     for (int sg = 0; sg <= kSegs; ++sg) {
@@ -1046,7 +1047,7 @@ __global__ __launch_bounds__(kPlanThreads) void thrs_plan(const uint32_t* __rest
   // second-digit pass (position ranges)
   if (tid == 0 || tid == 64) {
     const bool top = tid == 0;
-    constexpr bool planes = false;  // the 32-bit local sort's passes move keys
+    constexpr int planes = 0;  // the 32-bit local sort's passes move keys
     uint32_t* info = top ? segInfo : segInfoA;
     auto pos_of = [&](int sg) -> uint32_t {
       if (sg >= kSegs) return n;
@@ -1054,9 +1055,10 @@ __global__ __launch_bounds__(kPlanThreads) void thrs_plan(const uint32_t* __rest
     };
     uint32_t tiles = 0;
     // the top-digit pass's tiles are aligned when it reads the key planes
-    // (their vector loads, thrs_pass_seg_body); other codecs count tiles from
-    // the segment start (aligned tiles measured slower, docs/EXPERIMENTS.md row 85)
-    const bool align = top && planes;
+    // without values (their vector loads, thrs_pass_seg_body; planes == 2,
+    // pairs, take none); other codecs count tiles from the segment start
+    // (aligned tiles measured slower, docs/EXPERIMENTS.md row 85)
+    const bool align = top && planes == 1;
     info[kSegAlignWord] = align ? 1u : 0u;
     info[kSegVecWord] = 0;  // vector-load tiles of the top-digit pass (diagnostics)
     for (int sg = 0; sg <= kSegs; ++sg) {
@@ -2211,11 +2213,47 @@ __device__ __forceinline__ void pairs_items(uint32_t (&it)[KPT], KM km, uint32_t
   }
 }
 
+// f32 pairs from the key planes (mode 0) after a -0 was seen: the chunk of
+// +0's image takes its zeros' signs from the zero log, by loc16_write_zero_log's
+// rule (a zero's rank among the zeros = logged zeros at smaller input
+// positions: their stable order).  stage: the chunk's sorted items (image low
+// 16 bits << 16 | position); leaves the signs in negBits[kZeroLogCap / 32] and
+// returns the zeros' first slot.  Every thread of the workgroup calls it.
+template <typename LG>
+__device__ __attribute__((noinline)) uint32_t pairs_zero_signs(const uint32_t* stage, uint32_t size, uint32_t zlo,
+                                                               uint32_t* negBits, const uint32_t* __restrict__ zlog,
+                                                               uint32_t z) {
+  constexpr uint32_t CHUNK = 64 * LG::KPT;
+  static_assert(kZeroLogCap / 32 + 1 <= (uint32_t)LG::WAVES * kBins, "sign bits fit the counters' LDS");
+  uint32_t* s_s0 = negBits + kZeroLogCap / 32;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (uint32_t i = tid; i < kZeroLogCap / 32 + 1; i += LG::THREADS) negBits[i] = 0;
+  lds_barrier();
+  uint32_t below = 0;  // sorted items below the zeros' item: the run's start
+  for (int j = 0; j < LG::KPT; ++j) {
+    const uint32_t slot = w * CHUNK + 64 * j + lane;
+    if (slot < size) below += (stage[slot] >> 16) < zlo ? 1u : 0u;
+  }
+  atomicAdd(s_s0, below);
+  for (uint32_t e = tid; e < z; e += LG::THREADS) {
+    const uint32_t x = zlog[e];
+    if (x >> 31) {
+      const uint32_t p = x & 0x7FFFFFFFu;
+      uint32_t r = 0;
+      for (uint32_t f = 0; f < z; ++f) r += (zlog[f] & 0x7FFFFFFFu) < p ? 1u : 0u;
+      atomicOr(&negBits[r >> 5], 1u << (r & 31));
+    }
+  }
+  lds_barrier();
+  return *s_s0;
+}
+
 template <int KT, bool ATOMIC_RANK, typename LG>
 __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(LG::WPE))) void thrs_local_pairs(
     uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, KeyMap<uint32_t> km,
     const uint32_t* __restrict__ chunkOff, const uint32_t* __restrict__ chunkB0, const uint32_t* __restrict__ meta,
-    const SqueezeWords* __restrict__ sq, const uint32_t* __restrict__ zeroFlag, const uint16_t* __restrict__ lo) {
+    const SqueezeWords* __restrict__ sq, const uint32_t* __restrict__ zeroFlag, const uint16_t* __restrict__ lo,
+    const uint32_t* __restrict__ zeroLog) {
   constexpr int KPT = LG::KPT;
   constexpr uint32_t CHUNK = 64 * KPT;
   const uint32_t c = blockIdx.x;
@@ -2262,17 +2300,34 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(LG:
   uint32_t* stage = reinterpret_cast<uint32_t*>(smem);
   const uint32_t* stw = stage + w * CHUNK + lane;
   // f32 keys: rebuilt from the bucket and the items, like u32 keys, unless
-  // the input holds a -0 (thrs_hist_joint's flag; +0 and -0 share one image):
-  // then they travel by position like the values.  The chunk's image half
-  // fixes the squeeze's masks (scalars).
-  const bool f32Rebuild = KT == 2 && zeroFlag && load_agent(zeroFlag) == 0u;
+  // whole keys crossed the passes and the input holds a -0 (thrs_hist_joint's
+  // flag; +0 and -0 share one image): then they travel by position like the
+  // values.  From the planes (mode 0) they are always rebuilt, and the chunk
+  // of +0's image takes the zeros' signs from the zero log (at most
+  // kZeroLogCap zeros: thrs_plan_rows takes mode 3 above that).  The chunk's
+  // image half fixes the squeeze's masks (scalars).
+  const bool negZero = KT == 2 && zeroFlag && load_agent(zeroFlag) != 0u;
+  const bool f32Rebuild = KT == 2 && zeroFlag && (plane || !negZero);
   uint32_t hm2 = ~0u, lm2 = 0u, cs2 = 0u;
+  bool zfix = false;
+  uint32_t zlo = 0, zs0 = 0;
+  const uint32_t* negBits = stage + LG::CAP;  // (the rounds' counters: free now)
   if constexpr (KT == 2) {
-    if (sq && sq->on) {
+    const bool sqOn = sq && sq->on;
+    if (sqOn) {
       const int hh = (int)(hiImg >> 31);
       hm2 = (uint32_t)sq->hiM[hh];
       lm2 = (uint32_t)sq->loM[hh];
       cs2 = (uint32_t)sq->cst[hh];
+    }
+    if (plane && negZero && zeroLog) {
+      const uint32_t zimg = sqOn ? (uint32_t)kimg<2>(half_map(km, sq, (int)(hiImg >> 31)), 0u) : kimg<2>(km, 0u);
+      if ((zimg >> 16) == (hiImg >> 16)) {  // (uniform over the workgroup)
+        zfix = true;
+        zlo = zimg & 0xFFFFu;
+        zs0 = pairs_zero_signs<LG>(stage, ch.size, zlo, stage + LG::CAP, zeroLog,
+                                   min(meta[kMetaZeroCount], kZeroLogCap));
+      }
     }
   }
   auto f32_key = [&](uint32_t y) -> uint32_t {
@@ -2296,7 +2351,14 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(LG:
       if (j < KPT) {
         id[j / 2] |= (j * 64 < lim ? (o[jj] & 0xFFFFu) : 0u) << (16 * (j & 1));
         if (KT == 0 && j * 64 < lim) ksrc[j * 64] = kinv_int(km, hiImg | (o[jj] >> 16));
-        if (KT == 2 && f32Rebuild && j * 64 < lim) ksrc[j * 64] = f32_key(hiImg | (o[jj] >> 16));
+        if (KT == 2 && f32Rebuild && j * 64 < lim) {
+          uint32_t key = f32_key(hiImg | (o[jj] >> 16));
+          if (zfix && (o[jj] >> 16) == zlo) {
+            const uint32_t r = w * CHUNK + 64 * j + lane - zs0;
+            key = ((negBits[r >> 5] >> (r & 31)) & 1u) ? 0x80000000u : 0u;
+          }
+          ksrc[j * 64] = key;
+        }
       }
     }
   }
