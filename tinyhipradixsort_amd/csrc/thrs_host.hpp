@@ -170,10 +170,9 @@ inline Plan make_plan(int keyType, int valueBytesOrZero, uint32_t n) {
   // u32 / f32 keys with 4-byte values likewise, up to 2^30 + 2^26 (the u16 planes
   // fill keyOut, the values take valueOut as ever).
   p.hiPlaneOff = p.scratchBytes;
-  if (((keyType == THRS_KEY_U32 || keyType == THRS_KEY_F32) && valueBytesOrZero == 0 &&
-       (uint64_t)n <= (1ull << 31) + (1ull << 25)) ||
-      ((keyType == THRS_KEY_U32 || keyType == THRS_KEY_F32) && valueBytesOrZero == 4 &&
-       (uint64_t)n <= (1ull << 30) + (1ull << 26)))
+  if ((keyType == THRS_KEY_U32 || keyType == THRS_KEY_F32) &&
+      ((valueBytesOrZero == 0 && (uint64_t)n <= (1ull << 31) + (1ull << 25)) ||
+       (valueBytesOrZero == 4 && (uint64_t)n <= (1ull << 30) + (1ull << 26))))
     p.scratchBytes += round_up(n, kAlign);
   return p;
 }
@@ -323,11 +322,12 @@ PathSel select_path(uint32_t n, int startBits, int nPass, const thrs_options& op
   // u32 / f32 local16 with both top-digit passes segmented: the passes carry
   // the keys' IMAGES as planes (thrs_kernels.hpp kCodecSplit / kCodecPlanes):
   // keyOut (4n bytes) = lo u16[n] | lo2 u16[n], the u8 plane hi[n] at the end
-  // of the scratch.  f32: -0 and +0 share one image, so a plan that saw a -0
-  // key (thrs_hist_joint) runs the whole-key passes instead (mode 3)
-  // (u32 / f32 keys + 4-byte values: thrs_local_pairs over the lo2 plane,
-  // the values as they are; f32 with a -0 likewise runs whole keys, mode 3)
-  const bool planes = (KT == 0 || KT == 2) && ((local16) || (VB == 4 && bucket && fullWindow)) && segA &&
+  // of the scratch.  f32: -0 and +0 share one image, so the local sort takes
+  // the zeros' signs from the zero log (thrs_hist_joint), and a plan that saw
+  // a -0 among more zeros than the log holds runs the whole-key passes
+  // instead (mode 3).  u32 / f32 keys + 4-byte values likewise
+  // (thrs_local_pairs over the lo2 plane; the values move as they are).
+  const bool planes = (KT == 0 || KT == 2) && (local16 || (VB == 4 && bucket && fullWindow)) && segA &&
                       opt.planes != THRS_PLANES_OFF && plan.scratchBytes - plan.hiPlaneOff >= (uint64_t)n;
   // the local sort's chunk capacity (a bigger bucket is a big chunk)
   const uint32_t cap = kKV ? LocKV::CAP
@@ -451,8 +451,8 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
   auto kernel = useXb ? kernelXb : (atomicRank ? thrs_pass<KT, VB, ST, true> : thrs_pass<KT, VB, ST, false>);
   auto sk = atomicRank ? thrs_pass_seg<KT, VB, ST, true> : thrs_pass_seg<KT, VB, ST, false>;
   // plane codecs, each top-digit pass one launch with its whole-key body
-  // (thrs_pass_seg2; u32 / f32 keys-only and u32 + 4-byte-value
-  // instantiations only: `planes` is false elsewhere, and the others are
+  // (thrs_pass_seg2; u32 / f32 keys without values or with 4-byte values
+  // only: `planes` is false elsewhere, and the other instantiations are
   // never launched).  The planes codec reads images (identity map): the u32
   // kernel serves both key types.
   constexpr bool kPlanesK = (KT == 0 || KT == 2) && VB == 0;

@@ -2279,8 +2279,8 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(LG:
   uint32_t it[KPT];
   // lo != nullptr: the top-digit passes wrote the images' low 16 bits to the
   // u16 plane lo (kCodecPlanes) -- unless they ran on whole keys (mode 1, big
-  // chunks; mode 3, f32 with a -0) or not at all (mode 2), which leaves the
-  // keys
+  // chunks; mode 3, f32 with a -0 among more zeros than the zero log holds)
+  // or not at all (mode 2), which leaves the keys
   const bool plane = lo && meta[kMetaMode] == 0;
   if (plane) load_run<KPT>(it, lo + ch.start, myOff, ch.size, avail);
   else load_run<KPT>(it, keys + ch.start, myOff, ch.size, avail);

@@ -853,8 +853,8 @@ struct GroupWalk {
 // keyStart / valid: the tile's first key and key count (tile * TILE and
 // min(TILE, n - tile * TILE) except in segmented passes).
 // Key codecs of the pass kernels.  The bucket path for u32 / f32 keys without
-// values (thrs_hybrid.hpp, thrs_local16) and for u32 keys with 4-byte values
-// (thrs_local_pairs; the values travel as they are) carries only what the
+// values (thrs_hybrid.hpp, thrs_local16) and for u32 / f32 keys with 4-byte
+// values (thrs_local_pairs; the values travel as they are) carries only what the
 // next step reads, in two planes instead of the 4-byte keys:
 //   kCodecKeys    keys in, keys out
 //   kCodecSplit   keys in; out: the image's low 16 bits to the u16 plane
@@ -1725,7 +1725,7 @@ __attribute__((amdgpu_waves_per_eu(PassGeom<sizeof(typename KeyTraits<KT>::U), V
 }
 
 // The bucket path's two launches of one top-digit pass in ONE (u32 / f32 keys
-// without values, or u32 keys with 4-byte values, planes on; the values move
+// without values, or with 4-byte values, planes on; the values move
 // the same way in both bodies): the plan's mode picks the body -- mode 0 the
 // key-plane codec CODEC_A (kCodecSplit: keys in, planes out; kCodecPlanes:
 // planes in, a plane out, image space KTA), modes 1 / 3 whole keys
