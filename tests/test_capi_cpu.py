@@ -158,8 +158,8 @@ def test_path_info_matches_the_configs():
     assert info(U32, T.ValueType.U32, 89999999, False)["path"] == "lsd"
     assert info(U32, T.ValueType.U32, 90000000, False)["path"] == "bucket"
     assert info(U32, T.ValueType.U32, 90000000, False)["planes"]
-    assert info(F32, T.ValueType.U32, 149999999, False)["path"] == "lsd"
-    assert info(F32, T.ValueType.U32, 150000000, False)["path"] == "bucket"
+    assert info(F32, T.ValueType.U32, 74999999, False)["path"] == "lsd"
+    assert info(F32, T.ValueType.U32, 75000000, False)["path"] == "bucket"
     # u32 keys-only up to 3 x 2^26: 4096-key chunks (docs/EXPERIMENTS.md row 112)
     assert info(U32, T.ValueType.U32, 160000000, False)["local_cap"] == 4096
     assert info(U32, T.ValueType.U32, 3 << 26, False)["local_cap"] == 4096
@@ -167,10 +167,10 @@ def test_path_info_matches_the_configs():
     assert info(F32, T.ValueType.U32, 160000000, False)["local_cap"] == 9216
     assert info(U32, T.ValueType.U32, 160000000, True)["local_cap"] == 4096   # pairs too (row 115)
     assert info(F32, T.ValueType.U32, 160000000, True)["local_cap"] == 9216
-    assert info(U32, T.ValueType.U32, 49999999, True)["path"] == "lsd"
-    assert info(U32, T.ValueType.U32, 50000000, True)["path"] == "bucket"
-    assert info(F32, T.ValueType.U32, 99999999, True)["path"] == "lsd"
-    assert info(F32, T.ValueType.U32, 100000000, True)["path"] == "bucket"
+    assert info(U32, T.ValueType.U32, 34999999, True)["path"] == "lsd"
+    assert info(U32, T.ValueType.U32, 35000000, True)["path"] == "bucket"
+    assert info(F32, T.ValueType.U32, 59999999, True)["path"] == "lsd"
+    assert info(F32, T.ValueType.U32, 60000000, True)["path"] == "bucket"
     assert info(U64, T.ValueType.U32, (1 << 28) - 1, False)["path"] == "lsd"
     c5 = info(U64, T.ValueType.U64, 1 << 30, True)
     assert (c5["path"], c5["local"], c5["local_cap"]) == ("bucket", "thrs_local_kv", 17408)

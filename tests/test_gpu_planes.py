@@ -113,15 +113,17 @@ def test_u32_keys_default_path_planes_vs_oracle(gpu, n, desc):
 
 @pytest.mark.large
 @pytest.mark.parametrize("desc", [False, True])
-def test_f32_keys_default_path_planes_vs_oracle(gpu, desc):
-    """f32 keys-only at 150M on the default path (planes; the squeeze may go
-    on): raw NaN / Inf / denormal bits and 600 signed zeros, whose signs the
-    zero log restores in input order (getKeyBits maps -0 to +0,
-    kernel.cu:46-69).  Bit-exact against the oracle."""
+@pytest.mark.parametrize("n", [75_000_000, 150_000_000])
+def test_f32_keys_default_path_planes_vs_oracle(gpu, n, desc):
+    """f32 keys-only on the default path at its lower bound (75M) and at 150M
+    (planes; the squeeze may go on): raw NaN / Inf / denormal bits and 600
+    signed zeros, whose signs the zero log restores in input order
+    (getKeyBits maps -0 to +0, kernel.cu:46-69).  Bit-exact against the
+    oracle."""
     import tinyhipradixsort_amd as T
     torch = gpu
-    n = 150_000_000
-    keys = _f32_raw_keys(n, 6200 + int(desc))
+    assert _sorter(O.F32, 0, desc).pathInfo(n, 0, 32, False)["path"] == "bucket"
+    keys = _f32_raw_keys(n, 6200 + int(desc) + n % 7)
     rs = _sorter(O.F32, 0, desc)
     k, _, tmp = _sort_on_gpu(torch, rs, O.F32, keys)
     _expect_planes(rs, T, tmp, O.F32, n, 0.75)
@@ -144,6 +146,7 @@ def test_u32_pairs_default_path_vs_oracle(gpu, desc):
     info = rs.pathInfo(n, 0, 32, True)
     assert (info["path"], info["local"], info["local_cap"], info["planes"]) == ("bucket", "thrs_local_pairs", 4096,
                                                                                 True)
+    assert rs.pathInfo(35_000_000, 0, 32, True)["path"] == "bucket"   # the lower bound (row 129)
     k, v, tmp = _sort_on_gpu(torch, rs, O.U32, keys, vals)
     assert rs.debugBucketMode(tmp, n, True)[0] == 0            # mode 0: the planes ran
     ek, ev = O.lsd_sort(O.U32, keys, vals, 0, 32, desc)
@@ -296,10 +299,10 @@ def test_forced_bucket_f32_pairs_planes_vs_oracle(gpu, geom, zeros, desc):
 @pytest.mark.large
 @pytest.mark.parametrize("zeros", ["plus", "signed", "many"])
 def test_f32_pairs_default_path_vs_oracle(gpu, zeros):
-    """f32 pairs at 100M, the default bucket path's lower bound (planes, the
+    """f32 pairs at 60M, the default bucket path's lower bound (planes, the
     squeeze may go on): keys and values against the oracle."""
     torch = gpu
-    n = 100_000_000
+    n = 60_000_000
     keys = _f32_pairs_keys(n, 7000 + len(zeros), zeros)
     vals = np.arange(n, dtype=np.uint32)
     rs = _sorter(O.F32, 4, False)

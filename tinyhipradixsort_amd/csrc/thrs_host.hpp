@@ -36,12 +36,13 @@ using namespace thrs_dev;
 
 
 constexpr uint64_t kAlign = 256;
-// the bucket path's lower bounds (default path; docs/EXPERIMENTS.md row 87)
-constexpr uint64_t kBucketMinKeys4 = 150000000ull;   // f32 keys without values
+// the bucket path's lower bounds (default path; docs/EXPERIMENTS.md rows 87,
+// 112, 115, 129)
+constexpr uint64_t kBucketMinKeys4 = 75000000ull;    // f32 keys without values (row 129)
 constexpr uint64_t kBucketMinKeysU32 = 90000000ull;  // u32 keys without values (4096-key chunks: row 112)
 constexpr uint64_t kTiny16MaxKeys = 3ull << 26;      // u32 keys-only: 4096-key chunks (Loc16Tiny) up to here
-constexpr uint64_t kBucketMinPairs4 = 100000000ull;  // 4-byte keys with 4-byte values
-constexpr uint64_t kBucketMinPairsU32 = 50000000ull;  // u32 keys + 4-byte values (4096-key chunks: row 115)
+constexpr uint64_t kBucketMinPairs4 = 60000000ull;   // f32 keys with 4-byte values (key planes: row 129)
+constexpr uint64_t kBucketMinPairsU32 = 35000000ull;  // u32 keys + 4-byte values (4096-key chunks, key planes: rows 115, 129)
 constexpr uint64_t kHistOff = 0;                       // u32 [8][256]
 constexpr uint64_t kBaseOff = 8 * 256 * 4;             // u32 [8][256]
 constexpr uint64_t kCounterOff = 2 * 8 * 256 * 4;      // u32 [8]
