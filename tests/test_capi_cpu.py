@@ -82,10 +82,14 @@ def test_temporary_buffer_layout(kt, vt, n):
     # reserved for every n up to 2^31 + 2^25 (a forced bucket path carries
     # the planes too),
     # and room for a big chunk per 4097 keys (the 4096-key local geometry:
-    # 3 KiB of fallback tables each, ~0.75 B per key below 2^28 keys)
+    # 3 KiB of fallback tables each, ~0.75 B per key below 2^28 keys) -- per
+    # 4353 keys for thrs_local_kv's types (8-byte keys, 8/16-byte values: its
+    # 4352-key chunks, 6 KiB each, ~1.4 B per key below 2^28 keys; row 130)
     plane = -(-n // 256) * 256 if kt in (T.KeyType.U32, T.KeyType.F32) and n <= (1 << 31) + (1 << 25) else 0
+    kv = kb == 8 or vb >= 8
     if n >= (1 << 20):
-        assert d.pSumBuffer < (0.4 if kb == 4 else 0.3) * d.keyOutBuffer + plane + (3 << 20) // 2
+        assert d.pSumBuffer < ((0.4 if kb == 4 else 0.3) * d.keyOutBuffer + plane + (3 << 20) // 2
+                               + (1.5 * n if kv else 0))
 
 
 def test_argument_validation_needs_no_device():
@@ -174,6 +178,16 @@ def test_path_info_matches_the_configs():
     assert info(U64, T.ValueType.U32, (1 << 28) - 1, False)["path"] == "lsd"
     c5 = info(U64, T.ValueType.U64, 1 << 30, True)
     assert (c5["path"], c5["local"], c5["local_cap"]) == ("bucket", "thrs_local_kv", 17408)
+    # thrs_local_kv geometries by size (docs/EXPERIMENTS.md row 130): 8704-key
+    # chunks up to 2^29, 4352 up to 3 x 2^26; asked: big / small / tiny16
+    assert info(U64, T.ValueType.U64, (1 << 29) + 1, True, path="bucket")["local_cap"] == 17408
+    assert info(U64, T.ValueType.U64, 1 << 29, True)["local_cap"] == 8704
+    assert info(T.KeyType.F64, T.ValueType.U64, 1 << 29, True)["local_cap"] == 8704
+    assert info(U64, T.ValueType.U128, 1 << 29, True)["local_cap"] == 8704
+    assert info(U64, T.ValueType.U64, 3 << 26, True, path="bucket")["local_cap"] == 4352
+    assert info(U64, T.ValueType.U64, 1 << 20, True, path="bucket", localGeometry="big")["local_cap"] == 17408
+    assert info(U64, T.ValueType.U64, 1 << 20, True, path="bucket", localGeometry="small")["local_cap"] == 8704
+    assert info(U32, T.ValueType.U64, 1 << 30, True, path="bucket", localGeometry="tiny16")["local_cap"] == 4352
     wide = info(U32, T.ValueType.U128, 1 << 30, True)
     assert (wide["path"], wide["local"]) == ("bucket", "thrs_local_kv")
     assert info(U32, T.ValueType.U32, 1 << 20, False)["path"] == "lsd"

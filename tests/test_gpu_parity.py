@@ -460,15 +460,18 @@ def test_full_size_low_entropy(gpu, dist, kt, vb, n):
 @pytest.mark.parametrize("kt,vb", [(O.U32, 8), (O.U32, 16), (O.F32, 4), (O.F32, 8), (O.F32, 16), (O.U64, 4),
                                    (O.U64, 16), (O.F64, 4), (O.F64, 8), (O.F64, 16)])
 @pytest.mark.parametrize("desc", [False, True])
-def test_bucket_wide_payloads_vs_oracle(gpu, kt, vb, desc):
+@pytest.mark.parametrize("geom", ["auto", "small", "big"])
+def test_bucket_wide_payloads_vs_oracle(gpu, kt, vb, desc, geom):
     """f1 (SURVEY.md s8): sortPairs with 8/16-byte payloads (ValueType::U128,
     tinyhipradixsort.hpp:779; K64V128, unittest.cpp:469-487) and f32 pairs on
     the bucket path (forced for every size): thrs_local_kv / thrs_local_pairs
     carry chunk positions and permute values -- and float keys, whose +0 and
     -0 share one image -- through the LDS stage; 16-byte values move whole.
-    Big buckets take the per-bucket fallback."""
+    Big buckets take the per-bucket fallback.  thrs_local_kv in each of its
+    geometries (auto at these sizes = 4352-key chunks, small = 8704, big =
+    17408: sizes around every capacity)."""
     torch = gpu
-    rs = make_sorter(kt, vb, desc, path="bucket")
+    rs = make_sorter(kt, vb, desc, path="bucket", localGeometry=geom)
     kb = O.KEY_BYTES[kt]
     kdt = O.KEY_DTYPE[kt]
     sign = np.array(1 << (8 * kb - 1), dtype=kdt)
@@ -481,7 +484,7 @@ def test_bucket_wide_payloads_vs_oracle(gpu, kt, vb, desc):
     }
     j = 0
     for name, f in dists.items():
-        for n in [1, 100, 17408, 17409, 70001, 300007]:
+        for n in [1, 100, 4352, 4353, 8704, 8705, 17408, 17409, 70001, 300007]:
             j += 1
             keys = f(O.randomize_np(kt, O.splitmix64_stream(5151 * j + vb, n))).astype(kdt)
             vals = (np.arange(n * vb // 4, dtype=np.uint32) * np.uint32(2654435761)).view(
@@ -503,9 +506,10 @@ def test_local_kv_tie_runs(gpu, kt, vb, desc):
     sends the chunk back to input order and six rounds.  Keys here fill 256
     buckets of ~16K keys (near the 17408-key chunk capacity) with those 16
     bits drawn from 4096 values (runs of ~4: the fix-up), from 64 values (runs
-    of ~256: the six rounds), constant, or with whole keys repeated in runs."""
+    of ~256: the six rounds), constant, or with whole keys repeated in runs
+    (the 17408-key geometry, asked: by size this n takes 4352-key chunks)."""
     torch = gpu
-    rs = make_sorter(kt, vb, desc, path="bucket")
+    rs = make_sorter(kt, vb, desc, path="bucket", localGeometry="big")
     kdt = O.KEY_DTYPE[kt]
     n = 1 << 22
     r = O.splitmix64_stream(777 + vb + 2 * desc, 2 * n)

@@ -124,7 +124,7 @@ constexpr uint64_t kBigTileOff = kBigPosOff + round_up_c((kBuckets + 1) * 4, 256
 constexpr uint64_t kZeroLogOff = kBigTileOff + round_up_c((kBuckets + 1) * 4, 256);  // f32: +-0 keys (thrs_hist_joint)
 constexpr uint64_t kHybridBytes = kZeroLogOff + round_up_c(kZeroLogCap * 4, 256);
 // the smallest local-sort capacity (LocSmall): a big chunk holds more keys
-constexpr uint64_t kMinLocalCap = LocSmall::CAP;
+constexpr uint64_t kMinLocalCap = LocKVS::CAP;  // (8-byte keys or 8/16-byte values: the smallest thrs_local_kv chunk)
 // tile ids of the segmented pass: each of the 8 segments adds at most two
 // partial tiles (its first and last: seg_tiles) and rounds its id range up
 // to a multiple of kGroup
@@ -232,6 +232,7 @@ hipError_t allow_lds(F kernel, size_t bytes) {
 struct PathSel {
   bool bucket, fullWindow, smallLocal, local16, wide16, tiny16, tinyPairs, small16, count16, local32, segTop, segA, planes, ranged, useXb;
   int nLow;
+  int kvGeom;  // thrs_local_kv's geometry: 0 LocKV, 1 LocKVM, 2 LocKVS
   uint32_t cap;
 };
 template <int KT, int VB>
@@ -318,6 +319,16 @@ PathSel select_path(uint32_t n, int startBits, int nPass, const thrs_options& op
   // measured slower, docs/EXPERIMENTS.md row 56)
   const bool count16 = local16 && KT == 0 && !wide16 && !small16 && opt.localGeometry == THRS_LOCAL_COUNT16;
   const bool local32 = kKeys4 && bucket && !local16;
+  // thrs_local_kv (8-byte keys, 8/16-byte values): 17408-key chunks from 2^29
+  // keys, 8704 up to there, 4352 up to 3 x 2^26 (mean bucket + ~5 sigma below
+  // the capacity; docs/EXPERIMENTS.md row 130); asked: BIG / SMALL / TINY16
+  const int kvGeom = !kKV                                           ? 0
+                     : opt.localGeometry == THRS_LOCAL_TINY16       ? 2
+                     : opt.localGeometry == THRS_LOCAL_SMALL        ? 1
+                     : opt.localGeometry != THRS_LOCAL_AUTO         ? 0
+                     : nEff <= (double)kTiny16MaxKeys               ? 2
+                     : nEff <= (double)(1ull << 29)                 ? 1
+                                                                    : 0;
   const bool segTop = opt.segmented != THRS_SEG_NONE;
   const bool segA = opt.segmented == THRS_SEG_AUTO;
   // u32 / f32 local16 with both top-digit passes segmented: the passes carry
@@ -331,7 +342,7 @@ PathSel select_path(uint32_t n, int startBits, int nPass, const thrs_options& op
   const bool planes = (KT == 0 || KT == 2) && (local16 || (VB == 4 && bucket && fullWindow)) && segA &&
                       opt.planes != THRS_PLANES_OFF && plan.scratchBytes - plan.hiPlaneOff >= (uint64_t)n;
   // the local sort's chunk capacity (a bigger bucket is a big chunk)
-  const uint32_t cap = kKV ? LocKV::CAP
+  const uint32_t cap = kKV ? (kvGeom == 2 ? LocKVS::CAP : kvGeom == 1 ? LocKVM::CAP : LocKV::CAP)
                        : local16 ? (wide16    ? Loc16Wide::CAP
                                     : tiny16  ? Loc16Tiny::CAP
                                     : small16 ? Loc16Small::CAP
@@ -365,6 +376,7 @@ PathSel select_path(uint32_t n, int startBits, int nPass, const thrs_options& op
   P.ranged = ranged;
   P.useXb = useXb;
   P.nLow = nLow;
+  P.kvGeom = kvGeom;
   P.cap = cap;
   return P;
 }
@@ -477,7 +489,12 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
     if (planes && (allow_lds(sk2Split, lds) != hipSuccess || allow_lds(sk2Planes, lds) != hipSuccess))
       return THRS_ERROR_HIP;
     if constexpr (kKV) {
-      if (allow_lds(atomicRank ? thrs_local_kv<KT, VB, true> : thrs_local_kv<KT, VB, false>, LocKV::LDS) != hipSuccess)
+      if (allow_lds(atomicRank ? thrs_local_kv<KT, VB, true, LocKV> : thrs_local_kv<KT, VB, false, LocKV>,
+                    LocKV::LDS) != hipSuccess ||
+          allow_lds(atomicRank ? thrs_local_kv<KT, VB, true, LocKVM> : thrs_local_kv<KT, VB, false, LocKVM>,
+                    LocKVM::LDS) != hipSuccess ||
+          allow_lds(atomicRank ? thrs_local_kv<KT, VB, true, LocKVS> : thrs_local_kv<KT, VB, false, LocKVS>,
+                    LocKVS::LDS) != hipSuccess)
         return THRS_ERROR_HIP;
     } else if constexpr (kPairs4) {
       if (allow_lds(atomicRank ? thrs_local_pairs<KT, true, LocBig> : thrs_local_pairs<KT, false, LocBig>,
@@ -793,9 +810,15 @@ int run_sort(void* keys, void* vals, uint32_t n, void* tmp, void* keyOutBuf, voi
       const uint64_t maxChunks = !local32 ? kBuckets : std::min<uint64_t>(kBuckets, 256 + 2 * (uint64_t)n);
       const dim3 lgrid((uint32_t)maxChunks);
       if constexpr (kKV) {
-        auto lk = atomicRank ? thrs_local_kv<KT, VB, true> : thrs_local_kv<KT, VB, false>;
-        hipLaunchKernelGGL(lk, lgrid, dim3(LocKV::THREADS), LocKV::LDS, stream, K, V, km, chunkOff, chunkB0, meta,
-                           sqw, g_lstamps);
+        auto launch_kv = [&](auto geom) {
+          using LK = decltype(geom);
+          auto lk = atomicRank ? thrs_local_kv<KT, VB, true, LK> : thrs_local_kv<KT, VB, false, LK>;
+          hipLaunchKernelGGL(lk, lgrid, dim3(LK::THREADS), LK::LDS, stream, K, V, km, chunkOff, chunkB0, meta, sqw,
+                             g_lstamps);
+        };
+        if (P.kvGeom == 2) launch_kv(LocKVS{});
+        else if (P.kvGeom == 1) launch_kv(LocKVM{});
+        else launch_kv(LocKV{});
       } else if constexpr (kPairs4) {
         auto launch_pairs = [&](auto geom) {
           using LG = decltype(geom);

@@ -2411,15 +2411,27 @@ __global__ __launch_bounds__(LG::THREADS) __attribute__((amdgpu_waves_per_eu(LG:
 // keys (+0 and -0 share one image).  u32 / u64 keys are rebuilt from the
 // bucket and the item.  16-byte values are loaded and stored whole (one
 // 16-B access per lane, full lines) and pass the 8-byte stage in two halves.
-// One workgroup of 16 waves x 17 items = 17408 slots: 136 KiB of 8-byte
-// stage + 16 KiB of per-wave counters, one per CU.
+// Geometries (W waves x 17 items, 8 bytes of LDS stage per slot + W x 1 KiB
+// of per-wave counters; 17 items per lane in every one, so the same 128-VGPR
+// budget at four waves per SIMD):
+//   LocKV   16 x 17 = 17408 slots, 152 KiB, one workgroup per CU: buckets of
+//           2^30-key sorts (~16K keys)
+//   LocKVM   8 x 17 =  8704 slots,  76 KiB, two per CU: up to 2^29 keys
+//   LocKVS   4 x 17 =  4352 slots,  38 KiB, four per CU: up to 3 x 2^26 keys
+// (the per-chunk fixed cost -- barriers, scans, counter zeroing -- is what a
+// bucket far below its chunk's capacity pays, and one workgroup per CU
+// exposes every barrier: docs/EXPERIMENTS.md row 130)
 // (8 waves x 34 items, 248 VGPRs at two waves per SIMD: u64 keys 5.76 vs
 // 5.00 ms, C5 shape 7.82 vs 7.29 -- docs/EXPERIMENTS.md row 116)
-struct LocKV {
-  static constexpr int WAVES = 16, KPT = 17, THREADS = 64 * WAVES;
-  static constexpr uint32_t CAP = (uint32_t)THREADS * KPT;  // 17408
+template <int W> struct LocKVG {
+  static constexpr int WAVES = W, KPT = 17, THREADS = 64 * WAVES, WPE = 4;
+  static constexpr uint32_t CAP = (uint32_t)THREADS * KPT;
   static constexpr size_t LDS = (size_t)CAP * 8 + (size_t)WAVES * kBins * 4;
+  static_assert(W >= 4, "the scans take the first 256 threads");
 };
+using LocKV = LocKVG<16>;
+using LocKVM = LocKVG<8>;
+using LocKVS = LocKVG<4>;
 static_assert(LocKV::CAP < 65536, "positions are carried in 16 bits");
 constexpr int kTieScan = 32;  // thrs_local_kv: longest tie run the fix-up walks
 
@@ -2427,10 +2439,10 @@ constexpr int kTieScan = 32;  // thrs_local_kv: longest tie run the fix-up walks
 // of it[] (32- or 64-bit items): count (per-wave counters), scan, lane-ordered
 // rank, scatter into st (sorted order).  Items past nItems of the wave are
 // not there; the counters sit after the 64-bit stage.
-template <bool ATOMIC_RANK, typename Item>
-__device__ __forceinline__ void kv_round(Item (&it)[LocKV::KPT], Item* st, int shift, unsigned char* smem, int nItems) {
-  constexpr int KPT = LocKV::KPT, W = LocKV::WAVES;
-  uint32_t* s_cnt = reinterpret_cast<uint32_t*>(smem + (size_t)LocKV::CAP * 8);  // [W][256]
+template <bool ATOMIC_RANK, typename LK, typename Item>
+__device__ __forceinline__ void kv_round(Item (&it)[LK::KPT], Item* st, int shift, unsigned char* smem, int nItems) {
+  constexpr int KPT = LK::KPT, W = LK::WAVES;
+  uint32_t* s_cnt = reinterpret_cast<uint32_t*>(smem + (size_t)LK::CAP * 8);  // [W][256]
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6);
   uint32_t* cnt = s_cnt + w * kBins;
@@ -2501,12 +2513,12 @@ __device__ __forceinline__ void kv_round(Item (&it)[LocKV::KPT], Item* st, int s
 // 64-bit stage, then six rounds; leaves the sorted items in that stage.  A
 // call (not inlined): the caller's live registers (prefetched values) are
 // saved around it instead of squeezing the six rounds.
-template <bool ATOMIC_RANK>
+template <bool ATOMIC_RANK, typename LK>
 __device__ __noinline__ void kv8_six_rounds(unsigned char* smem, uint32_t size) {
-  constexpr int KPT = LocKV::KPT;
+  constexpr int KPT = LK::KPT;
   constexpr uint32_t CHUNK = 64 * KPT;
   const uint32_t* st = reinterpret_cast<const uint32_t*>(smem);
-  const uint32_t* low = st + LocKV::CAP;
+  const uint32_t* low = st + LK::CAP;
   uint64_t* st64 = reinterpret_cast<uint64_t*>(smem);
   const uint32_t lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t myOff = w * CHUNK + lane;
@@ -2528,7 +2540,7 @@ __device__ __noinline__ void kv8_six_rounds(unsigned char* smem, uint32_t size) 
   for (int j = 0; j < KPT; ++j)
     if (j < nItems) it[j] = (j * 64 < lim) ? st64[myOff + j * 64] : ~(uint64_t)0xFFFF;
   for (int r = 0; r < 6; ++r) {
-    kv_round<ATOMIC_RANK>(it, st64, 16 + 8 * r, smem, nItems);
+    kv_round<ATOMIC_RANK, LK>(it, st64, 16 + 8 * r, smem, nItems);
     if (r < 5) {
 #pragma unroll
       for (int j = 0; j < KPT; ++j)
@@ -2540,7 +2552,7 @@ __device__ __noinline__ void kv8_six_rounds(unsigned char* smem, uint32_t size) 
 // One chunk of thrs_local_kv under the key map km (plain, or the squeeze).
 // A device function, not a lambda handed to with_map: the closure cost the
 // 8-byte-key kernel 12 spilled VGPRs (C5 shape local sort 9.6 -> 11.1 ms).
-template <int KT, int VB, bool ATOMIC_RANK, typename KM>
+template <int KT, int VB, bool ATOMIC_RANK, typename LK, typename KM>
 __device__ __forceinline__ void local_kv_chunk(typename KeyTraits<KT>::U* __restrict__ keys,
                                                typename ValueWord<VB>::T* __restrict__ vals, KM km, uint32_t c,
                                                uint32_t start, uint32_t size, const uint32_t* __restrict__ chunkB0,
@@ -2548,7 +2560,7 @@ __device__ __forceinline__ void local_kv_chunk(typename KeyTraits<KT>::U* __rest
   using U = typename KeyTraits<KT>::U;
   constexpr int KB = (int)sizeof(U);
   using Item = typename std::conditional<KB == 4, uint32_t, uint64_t>::type;
-  constexpr int KPT = LocKV::KPT;
+  constexpr int KPT = LK::KPT;
   constexpr uint32_t CHUNK = 64 * KPT;
   // Float keys are rebuilt from their images like integer keys, except in
   // the chunk holding +0's image: -0 shares it, so that chunk's keys travel
@@ -2570,7 +2582,7 @@ __device__ __forceinline__ void local_kv_chunk(typename KeyTraits<KT>::U* __rest
 
   const bool wfull = nItems == KPT;  // whole wave: no per-item tests (see loc_rounds)
   auto round = [&](auto& it, auto* st, int shift) __attribute__((always_inline)) {
-    kv_round<ATOMIC_RANK>(it, st, shift, smem, nItems);
+    kv_round<ATOMIC_RANK, LK>(it, st, shift, smem, nItems);
   };
   auto reload = [&](auto& it, const auto* st) __attribute__((always_inline)) {  // this lane's slots (past the chunk: padding)
     if (wfull) {
@@ -2629,7 +2641,7 @@ __device__ __forceinline__ void local_kv_chunk(typename KeyTraits<KT>::U* __rest
     // rounds on 64-bit items (the image's low 48 bits << 16 | position), in
     // the same LDS seen as one 64-bit stage.
     uint32_t* st = reinterpret_cast<uint32_t*>(smem);
-    uint32_t* low = st + LocKV::CAP;
+    uint32_t* low = st + LK::CAP;
     uint64_t* st64 = reinterpret_cast<uint64_t*>(smem);
     __shared__ uint32_t s_over;
     if (tid == 0) s_over = 0;  // (the rounds' barriers order this before any set)
@@ -2682,7 +2694,7 @@ __device__ __forceinline__ void local_kv_chunk(typename KeyTraits<KT>::U* __rest
       x = lo;
       y = hi;
     };
-    static_assert(LocKV::KPT <= 64, "one mask bit per slot of the lane");
+    static_assert(LK::KPT <= 64, "one mask bit per slot of the lane");
     uint64_t fm = 0;
     constexpr int FB = 6;
 #pragma unroll
@@ -2716,7 +2728,7 @@ __device__ __forceinline__ void local_kv_chunk(typename KeyTraits<KT>::U* __rest
         sort_run(h, pre);
         return;
       }
-      constexpr uint32_t PMAX = LocKV::CAP - 1;  // (a slot past the run may hold anything)
+      constexpr uint32_t PMAX = LK::CAP - 1;  // (a slot past the run may hold anything)
       const uint32_t l0 = low[w0 & 0xFFFFu], l1 = low[w1 & 0xFFFFu];
       const uint32_t l2 = low[min(w2 & 0xFFFFu, PMAX)], l3 = low[min(w3 & 0xFFFFu, PMAX)];
       uint64_t k0 = ((uint64_t)l0 << 16) | (w0 & 0xFFFFu), k1 = ((uint64_t)l1 << 16) | (w1 & 0xFFFFu);
@@ -2736,7 +2748,7 @@ __device__ __forceinline__ void local_kv_chunk(typename KeyTraits<KT>::U* __rest
     {
       // the wave's runs listed in its (now free) counter words, then taken
       // one per lane: ~2 passes instead of the busiest lane's ~6 runs
-      uint32_t* list = reinterpret_cast<uint32_t*>(smem + (size_t)LocKV::CAP * 8) + w * kBins;
+      uint32_t* list = reinterpret_cast<uint32_t*>(smem + (size_t)LK::CAP * 8) + w * kBins;
       const uint32_t cnt = (uint32_t)__builtin_popcountll(fm);
       const uint32_t incl = wave_incl_scan(cnt, lane);
       const uint32_t R = min(lane63(incl), (uint32_t)kBins);
@@ -2768,7 +2780,7 @@ __device__ __forceinline__ void local_kv_chunk(typename KeyTraits<KT>::U* __rest
 #pragma unroll
       for (int j = 0; j < KPT; ++j) pos[j / 2] |= (it[j] & 0xFFFFu) << (16 * (j & 1));
     } else {
-      kv8_six_rounds<ATOMIC_RANK>(smem, size);  // (a call: its registers are its own)
+      kv8_six_rounds<ATOMIC_RANK, LK>(smem, size);  // (a call: its registers are its own)
 #pragma unroll
       for (int j = 0; j < KPT; ++j) {
         const uint64_t v = st64[myOff + j * 64];
@@ -2852,8 +2864,9 @@ __device__ __forceinline__ void local_kv_chunk(typename KeyTraits<KT>::U* __rest
 #endif
 }
 
-template <int KT, int VB, bool ATOMIC_RANK>
-__global__ __launch_bounds__(LocKV::THREADS) void thrs_local_kv(typename KeyTraits<KT>::U* __restrict__ keys,
+template <int KT, int VB, bool ATOMIC_RANK, typename LK = LocKV>
+__global__ __launch_bounds__(LK::THREADS) __attribute__((amdgpu_waves_per_eu(LK::WPE))) void thrs_local_kv(
+    typename KeyTraits<KT>::U* __restrict__ keys,
                                                                 typename ValueWord<VB>::T* __restrict__ vals,
                                                                 KeyMap<typename KeyTraits<KT>::U> kmh,
                                                                 const uint32_t* __restrict__ chunkOff,
@@ -2867,17 +2880,17 @@ __global__ __launch_bounds__(LocKV::THREADS) void thrs_local_kv(typename KeyTrai
   const uint32_t c = blockIdx.x;
   if (c >= meta[kMetaChunks]) return;
   const uint32_t start = chunkOff[c], size = chunkOff[c + 1] - start;
-  if (size == 0 || size > LocKV::CAP) return;  // big chunk: the per-bucket fallback sorts it
+  if (size == 0 || size > LK::CAP) return;  // big chunk: the per-bucket fallback sorts it
   uint64_t* st = stamps ? stamps + (uint64_t)c * kLocStampSlots : nullptr;
   loc_stamp(st, 0);
   if constexpr (kSqueezable<KT>) {
     if (sq && sq->on) {  // (the squeeze fixed to the chunk's image half: fewer scalars, as thrs_local16)
       const int h = (int)(chunkB0[c] >> 15);
-      local_kv_chunk<KT, VB, ATOMIC_RANK>(keys, vals, half_map(kmh, sq, h), c, start, size, chunkB0, st);
+      local_kv_chunk<KT, VB, ATOMIC_RANK, LK>(keys, vals, half_map(kmh, sq, h), c, start, size, chunkB0, st);
       return;
     }
   }
-  local_kv_chunk<KT, VB, ATOMIC_RANK>(keys, vals, kmh, c, start, size, chunkB0, st);
+  local_kv_chunk<KT, VB, ATOMIC_RANK, LK>(keys, vals, kmh, c, start, size, chunkB0, st);
 }
 
 }  // namespace
