@@ -175,7 +175,15 @@ def test_path_info_matches_the_configs():
     assert info(U32, T.ValueType.U32, 35000000, True)["path"] == "bucket"
     assert info(F32, T.ValueType.U32, 59999999, True)["path"] == "lsd"
     assert info(F32, T.ValueType.U32, 60000000, True)["path"] == "bucket"
-    assert info(U64, T.ValueType.U32, (1 << 28) - 1, False)["path"] == "lsd"
+    # thrs_local_kv's types (row 130)
+    assert info(U64, T.ValueType.U32, 19999999, False)["path"] == "lsd"
+    assert info(U64, T.ValueType.U32, 20000000, False)["path"] == "bucket"
+    assert info(U64, T.ValueType.U64, 11999999, True)["path"] == "lsd"
+    assert info(U64, T.ValueType.U64, 12000000, True)["path"] == "bucket"
+    assert info(T.KeyType.F64, T.ValueType.U64, 14999999, True)["path"] == "lsd"
+    assert info(U64, T.ValueType.U128, 8000000, True)["path"] == "bucket"
+    assert info(U32, T.ValueType.U64, 31999999, True)["path"] == "lsd"
+    assert info(U32, T.ValueType.U128, 25000000, True)["path"] == "bucket"
     c5 = info(U64, T.ValueType.U64, 1 << 30, True)
     assert (c5["path"], c5["local"], c5["local_cap"]) == ("bucket", "thrs_local_kv", 17408)
     # thrs_local_kv geometries by size (docs/EXPERIMENTS.md row 130): 8704-key

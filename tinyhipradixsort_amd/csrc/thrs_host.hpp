@@ -43,6 +43,14 @@ constexpr uint64_t kBucketMinKeysU32 = 90000000ull;  // u32 keys without values 
 constexpr uint64_t kTiny16MaxKeys = 3ull << 26;      // u32 keys-only: 4096-key chunks (Loc16Tiny) up to here
 constexpr uint64_t kBucketMinPairs4 = 60000000ull;   // f32 keys with 4-byte values (key planes: row 129)
 constexpr uint64_t kBucketMinPairsU32 = 35000000ull;  // u32 keys + 4-byte values (4096-key chunks, key planes: rows 115, 129)
+// thrs_local_kv's types (8-byte keys, 8/16-byte values), with its 8704- and
+// 4352-key chunks (row 130)
+constexpr uint64_t kBucketMinK8 = 20000000ull;       // 8-byte keys alone or with 4-byte values
+constexpr uint64_t kBucketMinK8V8 = 12000000ull;     // u64 keys + 8-byte values (f64: 15M)
+constexpr uint64_t kBucketMinF64V8 = 15000000ull;
+constexpr uint64_t kBucketMinK8V16 = 8000000ull;     // 8-byte keys + 16-byte values
+constexpr uint64_t kBucketMinK4V8 = 32000000ull;     // 4-byte keys + 8-byte values
+constexpr uint64_t kBucketMinK4V16 = 25000000ull;    // 4-byte keys + 16-byte values
 constexpr uint64_t kHistOff = 0;                       // u32 [8][256]
 constexpr uint64_t kBaseOff = 8 * 256 * 4;             // u32 [8][256]
 constexpr uint64_t kCounterOff = 2 * 8 * 256 * 4;      // u32 [8]
@@ -255,28 +263,31 @@ PathSel select_path(uint32_t n, int startBits, int nPass, const thrs_options& op
   const bool fullWindow = startBits == 0 && nPass * 8 >= (int)(8 * sizeof(U));
   // Size window of the default (uniform keys: n / 65536 keys per bucket;
   // docs/EXPERIMENTS.md row 29): the local sort costs about the same per chunk
-  // whatever its size, so below ~1.5e8 keys (1e8 pairs, 2^28 for the other
-  // types) the two passes it replaces are cheaper;
+  // whatever its size, so below a measured bound per key / value type (the
+  // kBucketMin* constants) the two passes it replaces are cheaper;
   // above 2^30 + 2^26 the largest of 65536 uniform buckets (mean + ~4.5 sigma)
   // outgrows the chunk capacity and big chunks would take the per-bucket
   // fallback.  THRS_PATH_BUCKET forces the path for any n (tests).
-  // Local geometries: 9216-key chunks for n <= 2^29, 18432 above (17408 for
-  // thrs_local_kv: up to 2^30 + 2^24, the largest uniform bucket ~3 sigma
-  // below the capacity); 4-byte keys-only up to 2^31 + 2^25 in 34816-key
-  // chunks (Loc16Wide).
+  // Local geometries: 9216-key chunks for n <= 2^29, 18432 above (thrs_local_kv:
+  // 4352 / 8704 / 17408, the last up to 2^30 + 2^24, the largest uniform
+  // bucket ~3 sigma below the capacity); 4-byte keys-only up to 2^31 + 2^25
+  // in 34816-key chunks (Loc16Wide).
   const uint64_t nn = n;
   // a key range (the multi-GPU finish: its keys fill the image space, so the
   // buckets are uniform whatever the global distribution) takes the bucket
   // path from 2^27 (C2's 2^30 keys over 8 GPUs; docs/EXPERIMENTS.md row 84)
   const bool rangedReq = opt.keyRange == 1 && fullWindow && !counts;
-  // lower bounds by measurement (docs/EXPERIMENTS.md row 87): 4-byte keys
-  // alone from 150M keys, with 4-byte values from 100M, the rest from 2^28
-  // (the 2^27 bound of a ranged finish is measured for 4-byte keys without
-  // values, the C2 finish; other key / value types keep their own bounds)
+  // lower bounds by measurement (docs/EXPERIMENTS.md rows 87, 112, 115, 129,
+  // 130; the kBucketMin* constants) (the 2^27 bound of a ranged finish is
+  // measured for 4-byte keys without values, the C2 finish; other key /
+  // value types keep their own bounds)
   const uint64_t minN = (rangedReq && kKeys4) ? (1ull << 27)
                         : kKeys4  ? (KT == 0 ? kBucketMinKeysU32 : kBucketMinKeys4)
                         : (KB == 4 && VB == 4) ? (KT == 0 ? kBucketMinPairsU32 : kBucketMinPairs4)
-                                               : (1ull << 28);
+                        : KB == 4 ? (VB == 8 ? kBucketMinK4V8 : kBucketMinK4V16)
+                        : VB == 16 ? kBucketMinK8V16
+                        : VB == 8 ? (KT == 3 ? kBucketMinF64V8 : kBucketMinK8V8)
+                                  : kBucketMinK8;
   const bool sizeOk = nn >= minN && nn <= (1ull << 30) + (kKV ? (1ull << 24) : (1ull << 26));
   const bool wideOk = kKeys4 && fullWindow && nn > (1ull << 30) + (1ull << 26) && nn <= (1ull << 31) + (1ull << 25);
   // the local geometry follows the keys per USED bucket: a range whose span
