@@ -276,7 +276,7 @@ def test_bucket_finish_with_key_range(gpu, tmp_path, world, kt, vb, n):
     balanced and the local sort -- not the per-bucket fallback -- finishes
     the sort.  World 2 over gloo with real HIP steps (u32 keys, 2^27 .. 2^29
     per rank: 2^27 is C2's per-rank share at 8 GPUs, VERDICT r03 item 6;
-    u64 + u64 at 2^27 stays on the LSD path, below its measured bound),
+    u64 + u64 at 2^27 too: its measured bound is 12M keys, row 130),
     world 1 over RCCL (u32 at 2^27; the C5 shape at 2^28: u64 keys + u64
     index payload)."""
     import json
@@ -288,8 +288,9 @@ def test_bucket_finish_with_key_range(gpu, tmp_path, world, kt, vb, n):
     res = [json.load(open(tmp_path / f"r{r}.json")) for r in range(world)]
     assert sum(r["n_out"] for r in res) == world * n
     # the ranged finish's bucket-path bound is 2^27 for 4-byte keys without
-    # values only (the measured C2 shape); other types keep 2^28
-    bucket = (O.KEY_BYTES[kt] == 4 and vb == 0) or n >= (1 << 28)
+    # values (the measured C2 shape); other types keep their own
+    # (u64 + u64: 12M keys, docs/EXPERIMENTS.md row 130)
+    bucket = (O.KEY_BYTES[kt] == 4 and vb == 0) or n >= 12_000_000
     for r in res:
         assert r["unsorted"] == 0, r
         if bucket:
