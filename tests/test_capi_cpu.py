@@ -170,7 +170,9 @@ def test_path_info_matches_the_configs():
     assert info(U32, T.ValueType.U32, (3 << 26) + 1, False)["local_cap"] == 9216
     assert info(F32, T.ValueType.U32, 160000000, False)["local_cap"] == 9216
     assert info(U32, T.ValueType.U32, 160000000, True)["local_cap"] == 4096   # pairs too (row 115)
-    assert info(F32, T.ValueType.U32, 160000000, True)["local_cap"] == 9216
+    assert info(F32, T.ValueType.U32, 160000000, True)["local_cap"] == 4096   # f32 pairs too (row 131)
+    assert info(F32, T.ValueType.U32, 1 << 27, False)["local_cap"] == 4096      # f32 keys up to 2^27 (row 131)
+    assert info(F32, T.ValueType.U32, (1 << 27) + 1, False)["local_cap"] == 9216
     assert info(U32, T.ValueType.U32, 34999999, True)["path"] == "lsd"
     assert info(U32, T.ValueType.U32, 35000000, True)["path"] == "bucket"
     assert info(F32, T.ValueType.U32, 59999999, True)["path"] == "lsd"

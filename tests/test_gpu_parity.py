@@ -781,7 +781,7 @@ def test_squeeze_vs_oracle(gpu, kt, vb, desc, fits):
     kb = O.KEY_BYTES[kt]
     kdt = O.KEY_DTYPE[kt]
     n = (1 << 20) + 333
-    kv = kb == 8 or vb >= 8          # 17408-key chunks (thrs_local_kv, asked), else 9216 (n <= 2^29)
+    kv = kb == 8 or vb >= 8          # 17408-key chunks (thrs_local_kv), else 9216 (both asked)
     varying = (5 if kv else 6) if fits else 3
     keys = _squeeze_case_keys(kt, n, desc, varying, 71 * kb + vb + (5 if desc else 0) + (3 if fits else 0))
     vals = None
@@ -789,7 +789,7 @@ def test_squeeze_vs_oracle(gpu, kt, vb, desc, fits):
         vals = (np.arange(n * vb // 4, dtype=np.uint32) * np.uint32(2654435761)).view(
             {4: np.uint32, 8: np.uint64}[vb])
     ek, ev = O.lsd_sort(kt, keys, vals, 0, 8 * kb, desc)
-    rs = make_sorter(kt, vb, desc, path="bucket", **({"localGeometry": "big"} if kv else {}))
+    rs = make_sorter(kt, vb, desc, path="bucket", localGeometry="big" if kv else "small")
     (mode, big), k, v = _mode_after(torch, rs, keys, vals, kt, vb)
     assert np.array_equal(k.view(kdt), ek.view(kdt)), (mode, big)
     if vb:

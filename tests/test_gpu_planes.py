@@ -309,7 +309,10 @@ def test_f32_pairs_default_path_vs_oracle(gpu, zeros):
     info = rs.pathInfo(n, 0, 32, True)
     assert (info["path"], info["local"], info["planes"]) == ("bucket", "thrs_local_pairs", True)
     k, v, tmp = _sort_on_gpu(torch, rs, O.F32, keys, vals)
-    assert rs.debugBucketMode(tmp, n, True)[0] == _F32_PAIRS_MODE[zeros]
+    mode = rs.debugBucketMode(tmp, n, True)[0]
+    # (3000 zeros overflow the zero's 4096-key chunk at this size: mode 1,
+    # big chunks, which also runs whole keys)
+    assert mode == _F32_PAIRS_MODE[zeros] or (zeros == "many" and mode == 1), mode
     ek, ev = O.lsd_sort(O.F32, keys, vals, 0, 32, False)
     assert np.array_equal(k, ek)
     assert np.array_equal(v, ev)

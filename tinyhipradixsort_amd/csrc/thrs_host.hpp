@@ -40,7 +40,8 @@ constexpr uint64_t kAlign = 256;
 // 112, 115, 129)
 constexpr uint64_t kBucketMinKeys4 = 75000000ull;    // f32 keys without values (row 129)
 constexpr uint64_t kBucketMinKeysU32 = 90000000ull;  // u32 keys without values (4096-key chunks: row 112)
-constexpr uint64_t kTiny16MaxKeys = 3ull << 26;      // u32 keys-only: 4096-key chunks (Loc16Tiny) up to here
+constexpr uint64_t kTiny16MaxKeys = 3ull << 26;      // u32 keys-only, 4-byte pairs: 4096-key chunks up to here
+constexpr uint64_t kTiny16MaxKeysF32 = 1ull << 27;   // f32 keys-only: 4096-key chunks up to here (row 131)
 constexpr uint64_t kBucketMinPairs4 = 60000000ull;   // f32 keys with 4-byte values (key planes: row 129)
 constexpr uint64_t kBucketMinPairsU32 = 35000000ull;  // u32 keys + 4-byte values (4096-key chunks, key planes: rows 115, 129)
 // thrs_local_kv's types (8-byte keys, 8/16-byte values), with its 8704- and
@@ -317,15 +318,17 @@ PathSel select_path(uint32_t n, int startBits, int nPass, const thrs_options& op
   // 9216-key chunks for n <= 2^29 (or asked: SMALL)
   const bool wide16 = local16 && (opt.localGeometry == THRS_LOCAL_WIDE16 ||
                                   (opt.localGeometry == THRS_LOCAL_AUTO && nEff > (double)((1ull << 30) + (1ull << 26))));
-  // ... in 4096-key chunks for u32 up to 3 x 2^26 keys (or asked: TINY16)
+  // ... in 4096-key chunks for u32 up to 3 x 2^26 keys, f32 up to 2^27 (or
+  // asked: TINY16; docs/EXPERIMENTS.md rows 112, 131)
   const bool tiny16 = local16 && !wide16 &&
                       (opt.localGeometry == THRS_LOCAL_TINY16 ||
-                       (opt.localGeometry == THRS_LOCAL_AUTO && KT == 0 && nEff <= (double)kTiny16MaxKeys));
+                       (opt.localGeometry == THRS_LOCAL_AUTO &&
+                        nEff <= (double)(KT == 0 ? kTiny16MaxKeys : kTiny16MaxKeysF32)));
   const bool small16 = local16 && !wide16 && !tiny16 && smallLocal;
   // u32 keys + 4-byte values likewise (thrs_local_pairs in LocTiny chunks)
   const bool tinyPairs = KB == 4 && VB == 4 && bucket && fullWindow &&
                          (opt.localGeometry == THRS_LOCAL_TINY16 ||
-                          (opt.localGeometry == THRS_LOCAL_AUTO && KT == 0 && nEff <= (double)kTiny16MaxKeys));
+                          (opt.localGeometry == THRS_LOCAL_AUTO && nEff <= (double)kTiny16MaxKeys));
   // ... u32 only: sorted by counting (thrs_local_count16) when asked (it
   // measured slower, docs/EXPERIMENTS.md row 56)
   const bool count16 = local16 && KT == 0 && !wide16 && !small16 && opt.localGeometry == THRS_LOCAL_COUNT16;
