@@ -2220,7 +2220,7 @@ __device__ __forceinline__ void pairs_items(uint32_t (&it)[KPT], KM km, uint32_t
 // 16 bits << 16 | position); leaves the signs in negBits[kZeroLogCap / 32] and
 // returns the zeros' first slot.  Every thread of the workgroup calls it.
 template <typename LG>
-__device__ __attribute__((noinline)) uint32_t pairs_zero_signs(const uint32_t* stage, uint32_t size, uint32_t zlo,
+__device__ __forceinline__ uint32_t pairs_zero_signs(const uint32_t* stage, uint32_t size, uint32_t zlo,
                                                                uint32_t* negBits, const uint32_t* __restrict__ zlog,
                                                                uint32_t z) {
   constexpr uint32_t CHUNK = 64 * LG::KPT;
