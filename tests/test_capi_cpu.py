@@ -159,11 +159,11 @@ def test_path_info_matches_the_configs():
     assert (c4["path"], c4["local"], c4["planes"], c4["local_cap"]) == ("bucket", "thrs_local16", True, 9216)
     assert c4["min_bytes"] == (4 + 7 + 5 + 6) * (1 << 28)
     # the lower bounds of the default's bucket window (docs/EXPERIMENTS.md row 87)
-    assert info(U32, T.ValueType.U32, 89999999, False)["path"] == "lsd"
-    assert info(U32, T.ValueType.U32, 90000000, False)["path"] == "bucket"
-    assert info(U32, T.ValueType.U32, 90000000, False)["planes"]
-    assert info(F32, T.ValueType.U32, 74999999, False)["path"] == "lsd"
-    assert info(F32, T.ValueType.U32, 75000000, False)["path"] == "bucket"
+    assert info(U32, T.ValueType.U32, 59999999, False)["path"] == "lsd"
+    assert info(U32, T.ValueType.U32, 60000000, False)["path"] == "bucket"
+    assert info(U32, T.ValueType.U32, 60000000, False)["planes"]
+    assert info(F32, T.ValueType.U32, 39999999, False)["path"] == "lsd"
+    assert info(F32, T.ValueType.U32, 40000000, False)["path"] == "bucket"
     # u32 keys-only up to 3 x 2^26: 4096-key chunks (docs/EXPERIMENTS.md row 112)
     assert info(U32, T.ValueType.U32, 160000000, False)["local_cap"] == 4096
     assert info(U32, T.ValueType.U32, 3 << 26, False)["local_cap"] == 4096
@@ -175,8 +175,8 @@ def test_path_info_matches_the_configs():
     assert info(F32, T.ValueType.U32, (1 << 27) + 1, False)["local_cap"] == 9216
     assert info(U32, T.ValueType.U32, 34999999, True)["path"] == "lsd"
     assert info(U32, T.ValueType.U32, 35000000, True)["path"] == "bucket"
-    assert info(F32, T.ValueType.U32, 59999999, True)["path"] == "lsd"
-    assert info(F32, T.ValueType.U32, 60000000, True)["path"] == "bucket"
+    assert info(F32, T.ValueType.U32, 31999999, True)["path"] == "lsd"
+    assert info(F32, T.ValueType.U32, 32000000, True)["path"] == "bucket"
     # thrs_local_kv's types (row 130)
     assert info(U64, T.ValueType.U32, 19999999, False)["path"] == "lsd"
     assert info(U64, T.ValueType.U32, 20000000, False)["path"] == "bucket"

@@ -9,7 +9,7 @@ reference's own timed shape (160M keys, unittest.cpp:490-571) all run these
 codecs, so they are compared here with the oracle's pass-by-pass restatement
 of RadixSort::sort (tinyhipradixsort.hpp:854-944), key for key:
 
-* the DEFAULT path at the sizes where it runs them: u32 keys at 90,000,000 and
+* the DEFAULT path at the sizes where it runs them: u32 keys at 60,000,000 and
   160,000,000 (4096-key chunks, Loc16Tiny) and 2^28 (9216-key chunks), f32
   keys at 150,000,000 with raw NaN / Inf / denormal bits and signed zeros,
   u32 pairs at 160M (LocTiny; pairs carry whole keys);
@@ -91,7 +91,7 @@ def _expect_planes(rs, T, tmp, kt, n, min_frac):
 
 @pytest.mark.large
 @pytest.mark.parametrize("desc", [False, True])
-@pytest.mark.parametrize("n", [90_000_000, 160_000_000, 1 << 28])
+@pytest.mark.parametrize("n", [60_000_000, 160_000_000, 1 << 28])
 def test_u32_keys_default_path_planes_vs_oracle(gpu, n, desc):
     """u32 keys-only on the DEFAULT path at the sizes where it takes the
     planes: 4096-key chunks (<= 3 x 2^26 keys; 160M is the reference's own
@@ -113,9 +113,9 @@ def test_u32_keys_default_path_planes_vs_oracle(gpu, n, desc):
 
 @pytest.mark.large
 @pytest.mark.parametrize("desc", [False, True])
-@pytest.mark.parametrize("n", [75_000_000, 150_000_000])
+@pytest.mark.parametrize("n", [40_000_000, 150_000_000])
 def test_f32_keys_default_path_planes_vs_oracle(gpu, n, desc):
-    """f32 keys-only on the default path at its lower bound (75M) and at 150M
+    """f32 keys-only on the default path at its lower bound (40M) and at 150M
     (planes; the squeeze may go on): raw NaN / Inf / denormal bits and 600
     signed zeros, whose signs the zero log restores in input order
     (getKeyBits maps -0 to +0, kernel.cu:46-69).  Bit-exact against the
@@ -299,10 +299,10 @@ def test_forced_bucket_f32_pairs_planes_vs_oracle(gpu, geom, zeros, desc):
 @pytest.mark.large
 @pytest.mark.parametrize("zeros", ["plus", "signed", "many"])
 def test_f32_pairs_default_path_vs_oracle(gpu, zeros):
-    """f32 pairs at 60M, the default bucket path's lower bound (planes, the
+    """f32 pairs at 32M, the default bucket path's lower bound (planes, the
     squeeze may go on): keys and values against the oracle."""
     torch = gpu
-    n = 60_000_000
+    n = 32_000_000
     keys = _f32_pairs_keys(n, 7000 + len(zeros), zeros)
     vals = np.arange(n, dtype=np.uint32)
     rs = _sorter(O.F32, 4, False)

@@ -38,11 +38,11 @@ using namespace thrs_dev;
 constexpr uint64_t kAlign = 256;
 // the bucket path's lower bounds (default path; docs/EXPERIMENTS.md rows 87,
 // 112, 115, 129)
-constexpr uint64_t kBucketMinKeys4 = 75000000ull;    // f32 keys without values (row 129)
-constexpr uint64_t kBucketMinKeysU32 = 90000000ull;  // u32 keys without values (4096-key chunks: row 112)
+constexpr uint64_t kBucketMinKeys4 = 40000000ull;    // f32 keys without values (rows 129, 132)
+constexpr uint64_t kBucketMinKeysU32 = 60000000ull;  // u32 keys without values (4096-key chunks: rows 112, 132)
 constexpr uint64_t kTiny16MaxKeys = 3ull << 26;      // u32 keys-only, 4-byte pairs: 4096-key chunks up to here
 constexpr uint64_t kTiny16MaxKeysF32 = 1ull << 27;   // f32 keys-only: 4096-key chunks up to here (row 131)
-constexpr uint64_t kBucketMinPairs4 = 60000000ull;   // f32 keys with 4-byte values (key planes: row 129)
+constexpr uint64_t kBucketMinPairs4 = 32000000ull;   // f32 keys with 4-byte values (key planes, 4096-key chunks: rows 129, 132)
 constexpr uint64_t kBucketMinPairsU32 = 35000000ull;  // u32 keys + 4-byte values (4096-key chunks, key planes: rows 115, 129)
 // thrs_local_kv's types (8-byte keys, 8/16-byte values), with its 8704- and
 // 4352-key chunks (row 130)
