@@ -169,8 +169,9 @@ def test_cpp_port_with_claim_mode_forced(gpu, claims):
 @pytest.mark.parametrize("path", ["bucket", "lsd"])
 def test_cpp_port_with_path_forced(gpu, path):
     """The UTEST matrix with the 3-HBM-pass path (bucket passes + local LDS
-    sort, thrs_hybrid.hpp) forced on for every size (by default it runs for n
-    in [2^28, 2^30 + 2^26]) and off (plain LSD passes)."""
+    sort, thrs_hybrid.hpp) forced on for every size (by default it runs from a
+    measured bound per key / value type, thrs_host.hpp kBucketMin*) and off
+    (plain LSD passes)."""
     exe = os.path.join(ROOT, "tests", "cpp", "unittest_thrs")
     r = subprocess.run([exe, f"--path={path}"], capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
@@ -184,7 +185,7 @@ def test_cpp_port_with_path_forced(gpu, path):
 @pytest.mark.parametrize("desc", [False, True])
 def test_hybrid_paths_vs_oracle(gpu, kt, desc, geom, seg):
     """4-byte keys-only sorts with >= 3 digits take the hybrid path (forced
-    here for every size; by default it runs for n in [2^28, 2^30 + 2^26]): chunked
+    here for every size; by default from 60M u32 / 40M f32 keys): chunked
     local sort (single- and multi-bucket chunks), and the gated fallback to
     plain LSD when one bucket exceeds the local capacity (18432 keys) --
     including an odd number of low passes (window of 3 digits: gated copy)."""
@@ -263,9 +264,9 @@ def test_hybrid_pairs_vs_oracle(gpu, kt, desc, geom):
 @pytest.mark.parametrize("desc", [False, True])
 def test_bucket64_vs_oracle(gpu, kt, vb, desc):
     """8-byte keys (with or without 8-byte values) over the whole key take the
-    bucket path (forced here for every size; by default n in [2^28, 2^30 +
-    2^24]): two device passes on the top 16 bits, six in-LDS rounds per
-    bucket (thrs_local64), u64 keys rebuilt / f64 keys and values permuted by
+    bucket path (forced here for every size; by default n in [12M-20M, 2^30 +
+    2^24]): two device passes on the top 16 bits, the in-LDS sort per bucket
+    (thrs_local_kv), u64 keys rebuilt / f64 keys and values permuted by
     carried positions; a bucket above 17408 keys takes the LSD fallback."""
     torch = gpu
     rs = make_sorter(kt, vb, desc, path="bucket")
